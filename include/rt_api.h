@@ -1,0 +1,201 @@
+/*
+ * rt_api.h -- C ABI of the MI355X-native render path for erichgess/rust_tracer.
+ *
+ * This is the drop-in boundary.  It replaces the reference's Rust seam
+ *
+ *     pub fn render(camera: &Camera, scene: &Scene, buffer: &mut RenderBuffer, depth: usize)
+ *                                                                    (src/render.rs:31-38)
+ *
+ * with a flat, insertion-ordered scene description (what src/scene/mod.rs:40-52
+ * `add_shape` / `add_light` / `set_ambient` accumulate), a camera record
+ * (src/render.rs:155-176) and caller-owned output buffers.  Everything is plain C:
+ * pointers, sizes, int32 status codes.  No torch or HIP types appear in the
+ * signatures; streams are passed as opaque `void*` (a hipStream_t).
+ *
+ * Conventions
+ *  - All entry points return rt_status (0 = RT_OK).  The reference panics instead
+ *    (Matrix::invert "Singular Matrix", src/math/matrix.rs:116-117); here the panic
+ *    becomes RT_ERR_SINGULAR_MATRIX from rt_scene_create.
+ *  - The library owns device memory; the caller owns host buffers.
+ *  - An rt_scene handle is not safe for concurrent rt_render calls (mirrors the
+ *    reference's !Sync Rc<RefCell<..>> scene).
+ *  - Output is row-major [v][u][rgb] float32 (image order).  The reference buffer is
+ *    column-major `buf[u][v]` (src/render.rs:5-19); INTEGRATION.md shows the
+ *    transposing copy a Rust binding does.
+ */
+#ifndef RT_API_H
+#define RT_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_API_VERSION 1
+
+typedef int32_t rt_status;
+enum {
+    RT_OK = 0,
+    RT_ERR_INVALID_ARG = 1,
+    RT_ERR_SINGULAR_MATRIX = 2,  /* src/math/matrix.rs:116-117 panic("Singular Matrix") */
+    RT_ERR_UNSUPPORTED = 3,      /* e.g. depth above RT_MAX_DEPTH */
+    RT_ERR_NO_DEVICE = 4,        /* no HIP device / HIP runtime failure at init */
+    RT_ERR_HIP = 5,              /* a HIP runtime call failed */
+    RT_ERR_OUT_OF_MEMORY = 6,
+    RT_ERR_BAD_MATERIAL = 7      /* material index out of range */
+};
+
+/* Largest `depth` the device path accepts (the DFS continuation stack has
+ * RT_MAX_DEPTH-1 frames).  The reference recursion is unbounded. */
+#define RT_MAX_DEPTH 64
+
+/* ---------------------------------------------------------------- scene description */
+
+typedef struct rt_color {
+    float r, g, b;                 /* src/scene/color.rs:2-6 */
+} rt_color;
+
+/* Texture programs.  The reference stores host fn pointers (`ColorFun`,
+ * src/scene/material.rs:3) -- a GPU needs a closed set.  Every texture used by the
+ * reference's scenes is one of these:
+ *   RT_TEX_CONST         -> `color`                          (Phong fields; dim_white
+ *                                                             = 0.1*WHITE, my_scene.rs:11-13)
+ *   RT_TEX_CHECKERBOARD  -> my_scene.rs:26-43 (WHITE / 0.5*WHITE), `color` unused      */
+enum { RT_TEX_CONST = 0, RT_TEX_CHECKERBOARD = 1 };
+typedef struct rt_texture {
+    int32_t kind;
+    rt_color color;
+} rt_texture;
+
+/* Materials (src/scene/material.rs).  PHONG uses the three CONST colours
+ * (`Phong::new(ambient, diffuse, specular, power, reflectivity, refraction_index)`,
+ * material.rs:35-51); TEXTURE_PHONG evaluates the texture programs at the hit's
+ * texture coordinates (material.rs:113-130, 144-186). */
+enum { RT_MAT_PHONG = 0, RT_MAT_TEXTURE_PHONG = 1 };
+typedef struct rt_material {
+    int32_t kind;
+    rt_texture ambient;
+    rt_texture diffuse;
+    rt_texture specular;
+    float power;
+    float reflectivity;
+    float refraction_index;
+} rt_material;
+
+/* Shapes, in Scene::add_shape order (that order is the nearest-hit tie-break,
+ * src/scene/mod.rs:98-116).
+ *   SPHERE   : unit sphere at the origin + `transform` (sphere.rs:57-103)
+ *   PLANE    : data[0..3] origin, data[3..6] normal (plane.rs:22-42) + `transform`
+ *   TRIANGLE : data[0..9] = v0, v1, v2 (triangle.rs:16-39); `transform` is stored
+ *              but, as in the reference, ignored by intersect (triangle.rs:51-99)
+ *   CUBE     : unit cube of 12 triangles (cube.rs:21-77) + `transform`
+ * `transform` is the row-major forward matrix handed to `set_transform`
+ * (matrix.rs:16-20; identity when never set).  The library inverts it with the
+ * reference's Gauss-Jordan (matrix.rs:99-153). */
+enum { RT_SHAPE_SPHERE = 0, RT_SHAPE_PLANE = 1, RT_SHAPE_TRIANGLE = 2, RT_SHAPE_CUBE = 3 };
+typedef struct rt_shape {
+    int32_t kind;
+    int32_t material;              /* index into rt_scene_desc.materials */
+    float transform[16];           /* row-major 4x4 */
+    float data[9];
+} rt_shape;
+
+/* Lights (src/scene/mod.rs:169-246). */
+enum { RT_LIGHT_POINT = 0, RT_LIGHT_AMBIENT = 1 };
+typedef struct rt_light {
+    int32_t kind;
+    float pos[3];                  /* POINT only */
+    rt_color color;
+} rt_light;
+
+typedef struct rt_scene_desc {
+    uint32_t n_materials;
+    const rt_material* materials;
+    uint32_t n_shapes;
+    const rt_shape* shapes;
+    uint32_t n_lights;
+    const rt_light* lights;
+    rt_color ambient;              /* Scene::set_ambient (mod.rs:50-52) */
+} rt_scene_desc;
+
+/* src/render.rs:155-176.  Camera::new(x_res, y_res) is origin (0,0,-8), window [-3,3]^2. */
+typedef struct rt_camera {
+    float origin[3];
+    float x_min, x_max, y_min, y_max;
+    uint32_t x_res, y_res;
+} rt_camera;
+
+/* ---------------------------------------------------------------- render options */
+
+typedef struct rt_counters {
+    uint64_t node_rays;     /* scene scans for primary/reflected/refracted rays
+                               (Scene::intersect from trace_ray, render.rs:47) */
+    uint64_t shadow_rays;   /* scene scans for point-light shadow rays (mod.rs:193) */
+    uint64_t pixels;        /* pixels rendered by this call */
+} rt_counters;
+
+typedef struct rt_render_opts {
+    int32_t device;          /* HIP device ordinal; -1 = current device */
+    rt_counters* counters;   /* optional out: ray counters of this call */
+    float* kernel_ms;        /* optional out: device time of the render kernel (HIP events) */
+} rt_render_opts;
+
+/* ---------------------------------------------------------------- entry points */
+
+typedef struct rt_scene rt_scene;
+
+/* Copies and flattens `desc`, runs the host-side preprocessing the reference does at
+ * scene build time (Matrix::inverse, Plane axes, Triangle normals, Cube triangles) and
+ * uploads the scene to `device` (-1 = current). */
+rt_status rt_scene_create(const rt_scene_desc* desc, int32_t device, rt_scene** out);
+rt_status rt_scene_destroy(rt_scene* scene);
+
+/* render.rs:31-38: fill `rgb` (h*w*3 float, row-major [v][u][c]) with
+ * trace_ray(get_ray(u, v), depth) for every pixel.  `rgb8` (optional, may be NULL)
+ * receives Color::as_u8 (color.rs:43-46) of every pixel, row-major RGB8. */
+rt_status rt_render(const rt_scene* scene, const rt_camera* camera, uint32_t depth,
+                    const rt_render_opts* opts, float* rgb, uint8_t* rgb8);
+
+/* Device-resident variant used by the multi-GPU driver: renders this rank's share of
+ * the frame into device memory on `stream`, asynchronously.
+ * Rows are dealt in bands of `band_rows`: band b (rows [b*band_rows, (b+1)*band_rows))
+ * belongs to rank b % world.  This rank's bands are written back to back into
+ * `d_rgb` (band-major, rows of x_res*3 floats), rt_band_rows_per_rank() rows in all
+ * (the last bands are padded; padded rows are written as 0).
+ * `d_counters` (optional) is a device array of 3 uint64 that the kernel ADDS
+ * node_rays, shadow_rays, pixels into. */
+rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* camera,
+                                uint32_t depth, uint32_t band_rows, uint32_t rank,
+                                uint32_t world, float* d_rgb, uint64_t* d_counters,
+                                void* stream);
+
+/* Number of rows (including padding) a rank's band buffer holds. */
+uint32_t rt_band_rows_per_rank(uint32_t y_res, uint32_t band_rows, uint32_t world);
+
+/* Scatter the `world` gathered band buffers (rank-major: world * rows_per_rank rows of
+ * x_res*3 floats) into a row-major frame `d_frame` (y_res rows), on `stream`. */
+rt_status rt_unpermute_bands_async(const float* d_gathered, uint32_t x_res, uint32_t y_res,
+                                   uint32_t band_rows, uint32_t world, float* d_frame,
+                                   void* stream);
+
+/* Color::as_u8 (color.rs:43-46) of a row-major float frame, on the device. */
+rt_status rt_quantize_u8_async(const float* d_rgb, size_t n_values, uint8_t* d_rgb8,
+                               void* stream);
+
+/* Algorithmic f32 operation count of one scene scan:
+ * sphere 57, triangle 52, cube 33 + 12*52, plane 49 per ray-primitive test. */
+uint64_t rt_scene_flops_per_scan(const rt_scene* scene);
+
+/* Bytes of the flattened device scene (for the HBM-traffic accounting). */
+uint64_t rt_scene_device_bytes(const rt_scene* scene);
+
+const char* rt_status_str(rt_status status);
+int32_t rt_api_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_API_H */

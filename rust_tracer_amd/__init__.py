@@ -1,0 +1,291 @@
+"""rust_tracer_amd -- MI355X-native render path of erichgess/rust_tracer.
+
+Python face of the C ABI in include/rt_api.h (librt_hip.so, HIP kernels for gfx950).
+It mirrors the reference's seam ``render(camera, scene, buffer, depth)``
+(src/render.rs:31) and the scene builders of src/my_scene.rs / src/scene.  There is no
+CPU render path here: without the built library every call raises.
+"""
+import ctypes as C
+import math
+
+import numpy as np
+
+from . import abi
+from .abi import (RT_LIGHT_AMBIENT, RT_LIGHT_POINT, RT_MAT_PHONG, RT_MAT_TEXTURE_PHONG,
+                  RT_SHAPE_CUBE, RT_SHAPE_PLANE, RT_SHAPE_SPHERE, RT_SHAPE_TRIANGLE,
+                  RT_TEX_CHECKERBOARD, RT_TEX_CONST, RtError, camera, check, lib)
+
+__all__ = ["Matrix", "SceneDesc", "DeviceScene", "camera", "render", "RtError", "lib"]
+
+F32 = np.float32
+PI_F = F32(math.pi)
+
+
+class Matrix:
+    """Row-major 4x4 f32 (src/math/matrix.rs) with the reference's exact f32 evaluation
+    order: products accumulate left to right from 0. (matrix.rs:68-86)."""
+
+    def __init__(self, rows=None):
+        self.m = [[F32(0)] * 4 for _ in range(4)] if rows is None else \
+            [[F32(v) for v in r] for r in rows]
+
+    @staticmethod
+    def identity():
+        return Matrix([[1 if i == j else 0 for j in range(4)] for i in range(4)])
+
+    @staticmethod
+    def scale(x, y, z):
+        m = Matrix.identity()
+        m.m[0][0], m.m[1][1], m.m[2][2] = F32(x), F32(y), F32(z)
+        return m
+
+    @staticmethod
+    def translate(x, y, z):
+        m = Matrix.identity()
+        m.m[0][3], m.m[1][3], m.m[2][3] = F32(x), F32(y), F32(z)
+        return m
+
+    @staticmethod
+    def _cs(deg):
+        # (angle / 180) * PI in f32; cos/sin evaluated in double then rounded (what
+        # rustc's constant folding of rotate_*(const) produces)
+        r = F32(F32(deg) / F32(180.0)) * PI_F
+        return F32(math.cos(float(r))), F32(math.sin(float(r)))
+
+    @staticmethod
+    def rotate_x(deg):
+        c, s = Matrix._cs(deg)
+        m = Matrix.identity()
+        m.m[1][1], m.m[1][2], m.m[2][1], m.m[2][2] = c, -s, s, c
+        return m
+
+    @staticmethod
+    def rotate_y(deg):
+        c, s = Matrix._cs(deg)
+        m = Matrix.identity()
+        m.m[0][0], m.m[0][2], m.m[2][0], m.m[2][2] = c, s, -s, c
+        return m
+
+    @staticmethod
+    def rotate_z(deg):
+        c, s = Matrix._cs(deg)
+        m = Matrix.identity()
+        m.m[0][0], m.m[0][1], m.m[1][0], m.m[1][1] = c, -s, s, c
+        return m
+
+    def __mul__(self, o):
+        r = Matrix()
+        for i in range(4):
+            for j in range(4):
+                acc = F32(0)
+                for k in range(4):
+                    acc = F32(acc + F32(self.m[i][k] * o.m[k][j]))
+                r.m[i][j] = acc
+        return r
+
+    def flat(self):
+        return [float(v) for row in self.m for v in row]
+
+
+def _color(c):
+    return abi.rt_color(*[float(F32(v)) for v in c])
+
+
+class SceneDesc:
+    """An rt_scene_desc: either produced by the C++ host builders (my_scene, synth,
+    bench_128) or assembled here shape by shape (Scene::add_shape order)."""
+
+    def __init__(self):
+        self._owned_ptr = None      # pointer from an rt_desc_* builder
+        self.materials, self.shapes, self.lights = [], [], []
+        self.ambient = (0.0, 0.0, 0.0)
+        self._keep = None
+
+    # ---- builders in librt_hip.so
+    @classmethod
+    def _from_builder(cls, fn, *args):
+        d = cls()
+        p = C.POINTER(abi.rt_scene_desc)()
+        check(fn(*args, C.byref(p)), fn.__name__)
+        d._owned_ptr = p
+        return d
+
+    @classmethod
+    def my_scene(cls):
+        """src/my_scene.rs:45-120"""
+        return cls._from_builder(lib().rt_desc_my_scene)
+
+    @classmethod
+    def bench_128(cls):
+        """src/render.rs:233-249"""
+        return cls._from_builder(lib().rt_desc_bench_128)
+
+    @classmethod
+    def synth(cls, seed, n_spheres, n_cubes=0, n_triangles=0, r_min=0.06, r_max=0.2):
+        p = abi.rt_synth_params(seed, n_spheres, n_cubes, n_triangles, r_min, r_max)
+        return cls._from_builder(lib().rt_desc_synth, C.byref(p))
+
+    @classmethod
+    def synth_config(cls, config):
+        """BASELINE.json configs 2..5."""
+        p = abi.rt_synth_params()
+        check(lib().rt_synth_config(config, C.byref(p)), "rt_synth_config")
+        return cls._from_builder(lib().rt_desc_synth, C.byref(p))
+
+    # ---- assembled in Python
+    def phong(self, ambient, diffuse, specular, power, reflectivity, refraction_index):
+        m = abi.rt_material()
+        m.kind = RT_MAT_PHONG
+        m.ambient = abi.rt_texture(RT_TEX_CONST, _color(ambient))
+        m.diffuse = abi.rt_texture(RT_TEX_CONST, _color(diffuse))
+        m.specular = abi.rt_texture(RT_TEX_CONST, _color(specular))
+        m.power, m.reflectivity, m.refraction_index = power, reflectivity, refraction_index
+        self.materials.append(m)
+        return len(self.materials) - 1
+
+    def texture_phong(self, ambient, diffuse, specular, power, reflectivity, refraction_index):
+        """Each texture is an RGB tuple (constant) or the string 'checkerboard'."""
+        def tex(t):
+            if isinstance(t, str):
+                assert t == "checkerboard"
+                return abi.rt_texture(RT_TEX_CHECKERBOARD, abi.rt_color(0, 0, 0))
+            return abi.rt_texture(RT_TEX_CONST, _color(t))
+        m = abi.rt_material()
+        m.kind = RT_MAT_TEXTURE_PHONG
+        m.ambient, m.diffuse, m.specular = tex(ambient), tex(diffuse), tex(specular)
+        m.power, m.reflectivity, m.refraction_index = power, reflectivity, refraction_index
+        self.materials.append(m)
+        return len(self.materials) - 1
+
+    def _shape(self, kind, mat, transform=None, data=()):
+        s = abi.rt_shape()
+        s.kind, s.material = kind, mat
+        s.transform[:] = (transform or Matrix.identity()).flat()
+        for i, v in enumerate(data):
+            s.data[i] = float(F32(v))
+        self.shapes.append(s)
+        return len(self.shapes) - 1
+
+    def sphere(self, mat, transform=None):
+        return self._shape(RT_SHAPE_SPHERE, mat, transform)
+
+    def plane(self, mat, origin, normal, transform=None):
+        return self._shape(RT_SHAPE_PLANE, mat, transform, tuple(origin) + tuple(normal))
+
+    def triangle(self, mat, v0, v1, v2):
+        return self._shape(RT_SHAPE_TRIANGLE, mat, None, tuple(v0) + tuple(v1) + tuple(v2))
+
+    def cube(self, mat, transform=None):
+        return self._shape(RT_SHAPE_CUBE, mat, transform)
+
+    def point_light(self, pos, color):
+        l = abi.rt_light()
+        l.kind = RT_LIGHT_POINT
+        l.pos[:] = [float(F32(v)) for v in pos]
+        l.color = _color(color)
+        self.lights.append(l)
+
+    def ambient_light(self, color):
+        l = abi.rt_light()
+        l.kind = RT_LIGHT_AMBIENT
+        l.color = _color(color)
+        self.lights.append(l)
+
+    def set_ambient(self, color):
+        self.ambient = color
+
+    def ptr(self):
+        """POINTER(rt_scene_desc) valid while this object lives."""
+        if self._owned_ptr is not None:
+            return self._owned_ptr
+        mats = (abi.rt_material * max(1, len(self.materials)))(*self.materials)
+        shapes = (abi.rt_shape * max(1, len(self.shapes)))(*self.shapes)
+        lights = (abi.rt_light * max(1, len(self.lights)))(*self.lights)
+        d = abi.rt_scene_desc(len(self.materials), mats, len(self.shapes), shapes,
+                              len(self.lights), lights, _color(self.ambient))
+        self._keep = (mats, shapes, lights, d)
+        return C.pointer(d)
+
+    @property
+    def n_shapes(self):
+        return self.ptr().contents.n_shapes
+
+    def __del__(self):
+        if self._owned_ptr is not None and abi._lib is not None:
+            abi._lib.rt_desc_free(self._owned_ptr)
+            self._owned_ptr = None
+
+
+class DeviceScene:
+    """An uploaded scene (rt_scene_create) on one HIP device."""
+
+    def __init__(self, desc, device=-1):
+        self._L = lib()
+        self.h = C.c_void_p()
+        self.desc = desc
+        check(self._L.rt_scene_create(desc.ptr(), device, C.byref(self.h)), "rt_scene_create")
+
+    def close(self):
+        if self.h:
+            self._L.rt_scene_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def flops_per_scan(self):
+        return int(self._L.rt_scene_flops_per_scan(self.h))
+
+    @property
+    def device_bytes(self):
+        return int(self._L.rt_scene_device_bytes(self.h))
+
+    def render(self, x_res, y_res, depth, want_u8=False, device=-1):
+        """render.rs:31-38 -> (rgb float32 [y_res, x_res, 3], counters dict, kernel_ms, rgb8)"""
+        cam = camera(x_res, y_res)
+        rgb = np.zeros((y_res, x_res, 3), np.float32)
+        rgb8 = np.zeros((y_res, x_res, 3), np.uint8) if want_u8 else None
+        cnt = abi.rt_counters()
+        ms = C.c_float(0)
+        opts = abi.rt_render_opts(device, C.pointer(cnt), C.pointer(ms))
+        check(self._L.rt_render(self.h, C.byref(cam), depth, C.byref(opts),
+                                rgb.ctypes.data_as(C.POINTER(C.c_float)),
+                                rgb8.ctypes.data_as(C.POINTER(C.c_uint8)) if want_u8 else None),
+              "rt_render")
+        counters = {"node_rays": cnt.node_rays, "shadow_rays": cnt.shadow_rays,
+                    "pixels": cnt.pixels}
+        return rgb, counters, ms.value, rgb8
+
+    def render_bands_async(self, cam, depth, band_rows, rank, world, d_rgb_ptr, d_counters_ptr,
+                           stream_ptr):
+        check(self._L.rt_render_bands_async(self.h, C.byref(cam), depth, band_rows, rank, world,
+                                            C.c_void_p(d_rgb_ptr), C.c_void_p(d_counters_ptr),
+                                            C.c_void_p(stream_ptr)), "rt_render_bands_async")
+
+
+def band_rows_per_rank(y_res, band_rows, world):
+    return int(lib().rt_band_rows_per_rank(y_res, band_rows, world))
+
+
+def unpermute_bands_async(d_gathered_ptr, x_res, y_res, band_rows, world, d_frame_ptr, stream_ptr):
+    check(lib().rt_unpermute_bands_async(C.c_void_p(d_gathered_ptr), x_res, y_res, band_rows, world,
+                                         C.c_void_p(d_frame_ptr), C.c_void_p(stream_ptr)),
+          "rt_unpermute_bands_async")
+
+
+def quantize_u8_async(d_rgb_ptr, n, d_rgb8_ptr, stream_ptr):
+    check(lib().rt_quantize_u8_async(C.c_void_p(d_rgb_ptr), n, C.c_void_p(d_rgb8_ptr),
+                                     C.c_void_p(stream_ptr)), "rt_quantize_u8_async")
+
+
+def render(x_res, y_res, desc, depth, device=-1, want_u8=False):
+    """One-shot: upload `desc`, render, release (the reference's render() seam)."""
+    s = DeviceScene(desc, device)
+    try:
+        return s.render(x_res, y_res, depth, want_u8=want_u8, device=device)
+    finally:
+        s.close()
