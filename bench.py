@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""bench.py -- Mpixels/s of the MI355X render path on BASELINE.json's headline workload.
+
+Workload (BASELINE.json configs[2]): synth(seed=2) = 600
+spheres + 25 cubes (300 triangles) + 100 loose triangles + my_scene's 2 textured planes,
+3 point lights; 1920x1080; depth 8 (reference semantics: primary + 7 secondary levels,
+src/render.rs:43-45).  Synthetic scene, no dataset.
+
+A step = one full frame: every rank renders its block-cyclic row bands with the HIP
+megakernel, then (N > 1) the bands are gathered to rank 0 over RCCL and un-permuted.
+The frame is fixed as N grows ("scaling": "strong").
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Prints ONE JSON line on rank 0 with `roofline` (VALU f32, the bound of this path: see
+DESIGN.md) and `cpu_baseline` (the CPU oracle -- a C++ restatement of the reference's
+single-threaded render.rs -- timed on a bounded row sample, rank 0, N = 1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402  (first: one HIP runtime per process, see rust_tracer_amd/abi.py)
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "Mpixels/sec (primary+8 bounces) at 1920×1080; fraction of HBM roofline"
+PEAK_F32_TFLOPS = 157.3      # MI355X FP32 vector peak (MI355X_MICROARCH.md)
+PEAK_HBM_GBPS = 8000.0       # MI355X HBM3E peak
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--config", type=int, default=3, help="BASELINE config (2..5 synth scenes)")
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--depth", type=int, default=8)
+    p.add_argument("--band-rows", type=int, default=8)
+    p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU oracle timing")
+    p.add_argument("--cpu-rows-step", type=int, default=24,
+                   help="CPU baseline renders every k-th row of the frame")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                   help="rocprofv3 FETCH_SIZE/WRITE_SIZE summary for the render kernel")
+    return p.parse_args()
+
+
+def cpu_baseline(args, desc):
+    """Single-threaded CPU oracle (the reference's algorithm, restated in C++) on every
+    k-th row of the same frame.  Mpixels/s = rendered pixels / wall time."""
+    from oracle.oracle import OracleScene
+    o = OracleScene(desc)
+    rows = range(0, args.height, args.cpu_rows_step)
+    t0 = time.perf_counter()
+    _, cnt = o.render(args.width, args.height, args.depth, rows=(0, args.height, args.cpu_rows_step),
+                      threads=1)
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(cnt["pixels"] / dt / 1e6, 6),
+        "unit": "Mpixels/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{len(rows)} of {args.height} rows (every {args.cpu_rows_step}th) of the "
+                  f"benchmark frame, {cnt['pixels']} pixels, {dt:.1f} s, single thread "
+                  f"(C++ restatement of src/render.rs, g++ -O2 -ffp-contract=off); "
+                  f"host: {os.cpu_count()} logical CPUs",
+        "seconds": round(dt, 2),
+    }
+
+
+def load_traffic(path, workload):
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("workload") == workload:
+            return t
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from rust_tracer_amd import DeviceScene, SceneDesc
+    from rust_tracer_amd.dist import FrameTiler
+
+    desc = SceneDesc.synth_config(args.config)
+    scene = DeviceScene(desc, device=dev.index)
+    tiler = FrameTiler(scene, args.width, args.height, args.depth, args.band_rows, rank, world, dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[dev.index])
+
+    for _ in range(args.warmup):
+        tiler.step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    tiler.counters.zero_()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record()
+        tiler.render_local()       # the megakernel, on torch's current stream
+        ev[k][1].record()
+        tiler.assemble()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    cnt = tiler.counters.double()
+    local_scans = float(cnt[0] + cnt[1]) / args.steps   # this rank's launch (for the roofline)
+    stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+    elapsed, kernel_ms_max = stats.tolist()
+    node_rays, shadow_rays, pixels = cnt.tolist()
+
+    if rank == 0:
+        steps = args.steps
+        mpix = args.width * args.height * steps / elapsed / 1e6
+        scans_per_step = (node_rays + shadow_rays) / steps
+        flops_per_step = scans_per_step * scene.flops_per_scan          # SURVEY.md §8(d) F_alg
+        per_launch_flops = local_scans * scene.flops_per_scan          # rank 0's launch
+        achieved = per_launch_flops / (kernel_ms / 1e3) / 1e12
+        workload = (f"config{args.config}: synth seed 2 (600 spheres, 25 cubes, 100 triangles, "
+                    f"2 planes, 3 point lights), {args.width}x{args.height}, depth {args.depth}")
+        traffic = load_traffic(args.traffic_json, workload)
+        roofline = {
+            "bound": "valu",
+            "achieved": round(achieved, 3),
+            "peak": PEAK_F32_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_F32_TFLOPS, 4),
+            "traffic": traffic["bytes_per_launch"] if traffic else None,
+            "kernel": "render_kernel<7>",
+            "kernel_ms": round(kernel_ms, 4),
+            "flops_per_launch": per_launch_flops,
+            "ceilings": {"no_fma_contraction": 0.5},
+            "hbm": {
+                "algorithmic_bytes_per_launch": scene.device_bytes + args.width * args.height * 12 / world,
+                "achieved_GBps": round((traffic["bytes_per_launch"] / (kernel_ms / 1e3) / 1e9), 3)
+                if traffic else None,
+                "peak_GBps": PEAK_HBM_GBPS,
+                "frac": round(traffic["bytes_per_launch"] / (kernel_ms / 1e3) / 1e9 / PEAK_HBM_GBPS, 6)
+                if traffic else None,
+            },
+        }
+        out = {
+            "metric": METRIC,
+            "value": round(mpix, 3),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded scene, SURVEY.md §8(d))",
+            "config": {
+                "workload": workload,
+                "width": args.width, "height": args.height, "depth": args.depth,
+                "leaf_primitives": 1000, "band_rows": args.band_rows,
+                "parallelism": f"row-bands x{world}" + (" + RCCL gather" if world > 1 else ""),
+                "node_rays_per_frame": node_rays / steps,
+                "shadow_rays_per_frame": shadow_rays / steps,
+            },
+            "roofline": roofline,
+            "cpu_baseline": None,
+        }
+        if world == 1 and args.cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args, desc)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

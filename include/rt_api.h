@@ -134,6 +134,9 @@ typedef struct rt_counters {
                                (Scene::intersect from trace_ray, render.rs:47) */
     uint64_t shadow_rays;   /* scene scans for point-light shadow rays (mod.rs:193) */
     uint64_t pixels;        /* pixels rendered by this call */
+    uint64_t wave_iterations; /* megakernel loop iterations summed over waves (each is one
+                                 scan per active lane): lane utilisation =
+                                 (node_rays + shadow_rays) / (64 * wave_iterations) */
 } rt_counters;
 
 typedef struct rt_render_opts {

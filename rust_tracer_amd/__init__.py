@@ -258,6 +258,7 @@ class DeviceScene:
               "rt_render")
         counters = {"node_rays": cnt.node_rays, "shadow_rays": cnt.shadow_rays,
                     "pixels": cnt.pixels}
+        self.last_wave_iterations = cnt.wave_iterations
         return rgb, counters, ms.value, rgb8
 
     def render_bands_async(self, cam, depth, band_rows, rank, world, d_rgb_ptr, d_counters_ptr,

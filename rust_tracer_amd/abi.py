@@ -61,7 +61,8 @@ class rt_camera(C.Structure):
 
 
 class rt_counters(C.Structure):
-    _fields_ = [("node_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("pixels", C.c_uint64)]
+    _fields_ = [("node_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("pixels", C.c_uint64),
+                ("wave_iterations", C.c_uint64)]
 
 
 class rt_render_opts(C.Structure):

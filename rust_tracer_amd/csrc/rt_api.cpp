@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <memory>
@@ -26,6 +27,12 @@ hipError_t render_occupancy(uint32_t depth, int* blocks_per_cu);
 hipError_t launch_unpermute(const float* in, uint32_t x_res, uint32_t y_res, uint32_t band_rows,
                             uint32_t world, uint32_t rows_per_rank, float* out, hipStream_t stream);
 hipError_t launch_quantize(const float* in, size_t n, uint8_t* out, hipStream_t stream);
+bool rt_cube_table_check(const float* table);
+hipError_t wave_occupancy(int* trace_blocks, int* combine_blocks);
+hipError_t launch_wave_init(uint32_t* levels, uint32_t n_words, uint32_t total_items, uint32_t* overflow,
+                            hipStream_t stream);
+hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream);
+hipError_t launch_wave_combine(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream);
 }  // namespace rtdev
 
 using namespace rtdev;
@@ -128,9 +135,22 @@ struct Workspace {
     size_t out_floats = 0;
     uint8_t* out8 = nullptr;
     size_t out8_bytes = 0;
-    unsigned long long* counters = nullptr;  // [node, shadow, pixels]
+    unsigned long long* counters = nullptr;  // [node, shadow, pixels, wave iterations]
     uint32_t* work = nullptr;        // persistent-kernel work counter
+    // level-synchronous pipeline
+    Task* tasks = nullptr;
+    NodeRec* nodes = nullptr;
+    uint32_t capacity = 0;
+    uint32_t* levels = nullptr;      // 2 * (RT_MAX_DEPTH + 2) words
+    uint32_t* overflow = nullptr;
 };
+
+// Device path: "wave" (level-synchronous, default) or "mega" (per-pixel megakernel),
+// chosen with RT_PIPELINE for A/B measurement.
+bool use_megakernel() {
+    const char* e = std::getenv("RT_PIPELINE");
+    return e && std::strcmp(e, "mega") == 0;
+}
 
 int g_num_cus(int device) {
     hipDeviceProp_t prop;
@@ -148,6 +168,7 @@ struct rt_scene {
     uint64_t flops_per_scan = 0;
     int num_cus = 256;
     int occ[3] = {0, 0, 0};  // blocks per CU for the MAXF 7 / 15 / 63 variants
+    int occ_trace = 0, occ_combine = 0;
     Workspace ws;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -242,6 +263,15 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     // ---- host preprocessing into per-type runs
     std::vector<float> dsph, gsph, tri, cube, plane, cubetri;
     std::vector<ShapeRec> shapes(d->n_shapes);
+    struct DiagSph {
+        float s[3], o[3], key;
+    };
+    struct LooseTri {
+        F3 v0, e1, e2;
+        float key;
+    };
+    std::vector<DiagSph> diag_sph;
+    std::vector<LooseTri> loose;
     uint64_t flops = 0;
     for (uint32_t i = 0; i < d->n_shapes; i++) {
         const rt_shape& s = d->shapes[i];
@@ -260,8 +290,8 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
                 bool diag = inv.m[0][1] == 0.f && inv.m[0][2] == 0.f && inv.m[1][0] == 0.f &&
                             inv.m[1][2] == 0.f && inv.m[2][0] == 0.f && inv.m[2][1] == 0.f;
                 if (diag) {
-                    put4(dsph, inv.m[0][0], inv.m[1][1], inv.m[2][2], key);
-                    put4(dsph, inv.m[0][3], inv.m[1][3], inv.m[2][3], 0.f);
+                    diag_sph.push_back(DiagSph{{inv.m[0][0], inv.m[1][1], inv.m[2][2]},
+                                           {inv.m[0][3], inv.m[1][3], inv.m[2][3]}, key});
                 } else {
                     for (int r = 0; r < 3; r++) put4(gsph, inv.m[r][0], inv.m[r][1], inv.m[r][2], inv.m[r][3]);
                     put4(gsph, key, 0.f, 0.f, 0.f);
@@ -292,9 +322,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
                 F3 e1 = fsub(v1, v0), e2 = fsub(v2, v0), nn = tri_normal(v0, v1, v2);
                 const float a[12] = {v0.x, v0.y, v0.z, e1.x, e1.y, e1.z, e2.x, e2.y, e2.z, nn.x, nn.y, nn.z};
                 std::memcpy(R.a, a, sizeof(a));
-                put4(tri, v0.x, v0.y, v0.z, key);
-                put4(tri, e1.x, e1.y, e1.z, 0.f);
-                put4(tri, e2.x, e2.y, e2.z, 0.f);
+                loose.push_back(LooseTri{v0, e1, e2, key});
                 flops += 52;
                 break;
             }
@@ -308,7 +336,35 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
                 return RT_ERR_INVALID_ARG;
         }
     }
+    // diag spheres in pairs (2-wide packed scan); an odd one out joins the general run
+    for (size_t k = 0; k + 1 < diag_sph.size(); k += 2) {
+        const DiagSph &A = diag_sph[k], &B = diag_sph[k + 1];
+        put4(dsph, A.s[0], B.s[0], A.s[1], B.s[1]);
+        put4(dsph, A.s[2], B.s[2], A.o[0], B.o[0]);
+        put4(dsph, A.o[1], B.o[1], A.o[2], B.o[2]);
+        put4(dsph, A.key, B.key, 0.f, 0.f);
+    }
+    if (diag_sph.size() & 1) {
+        const DiagSph& A = diag_sph.back();  // general form of the same inverse (exact formula)
+        put4(gsph, A.s[0], 0.f, 0.f, A.o[0]);
+        put4(gsph, 0.f, A.s[1], 0.f, A.o[1]);
+        put4(gsph, 0.f, 0.f, A.s[2], A.o[2]);
+        put4(gsph, A.key, 0.f, 0.f, 0.f);
+    }
+    // loose triangles in pairs; an odd count is padded with a degenerate triangle
+    // (e1 = e2 = 0 -> det = 0 -> |det| < EPS: never a hit)
+    if (loose.size() & 1) loose.push_back(LooseTri{f3(0, 0, 0), f3(0, 0, 0), f3(0, 0, 0), keyf(0xFFFFFFF0u)});
+    for (size_t k = 0; k < loose.size(); k += 2) {
+        const LooseTri &A = loose[k], &B = loose[k + 1];
+        put4(tri, A.v0.x, B.v0.x, A.v0.y, B.v0.y);
+        put4(tri, A.v0.z, B.v0.z, A.e1.x, B.e1.x);
+        put4(tri, A.e1.y, B.e1.y, A.e1.z, B.e1.z);
+        put4(tri, A.e2.x, B.e2.x, A.e2.y, B.e2.y);
+        put4(tri, A.e2.z, B.e2.z, A.key, B.key);
+        put4(tri, 0.f, 0.f, 0.f, 0.f);
+    }
     cube_triangles(cubetri);
+    if (!rt_cube_table_check(cubetri.data())) return RT_ERR_UNSUPPORTED;
     std::vector<MatRec> mats(d->n_materials);
     for (uint32_t i = 0; i < d->n_materials; i++) {
         const rt_material& m = d->materials[i];
@@ -351,7 +407,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     size_t total = 0;
     for (auto& s : secs) {
         s.off = total;
-        total += (s.bytes + 255) & ~(size_t)255;
+        total += (s.bytes + 96 + 255) & ~(size_t)255;  // + one record group of look-ahead slack
     }
     if (total == 0) total = 256;
 
@@ -376,9 +432,9 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     S.shapes = (const ShapeRec*)at(6);
     S.mats = (const MatRec*)at(7);
     S.lights = (const LightRec*)at(8);
-    S.n_dsph = (int32_t)(dsph.size() / 8);
+    S.n_dsph = (int32_t)(dsph.size() / 16);  // pairs
     S.n_gsph = (int32_t)(gsph.size() / 16);
-    S.n_tri = (int32_t)(tri.size() / 12);
+    S.n_tri = (int32_t)(tri.size() / 24);    // pairs
     S.n_cube = (int32_t)(cube.size() / 16);
     S.n_plane = (int32_t)(plane.size() / 20);
     S.n_shapes = (int32_t)d->n_shapes;
@@ -404,6 +460,10 @@ rt_status rt_scene_destroy(rt_scene* s) {
     if (s->ws.out8) (void)hipFree(s->ws.out8);
     if (s->ws.counters) (void)hipFree(s->ws.counters);
     if (s->ws.work) (void)hipFree(s->ws.work);
+    if (s->ws.tasks) (void)hipFree(s->ws.tasks);
+    if (s->ws.nodes) (void)hipFree(s->ws.nodes);
+    if (s->ws.levels) (void)hipFree(s->ws.levels);
+    if (s->ws.overflow) (void)hipFree(s->ws.overflow);
     if (s->dmem) (void)hipFree(s->dmem);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -415,6 +475,10 @@ rt_status rt_scene_destroy(rt_scene* s) {
 uint64_t rt_scene_flops_per_scan(const rt_scene* s) { return s ? s->flops_per_scan : 0; }
 uint64_t rt_scene_device_bytes(const rt_scene* s) { return s ? (uint64_t)s->dbytes : 0; }
 
+static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
+                                   uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
+                                   hipStream_t stream);
+
 static rt_status launch_bands(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
                               uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
                               hipStream_t stream) {
@@ -424,6 +488,8 @@ static rt_status launch_bands(rt_scene* s, const rt_camera* cam, uint32_t depth,
     if ((uint64_t)cam->x_res * cam->y_res * 3 >= (1ull << 32)) return RT_ERR_UNSUPPORTED;
     rt_status st = ensure_ws(s, 0, 0);
     if (st != RT_OK) return st;
+    if (!use_megakernel())
+        return launch_bands_wave(s, cam, depth, band_rows, rank, world, d_rgb, d_counters, stream);
     RenderParams p;
     std::memset(&p, 0, sizeof(p));
     p.S = s->S;
@@ -447,6 +513,7 @@ static rt_status launch_bands(rt_scene* s, const rt_camera* cam, uint32_t depth,
     p.total_items = p.tiles_x * tiles_y * 64u;
     p.out = d_rgb;
     p.ray_counters = d_counters;
+    p.iter_counter = s->ws.counters + 3;
     p.work_counter = s->ws.work;
 
     int var = variant_of(depth);
@@ -461,6 +528,72 @@ static rt_status launch_bands(rt_scene* s, const rt_camera* cam, uint32_t depth,
     if (blocks < 1) blocks = 1;
     HIP_TRY(hipMemsetAsync(s->ws.work, 0, sizeof(uint32_t), stream));
     HIP_TRY(launch_render(p, (int)blocks, stream));
+    return RT_OK;
+}
+
+// Level-synchronous pipeline: trace(0..L-1), then combine(L-1..0), all on `stream`.
+static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
+                                   uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
+                                   hipStream_t stream) {
+    WaveParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.S = s->S;
+    p.cam_ox = cam->origin[0];
+    p.cam_oy = cam->origin[1];
+    p.cam_oz = cam->origin[2];
+    p.x_min = cam->x_min;
+    p.y_max = cam->y_max;
+    p.x_delta = (cam->x_max - cam->x_min) / (float)cam->x_res;  // render.rs:179-180
+    p.y_delta = (cam->y_max - cam->y_min) / (float)cam->y_res;
+    p.width = cam->x_res;
+    p.height = cam->y_res;
+    p.depth = depth;
+    p.band_rows = band_rows;
+    p.rank = rank;
+    p.world = world;
+    p.rows_local = rt_band_rows_per_rank(cam->y_res, band_rows, world);
+    p.tiles_x = (cam->x_res + 7) / 8;
+    uint64_t total = (uint64_t)p.tiles_x * ((p.rows_local + 7) / 8) * 64u;
+    if (total >= (1ull << 30)) return RT_ERR_UNSUPPORTED;
+    p.total_items = (uint32_t)total;
+    // node / task pool: level 0 plus room for ~11 secondary nodes per pixel on average
+    // (config 3 needs 2.7); an overflow is reported, never silently truncated
+    uint64_t want = std::max<uint64_t>(total * 12u, 1u << 20);
+    if (want > 0x7FFFFFFFu) want = 0x7FFFFFFFu;
+    Workspace& w = s->ws;
+    if (w.capacity < want) {  // grows only (rt_render may have grown it after an overflow)
+        if (w.tasks) (void)hipFree(w.tasks);
+        if (w.nodes) (void)hipFree(w.nodes);
+        w.tasks = nullptr;
+        w.nodes = nullptr;
+        w.capacity = 0;
+        HIP_TRY(hipMalloc(&w.tasks, want * sizeof(Task)));
+        HIP_TRY(hipMalloc(&w.nodes, want * sizeof(NodeRec)));
+        w.capacity = (uint32_t)want;
+    }
+    if (!w.levels) {
+        HIP_TRY(hipMalloc(&w.levels, 2 * (RT_MAX_DEPTH + 2) * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&w.overflow, 64));
+    }
+    p.capacity = w.capacity;
+    p.tasks = w.tasks;
+    p.nodes = w.nodes;
+    p.levels = w.levels;
+    p.overflow = w.overflow;
+    p.out = d_rgb;
+    p.ray_counters = d_counters;
+    if (s->occ_trace == 0) {
+        int a = 0, b = 0;
+        HIP_TRY(wave_occupancy(&a, &b));
+        s->occ_trace = a > 0 ? a : 1;
+        s->occ_combine = b > 0 ? b : 1;
+    }
+    int tb = s->num_cus * s->occ_trace;
+    int cb = s->num_cus * s->occ_combine;
+    uint32_t levels = depth > 0 ? depth : 1;
+    HIP_TRY(launch_wave_init(w.levels, 2 * (RT_MAX_DEPTH + 2), p.total_items, w.overflow, stream));
+    for (uint32_t k = 0; k < levels; k++) HIP_TRY(launch_wave_trace(p, k, tb, stream));
+    for (uint32_t k = levels; k-- > 0;) HIP_TRY(launch_wave_combine(p, k, cb, stream));
     return RT_OK;
 }
 
@@ -500,12 +633,30 @@ rt_status rt_render(const rt_scene* scene, const rt_camera* cam, uint32_t depth,
     rt_status st = ensure_ws(s, n, rgb8 ? n : 0);
     if (st != RT_OK) return st;
     hipStream_t stream = s->stream;
-    HIP_TRY(hipMemsetAsync(s->ws.counters, 0, 4 * sizeof(unsigned long long), stream));
-    HIP_TRY(hipEventRecord(s->ev0, stream));
-    // single device: one "band" holding every row
-    st = launch_bands(s, cam, depth, 8, 0, 1, s->ws.out, s->ws.counters, stream);
-    if (st != RT_OK) return st;
-    HIP_TRY(hipEventRecord(s->ev1, stream));
+    for (int attempt = 0;; attempt++) {
+        HIP_TRY(hipMemsetAsync(s->ws.counters, 0, 4 * sizeof(unsigned long long), stream));
+        HIP_TRY(hipEventRecord(s->ev0, stream));
+        // single device: one "band" holding every row
+        st = launch_bands(s, cam, depth, 8, 0, 1, s->ws.out, s->ws.counters, stream);
+        if (st != RT_OK) return st;
+        HIP_TRY(hipEventRecord(s->ev1, stream));
+        if (use_megakernel() || !s->ws.overflow) break;
+        uint32_t ovf = 0;
+        HIP_TRY(hipMemcpyAsync(&ovf, s->ws.overflow, sizeof(ovf), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        if (!ovf) break;
+        // node pool too small for this scene's ray trees: grow it and render again
+        if (attempt >= 6 || s->ws.capacity >= 0x40000000u) return RT_ERR_OUT_OF_MEMORY;
+        uint32_t cap = s->ws.capacity * 2u;
+        (void)hipFree(s->ws.tasks);
+        (void)hipFree(s->ws.nodes);
+        s->ws.tasks = nullptr;
+        s->ws.nodes = nullptr;
+        s->ws.capacity = 0;
+        HIP_TRY(hipMalloc(&s->ws.tasks, (size_t)cap * sizeof(Task)));
+        HIP_TRY(hipMalloc(&s->ws.nodes, (size_t)cap * sizeof(NodeRec)));
+        s->ws.capacity = cap;
+    }
     if (rgb8) HIP_TRY(launch_quantize(s->ws.out, n, s->ws.out8, stream));
     HIP_TRY(hipMemcpyAsync(rgb, s->ws.out, n * sizeof(float), hipMemcpyDeviceToHost, stream));
     if (rgb8) HIP_TRY(hipMemcpyAsync(rgb8, s->ws.out8, n, hipMemcpyDeviceToHost, stream));
@@ -516,6 +667,7 @@ rt_status rt_render(const rt_scene* scene, const rt_camera* cam, uint32_t depth,
         opts->counters->node_rays = cnt[0];
         opts->counters->shadow_rays = cnt[1];
         opts->counters->pixels = cnt[2];
+        opts->counters->wave_iterations = cnt[3];
     }
     if (opts && opts->kernel_ms) {
         float ms = 0.f;

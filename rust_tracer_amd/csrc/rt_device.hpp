@@ -6,11 +6,14 @@
 // SMEM loads: every lane tests the same primitive against its own ray).
 //
 //   run      record (float4s)                              bytes   used by
-//   dsph     {s0 s1 s2 key} {o0 o1 o2 -}                   32      scan: spheres whose inverse has a
-//                                                                  zero 3x3 off-diagonal (translate*scale)
-//   gsph     {inv row0} {inv row1} {inv row2} {key - - -}  64      scan: all other spheres
-//   tri      {v0 key} {e1 -} {e2 -}                        48      scan: loose triangles (world space)
-//   cube     {inv row0} {inv row1} {inv row2} {key - - -}  64      scan: cube instances (12 object tris)
+//   dsph     PAIRS of spheres whose inverse has a zero 3x3   64      scan (2-wide packed)
+//            off-diagonal: {sxA sxB syA syB} {szA szB oxA oxB} {oyA oyB ozA ozB} {keyA keyB - -}
+//   gsph     {inv row0} {inv row1} {inv row2} {key - - -}  64      scan: other spheres (+ odd tail)
+//   tri      PAIRS of loose triangles (world space):        96      scan (2-wide packed)
+//            {v0xA v0xB v0yA v0yB} {v0zA v0zB e1xA e1xB} {e1yA e1yB e1zA e1zB}
+//            {e2xA e2xB e2yA e2yB} {e2zA e2zB keyA keyB} {- - - -}   (odd tail: degenerate pad)
+//   cube     {inv row0} {inv row1} {inv row2} {key - - -}  64      scan: cube instances (12 object tris,
+//                                                                  compile-time, rt_scan.hpp)
 //   plane    {inv r0} {inv r1} {inv r2} {n key} {origin -} 80      scan: planes
 //   cubetri  12 x {v0 -} {e1 -} {e2 -} {n -}               768     unit-cube triangles (cube.rs:21-77)
 //   shapes   ShapeRec per shape, insertion order            128     attributes of the nearest hit
@@ -61,7 +64,7 @@ struct DevScene {
     const ShapeRec* shapes;
     const MatRec* mats;
     const LightRec* lights;
-    int32_t n_dsph, n_gsph, n_tri, n_cube, n_plane, n_shapes, n_lights, n_mats;
+    int32_t n_dsph, n_gsph, n_tri, n_cube, n_plane, n_shapes, n_lights, n_mats;  // dsph/tri: pairs
     float amb_r, amb_g, amb_b;
 };
 
@@ -76,7 +79,45 @@ struct RenderParams {
     uint32_t tiles_x, total_items;          // 8x8 pixel tiles over (width x rows_local)
     float* out;                             // rows_local * width * 3 floats
     unsigned long long* ray_counters;       // [node, shadow, pixels], added to
+    unsigned long long* iter_counter;       // optional: wave loop iterations (lane utilisation)
     uint32_t* work_counter;                 // zeroed before the launch
+};
+
+// ---- level-synchronous ("wavefront") pipeline, rt_wavefront.hip ----------------------
+// A ray task of tree level k >= 1 (level-0 tasks are the pixels themselves).
+struct Task {
+    float ox, oy, oz, dx, dy, dz;
+    uint32_t parent;   // (node index << 1) | slot  (slot 0 = reflected, 1 = refracted)
+    uint32_t pad;
+};
+
+// One traced tree node: everything render.rs:100 needs to combine it with the colours
+// its children return, plus where to return its own colour.
+struct NodeRec {
+    float ax, ay, az;          // ambient + lights
+    float fr, dr, pw, ft;      // reflected: fresnel, rdir.n, (m.h)^power; refracted: 1 - fresnel
+    float kdx, kdy, kdz, ksx, ksy, ksz;
+    float erx, ery, erz;       // colour of the reflected child (0 until it reports)
+    float etx, ety, etz;       // colour of the refracted child
+    uint32_t flags;
+    uint32_t parent;           // as Task::parent; level 0: unused
+    uint32_t pad[3];
+};
+
+struct WaveParams {
+    DevScene S;
+    float cam_ox, cam_oy, cam_oz;
+    float x_min, y_max, x_delta, y_delta;
+    uint32_t width, height, depth;
+    uint32_t band_rows, rank, world, rows_local;
+    uint32_t tiles_x, total_items;     // level-0 tasks (8x8 tiles over width x rows_local)
+    uint32_t capacity;                 // node / task slots
+    Task* tasks;                       // [capacity]
+    NodeRec* nodes;                    // [capacity]
+    uint32_t* levels;                  // [2 * (RT_MAX_DEPTH + 1)]: offset, count per level
+    uint32_t* overflow;                // set when an append would exceed capacity
+    float* out;
+    unsigned long long* ray_counters;  // [node, shadow, pixels], added to
 };
 
 }  // namespace rtdev

@@ -28,356 +28,9 @@
 #include "../../include/rt_api.h"
 #include "rt_device.hpp"
 
+#include "rt_common.hpp"
+
 namespace rtdev {
-
-#define RT_EPS 1.1920929e-07f  // std::f32::EPSILON
-
-struct V3 {
-    float x, y, z;
-};
-__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
-__device__ __forceinline__ V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ V3 mul(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
-__device__ __forceinline__ V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
-__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ float len2(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
-__device__ __forceinline__ V3 cross(V3 a, V3 b) {
-    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
-}
-// vector3.rs:91-94: three divisions by the length, not a reciprocal multiply
-__device__ __forceinline__ V3 norm(V3 a) {
-    float l = sqrtf(len2(a));
-    return v3(a.x / l, a.y / l, a.z / l);
-}
-// matrix.rs:248-263 / 240-246 on rows r0..r2 = (m_i0, m_i1, m_i2, m_i3)
-__device__ __forceinline__ V3 pt_mul(float4 r0, float4 r1, float4 r2, V3 p) {
-    return v3(p.x * r0.x + p.y * r0.y + p.z * r0.z + r0.w, p.x * r1.x + p.y * r1.y + p.z * r1.z + r1.w,
-              p.x * r2.x + p.y * r2.y + p.z * r2.z + r2.w);
-}
-__device__ __forceinline__ V3 vec3_mul(float4 r0, float4 r1, float4 r2, V3 v) {
-    return v3(v.x * r0.x + v.y * r0.y + v.z * r0.z, v.x * r1.x + v.y * r1.y + v.z * r1.z,
-              v.x * r2.x + v.y * r2.y + v.z * r2.z);
-}
-// inv_transform.transpose() * v  (sphere.rs:76, cube.rs:98)
-__device__ __forceinline__ V3 tr_vec3_mul(float4 r0, float4 r1, float4 r2, V3 v) {
-    return v3(v.x * r0.x + v.y * r1.x + v.z * r2.x, v.x * r0.y + v.y * r1.y + v.z * r2.y,
-              v.x * r0.z + v.y * r1.z + v.z * r2.z);
-}
-__device__ __forceinline__ V3 xyz(float4 a) { return v3(a.x, a.y, a.z); }
-__device__ __forceinline__ uint32_t keyof(float w) { return __float_as_uint(w); }
-
-// Scene records are read through the constant address space: with wave-uniform indices
-// the compiler then emits scalar (SMEM) loads into SGPRs, and every lane's VALU op takes
-// the primitive's coefficients as a scalar operand.
-#if defined(__HIP_DEVICE_COMPILE__)
-typedef const __attribute__((address_space(4))) float4 cfloat4;
-#else
-typedef const float4 cfloat4;  // host pass: the kernel body is never executed there
-#endif
-__device__ __forceinline__ cfloat4* cptr(const float4* p) { return (cfloat4*)p; }
-
-// Nearest-hit bookkeeping: (t, key) lexicographic minimum == Scene::intersect's strict `<`
-// in insertion order (ties keep the earlier shape / earlier cube triangle).
-__device__ __forceinline__ void take(float t, uint32_t key, float& bt, uint32_t& bk) {
-    bool better = (t < bt) | ((t == bt) & (key < bk));
-    bt = better ? t : bt;
-    bk = better ? key : bk;
-}
-
-// sphere.rs:126-145 + :66-77 on an object-space ray; returns t (false = no hit)
-__device__ __forceinline__ bool sphere_t(V3 o, V3 d, float& t_out, bool& entering) {
-    float a = len2(d);
-    float b = 2.f * dot(d, o);  // l = o - Point3(0,0,0) == o
-    float c = len2(o) - 1.f;
-    float discr = b * b - 4.f * a * c;
-    if (discr < 0.f) return false;
-    float t0, t1;
-    if (fabsf(discr) < RT_EPS) {
-        float x = -0.5f * b / a;
-        t0 = x;
-        t1 = x;
-    } else {
-        float sq = sqrtf(discr);
-        float q = (b > 0.f) ? -0.5f * (b + sq) : -0.5f * (b - sq);
-        t0 = q / a;
-        t1 = c / q;
-    }
-    if (t0 > t1) {
-        float tmp = t1;
-        t1 = t0;
-        t0 = tmp;
-    }
-    if (t0 < 0.f && t1 < 0.f) return false;
-    t_out = (t0 < 0.f) ? t1 : t0;
-    entering = t0 > 0.f;
-    return true;
-}
-
-// triangle.rs:51-80, Moller-Trumbore with e1 = v1 - v0, e2 = v2 - v0 precomputed
-// (bit-identical: the host evaluates the same f32 subtractions).
-// The division 1/det is only executed for lanes whose u-numerator can pass: for
-// |det| <= 2^20 and a normal |un| the sign / magnitude pre-test below rejects exactly
-// the lanes for which u = un * (1/det) would be < 0 or > 1.
-__device__ __forceinline__ bool tri_hit(V3 o, V3 d, V3 v0, V3 e1, V3 e2, float& t_out,
-                                        float& u_out, float& v_out, float& det_out) {
-    V3 pvec = cross(d, e2);
-    float det = dot(e1, pvec);
-    if (fabsf(det) < RT_EPS) return false;
-    V3 tvec = sub(o, v0);
-    float un = dot(tvec, pvec);
-    float adet = fabsf(det);
-    bool opp = (un < 0.f) != (det < 0.f);
-    bool early = (adet <= 1048576.f) &&
-                 ((opp && (un != 0.f) && (fabsf(un) >= 1.17549435e-38f)) || (fabsf(un) > 2.f * adet));
-    if (early) return false;
-    float inv_det = 1.0f / det;
-    float u = un * inv_det;
-    if (u < 0.f || u > 1.f) return false;
-    V3 qvec = cross(tvec, e1);
-    float v = dot(d, qvec) * inv_det;
-    if (v < 0.f || u + v > 1.f) return false;
-    float t = dot(e2, qvec) * inv_det;
-    if (t < 0.f) return false;
-    t_out = t;
-    u_out = u;
-    v_out = v;
-    det_out = det;
-    return true;
-}
-
-// plane.rs:59-66: object-space ray, returns t (can be negative)
-__device__ __forceinline__ bool plane_t(V3 o, V3 d, V3 n, V3 origin, float& t_out) {
-    float denom = -dot(n, d);
-    if (!(denom > RT_EPS)) return false;
-    V3 dir = sub(origin, o);
-    t_out = -dot(dir, n) / denom;
-    return true;
-}
-
-// ------------------------------------------------------------------ the scan
-// One pass over every primitive for one ray per lane.  All loop indices are
-// wave-uniform, so records come in through the scalar cache.
-__device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk) {
-    bt = __builtin_huge_valf();
-    bk = 0xFFFFFFFFu;
-    // planes
-    for (int i = 0; i < S.n_plane; ++i) {
-        cfloat4* r = cptr(S.plane) + 5 * i;
-        float4 r0 = r[0], r1 = r[1], r2 = r[2], rn = r[3], ro = r[4];
-        V3 to = pt_mul(r0, r1, r2, o);
-        V3 td = vec3_mul(r0, r1, r2, d);
-        float t;
-        if (plane_t(to, td, xyz(rn), xyz(ro), t)) take(t, keyof(rn.w), bt, bk);
-    }
-    // spheres with a translate*scale inverse: the zero off-diagonal products of pt_mul /
-    // vec3_mul are skipped; x*m + (+-0) == x*m, so t is unchanged (only a zero's sign
-    // can differ, which no comparison below observes).
-    for (int i = 0; i < S.n_dsph; ++i) {
-        cfloat4* r = cptr(S.dsph) + 2 * i;
-        float4 s = r[0], off = r[1];
-        V3 to = v3(o.x * s.x + off.x, o.y * s.y + off.y, o.z * s.z + off.z);
-        V3 td = v3(d.x * s.x, d.y * s.y, d.z * s.z);
-        float t;
-        bool ent;
-        if (sphere_t(to, td, t, ent)) take(t, keyof(s.w), bt, bk);
-    }
-    for (int i = 0; i < S.n_gsph; ++i) {
-        cfloat4* r = cptr(S.gsph) + 4 * i;
-        float4 r0 = r[0], r1 = r[1], r2 = r[2], rk = r[3];
-        V3 to = pt_mul(r0, r1, r2, o);
-        V3 td = vec3_mul(r0, r1, r2, d);
-        float t;
-        bool ent;
-        if (sphere_t(to, td, t, ent)) take(t, keyof(rk.x), bt, bk);
-    }
-    for (int i = 0; i < S.n_tri; ++i) {
-        cfloat4* r = cptr(S.tri) + 3 * i;
-        float4 a = r[0], b = r[1], c = r[2];
-        float t, u, v, det;
-        if (tri_hit(o, d, xyz(a), xyz(b), xyz(c), t, u, v, det)) take(t, keyof(a.w), bt, bk);
-    }
-    for (int i = 0; i < S.n_cube; ++i) {
-        cfloat4* r = cptr(S.cube) + 4 * i;
-        float4 r0 = r[0], r1 = r[1], r2 = r[2], rk = r[3];
-        V3 to = pt_mul(r0, r1, r2, o);
-        V3 td = vec3_mul(r0, r1, r2, d);
-        uint32_t key0 = keyof(rk.x);
-#pragma unroll 2
-        for (int k = 0; k < 12; ++k) {
-            cfloat4* q = cptr(S.cubetri) + 4 * k;
-            float t, u, v, det;
-            if (tri_hit(to, td, xyz(q[0]), xyz(q[1]), xyz(q[2]), t, u, v, det))
-                take(t, key0 | (uint32_t)k, bt, bk);
-        }
-    }
-}
-
-// ------------------------------------------------------------------ hit attributes
-struct Hit {
-    V3 p, n, eye;
-    float tu, tv;
-    float t;
-    int32_t mat;
-    bool entering;
-};
-
-__device__ __forceinline__ float4 ld4(const float* p) { return make_float4(p[0], p[1], p[2], p[3]); }
-
-// Recompute the full Intersection of the chosen shape with the reference formulas
-// (sphere.rs:57-98, plane.rs:59-84, triangle.rs:51-94, cube.rs:89-102).
-__device__ Hit hit_attrs(const DevScene& S, uint32_t key, V3 o, V3 d, bool need_sphere_tex) {
-    Hit h;
-    const ShapeRec& R = S.shapes[key >> 4];
-    h.mat = R.mat;
-    float4 r0 = ld4(R.inv), r1 = ld4(R.inv + 4), r2 = ld4(R.inv + 8);
-    h.eye = neg(norm(d));
-    h.tu = 0.f;
-    h.tv = 0.f;
-    if (R.kind == RT_SHAPE_SPHERE) {
-        V3 to = pt_mul(r0, r1, r2, o);
-        V3 td = vec3_mul(r0, r1, r2, d);
-        float t = 0.f;
-        bool ent = false;
-        sphere_t(to, td, t, ent);
-        h.t = t;
-        h.entering = ent;
-        h.p = add(o, mul(d, t));
-        V3 on = add(to, mul(td, t));
-        V3 n = norm(tr_vec3_mul(r0, r1, r2, on));
-        if (!ent) n = neg(n);
-        h.n = n;
-        if (need_sphere_tex) {  // sphere.rs:40-45
-            const float PI_F = 3.14159265358979323846f;
-            h.tu = (1.f + atan2f(n.z, n.x) / PI_F) * 0.5f;
-            h.tv = acosf(n.y) / PI_F;
-        }
-    } else if (R.kind == RT_SHAPE_PLANE) {
-        V3 to = pt_mul(r0, r1, r2, o);
-        V3 td = vec3_mul(r0, r1, r2, d);
-        V3 pn = v3(R.a[0], R.a[1], R.a[2]);
-        V3 po = v3(R.a[3], R.a[4], R.a[5]);
-        float t = 0.f;
-        plane_t(to, td, pn, po, t);
-        h.t = t;
-        h.entering = t >= 0.f;
-        h.p = add(o, mul(d, t));
-        h.n = v3(R.a[6], R.a[7], R.a[8]);  // transform * normal, evaluated on the host
-        h.tu = dot(v3(R.a[9], R.a[10], R.a[11]), h.p);
-        h.tv = dot(v3(R.a[12], R.a[13], R.a[14]), h.p);
-    } else if (R.kind == RT_SHAPE_TRIANGLE) {
-        float t = 0.f, u = 0.f, v = 0.f, det = 0.f;
-        tri_hit(o, d, v3(R.a[0], R.a[1], R.a[2]), v3(R.a[3], R.a[4], R.a[5]), v3(R.a[6], R.a[7], R.a[8]),
-                t, u, v, det);
-        h.t = t;
-        h.p = add(o, mul(d, t));
-        h.n = v3(R.a[9], R.a[10], R.a[11]);
-        h.entering = det > 0.f;
-        h.tu = u;
-        h.tv = v;
-    } else {  // cube
-        V3 to = pt_mul(r0, r1, r2, o);
-        V3 td = vec3_mul(r0, r1, r2, d);
-        const float4* q = S.cubetri + 4 * (key & 15u);
-        float t = 0.f, u = 0.f, v = 0.f, det = 0.f;
-        tri_hit(to, td, xyz(q[0]), xyz(q[1]), xyz(q[2]), t, u, v, det);
-        h.t = t;
-        h.p = add(o, mul(d, t));
-        h.n = norm(tr_vec3_mul(r0, r1, r2, xyz(q[3])));
-        h.entering = det > 0.f;
-        h.tu = u;
-        h.tv = v;
-    }
-    return h;
-}
-
-// Saturating f32 -> i32 cast (Rust `as i32`: NaN -> 0)
-__device__ __forceinline__ int32_t sat_i32(float x) {
-    if (x != x) return 0;
-    if (x >= 2147483648.f) return 2147483647;
-    if (x <= -2147483648.f) return (int32_t)0x80000000u;
-    return (int32_t)x;
-}
-
-// texture programs: CONST colour, or my_scene.rs:26-43 checkerboard
-__device__ __forceinline__ V3 tex_eval(const TexRec& t, float tu, float tv) {
-    if (t.kind == RT_TEX_CHECKERBOARD) {
-        int32_t u = sat_i32(fabsf(tu));
-        int32_t v = sat_i32(fabsf(tv));
-        bool same = (tu < 0.f && tv < 0.f) || (tu > 0.f && tv > 0.f);
-        bool white = same ? ((u % 2) == (v % 2)) : ((u % 2) != (v % 2));
-        float c = white ? 1.f : 0.5f * 1.f;
-        return v3(c, c, c);
-    }
-    return v3(t.r, t.g, t.b);
-}
-
-// render.rs:129-134; powi(5) = x * ((x*x)*(x*x)) (LLVM's square-and-multiply expansion)
-__device__ __forceinline__ float fresnel_reflection(V3 l, V3 n, float n1, float n2) {
-    float m_dot_r = dot(l, n);
-    float q = (n1 - n2) / (n1 + n2);
-    float r0 = q * q;
-    float x = 1.f - m_dot_r;
-    float x2 = x * x;
-    float p5 = x * (x2 * x2);
-    return r0 + (1.f - r0) * p5;
-}
-
-// Phong::get_reflected_energy (material.rs:77-93): lambert + phong, per channel
-//   ((l.n * E) * Kd) + ((m.h ^ power * E) * Ks)   (phong term BLACK when m.h < 0)
-__device__ __forceinline__ V3 reflected_energy(V3 E, V3 l, const Hit& h, V3 kd, V3 ks, float power) {
-    float ln = dot(l, h.n);
-    V3 hv = norm(add(norm(h.eye), norm(l)));
-    float mh = dot(h.n, hv);
-    V3 spec = v3(0.f, 0.f, 0.f);
-    if (!(mh < 0.f)) {
-        float pw = powf(mh, power);
-        spec = v3((pw * E.x) * ks.x, (pw * E.y) * ks.y, (pw * E.z) * ks.z);
-    }
-    return v3((ln * E.x) * kd.x + spec.x, (ln * E.y) * kd.y + spec.y, (ln * E.z) * kd.z + spec.z);
-}
-
-// Continuation frame of a tree node whose children are still being traced.
-struct Frame {
-    float ax, ay, az;       // ambient + lights
-    float fr, dr, pw, ft;   // reflected: fresnel, rdir.n, (m.h)^power; refracted: 1 - fresnel
-    float kdx, kdy, kdz, ksx, ksy, ksz;
-    float erx, ery, erz;    // colour returned by the reflection child
-    float rox, roy, roz, rdx, rdy, rdz;  // pending refraction ray
-    uint32_t flags;
-};
-enum : uint32_t {
-    F_REFL = 1u,       // reflectivity > EPS: a reflected term exists
-    F_SPEC = 2u,       // its phong part is not BLACK (m.h >= 0)
-    F_REFR = 4u,       // refraction_index > EPS: a refracted term exists
-    F_TIR = 8u,        // ... but refract_ray returned None
-    F_WAIT_REFL = 16u, // waiting for the reflection child
-    F_WAIT_REFR = 32u, // waiting for (or about to trace) the refraction child
-    F_PEND_REFR = 64u  // refraction child still to be traced after the reflection child
-};
-
-// ((ambient + lights) + reflected) + refracted, render.rs:100
-__device__ __forceinline__ V3 combine(const Frame& f, V3 er, V3 et) {
-    V3 c = v3(f.ax, f.ay, f.az);
-    if (f.flags & F_REFL) {
-        V3 sp = v3(0.f, 0.f, 0.f);
-        if (f.flags & F_SPEC) sp = v3((f.pw * er.x) * f.ksx, (f.pw * er.y) * f.ksy, (f.pw * er.z) * f.ksz);
-        V3 d = v3((f.dr * er.x) * f.kdx + sp.x, (f.dr * er.y) * f.kdy + sp.y, (f.dr * er.z) * f.kdz + sp.z);
-        c = add(c, v3(f.fr * d.x, f.fr * d.y, f.fr * d.z));
-    } else {
-        c = add(c, v3(0.f, 0.f, 0.f));
-    }
-    if (f.flags & F_REFR) {
-        V3 inner = v3(0.f, 0.f, 0.f);
-        if (!(f.flags & F_TIR)) inner = v3(f.ft * et.x, f.ft * et.y, f.ft * et.z);
-        c = add(c, v3(f.kdx * inner.x, f.kdy * inner.y, f.kdz * inner.z));
-    } else {
-        c = add(c, v3(0.f, 0.f, 0.f));
-    }
-    return c;
-}
-
-__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 template <int MAXF>
 __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
@@ -395,7 +48,8 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
     int32_t lvl = 0;       // tree level of the current node
     int32_t phase = 0;     // 0 = node scan, 1 = shadow scan for light `li`
     int32_t li = 0;
-    unsigned long long n_node = 0, n_shadow = 0, n_pix = 0;
+    // wave-uniform counters (SGPRs): scans by kind, pixels, loop iterations
+    unsigned long long n_node = 0, n_shadow = 0, n_pix = 0, n_iter = 0;
 
     // node being shaded
     Hit h;
@@ -415,6 +69,7 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
             uint32_t base = 0;
             if (lane == first) base = atomicAdd(P.work_counter, cnt);
             base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
+            bool got = false;
             if (item < 0 && !exhausted) {
                 uint32_t rank_in = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
@@ -428,8 +83,8 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
                     uint32_t band = lr / P.band_rows;
                     uint32_t v = (band * P.world + P.rank) * P.band_rows + (lr - band * P.band_rows);
                     if (u < P.width && lr < P.rows_local && v < P.height) {
+                        got = true;
                         out_idx = (lr * P.width + u) * 3u;
-                        n_pix++;
                         if (P.depth == 0) {  // trace_ray(.., 0) == BLACK
                             P.out[out_idx] = 0.f;
                             P.out[out_idx + 1] = 0.f;
@@ -447,8 +102,14 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
                     }
                 }
             }
+            n_pix += (unsigned long long)__builtin_popcountll(__ballot(got));
         }
-        if (__ballot(item >= 0) == 0) break;
+        uint64_t active = __ballot(item >= 0);
+        if (active == 0) break;
+        uint64_t node_lanes = __ballot(item >= 0 && phase == 0);
+        n_iter++;
+        n_node += (unsigned long long)__builtin_popcountll(node_lanes);
+        n_shadow += (unsigned long long)__builtin_popcountll(active & ~node_lanes);
         if (item < 0) continue;
 
         // ---- one scene scan
@@ -464,7 +125,6 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
         V3 ret = v3(0.f, 0.f, 0.f);
 
         if (phase == 0) {
-            n_node++;
             if (!hit) {
                 returning = true;  // trace_ray -> BLACK
             } else {
@@ -484,7 +144,6 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
                 node_done = true;  // unless a point light needs a shadow scan (below)
             }
         } else {
-            n_shadow++;
             const LightRec& L = S.lights[li];
             V3 lpos = v3(L.px, L.py, L.pz);
             bool shadowed = hit && (len2(sub(add(ps, mul(sd, bt)), ps)) < len2(sub(lpos, ps)));
@@ -613,17 +272,13 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
         }
     }
 
-    // ---- counters: one atomic per wave
-    for (int off = 32; off > 0; off >>= 1) {
-        n_node += __shfl_xor(n_node, off);
-        n_shadow += __shfl_xor(n_shadow, off);
-        n_pix += __shfl_xor(n_pix, off);
-    }
+    // ---- counters: one atomic per wave (values are wave totals already)
     if (lane == 0 && P.ray_counters) {
         atomicAdd(P.ray_counters + 0, n_node);
         atomicAdd(P.ray_counters + 1, n_shadow);
         atomicAdd(P.ray_counters + 2, n_pix);
     }
+    if (lane == 0 && P.iter_counter) atomicAdd(P.iter_counter, n_iter);
 }
 
 // Scatter gathered per-rank band buffers into the row-major frame (one block row per frame row).
@@ -657,6 +312,27 @@ __global__ void quantize_kernel(const float* __restrict__ in, size_t n, uint8_t*
 
 // ------------------------------------------------------------------ launch wrappers
 namespace rtdev {
+
+// The scan's compile-time cube triangles must equal the host-built Cube::new table.
+bool rt_cube_table_check(const float* table) {
+    struct T {
+        int k, sx, sy, sz, a, b, c, d, e, f;
+    };
+#define RT_CUBE_ROW(k, sx, sy, sz, a, b, c, d_, e, f) T{k, sx, sy, sz, a, b, c, d_, e, f},
+    const T rows[12] = {RT_CUBE_TRIS(RT_CUBE_ROW)};
+#undef RT_CUBE_ROW
+    for (int k = 0; k < 12; k++) {
+        const float* q = table + 16 * k;  // {v0 -} {e1 -} {e2 -} {n -}
+        const T& r = rows[k];
+        if (r.k != k) return false;
+        const float want[9] = {0.5f * r.sx, 0.5f * r.sy, 0.5f * r.sz, (float)r.a, (float)r.b,
+                               (float)r.c, (float)r.d, (float)r.e, (float)r.f};
+        const float got[9] = {q[0], q[1], q[2], q[4], q[5], q[6], q[8], q[9], q[10]};
+        for (int j = 0; j < 9; j++)
+            if (want[j] != got[j]) return false;
+    }
+    return true;
+}
 
 hipError_t launch_render(const RenderParams& p, int blocks, hipStream_t stream) {
     int maxf = (int)p.depth - 1;

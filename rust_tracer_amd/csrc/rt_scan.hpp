@@ -1,0 +1,290 @@
+// rt_scan.hpp -- the nearest-hit scan of Scene::intersect (scene/mod.rs:98-116), the
+// hot loop of the megakernel.  Included by rt_kernels.hip.
+//
+// Every lane scans the whole primitive list for its own ray; the list is walked with
+// wave-uniform indices, so primitive records arrive through SMEM into SGPRs and are
+// prefetched one group ahead (the s_load of group i+1 is in flight while group i
+// computes).  Two throughput devices, both bit-exact w.r.t. the reference arithmetic:
+//
+//  * 2-wide packed f32 (v_pk_mul_f32 / v_pk_add_f32): spheres and loose triangles are
+//    stored and tested in pairs, each packed instruction evaluating the same reference
+//    expression for two primitives.  Packed f32 ops round exactly like their scalar
+//    forms, so each lane of the pair computes what the reference computes.
+//  * Compile-time cube triangles: the 12 object-space triangles of Cube::new
+//    (cube.rs:21-77) have edges with components in {-1, 0, 1}.  Möller–Trumbore is
+//    instantiated per triangle with those constants as types (`Zero`, `One`, `MinusOne`):
+//    x*1 -> x, x*(-1) -> -x (exact), and terms x*0 are dropped, which changes at most the
+//    SIGN of a zero result -- never a non-zero value and never the outcome of any of the
+//    reference's comparisons (< 0, > 1, |det| < EPS all treat +0 and -0 alike).
+#pragma once
+// (included inside namespace rtdev, after the V3 helpers of rt_kernels.hip)
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 bc(float x) { return f2{x, x}; }
+
+// ------------------------------------------------------------------ zero-typed algebra
+struct Zero {};
+struct One {};
+struct MinusOne {};
+template <int C> struct Unit { typedef Zero type; };
+template <> struct Unit<1> { typedef One type; };
+template <> struct Unit<-1> { typedef MinusOne type; };
+
+__device__ __forceinline__ float mul_(float a, float b) { return a * b; }
+__device__ __forceinline__ Zero mul_(float, Zero) { return Zero{}; }
+__device__ __forceinline__ Zero mul_(Zero, float) { return Zero{}; }
+__device__ __forceinline__ Zero mul_(Zero, Zero) { return Zero{}; }
+__device__ __forceinline__ float mul_(float a, One) { return a; }
+__device__ __forceinline__ float mul_(One, float a) { return a; }
+__device__ __forceinline__ float mul_(float a, MinusOne) { return -a; }
+__device__ __forceinline__ float mul_(MinusOne, float a) { return -a; }
+__device__ __forceinline__ Zero mul_(Zero, One) { return Zero{}; }
+__device__ __forceinline__ Zero mul_(Zero, MinusOne) { return Zero{}; }
+__device__ __forceinline__ Zero mul_(One, Zero) { return Zero{}; }
+__device__ __forceinline__ Zero mul_(MinusOne, Zero) { return Zero{}; }
+
+__device__ __forceinline__ float add_(float a, float b) { return a + b; }
+__device__ __forceinline__ float add_(float a, Zero) { return a; }
+__device__ __forceinline__ float add_(Zero, float b) { return b; }
+__device__ __forceinline__ Zero add_(Zero, Zero) { return Zero{}; }
+__device__ __forceinline__ float sub_(float a, float b) { return a - b; }
+__device__ __forceinline__ float sub_(float a, Zero) { return a; }
+__device__ __forceinline__ float sub_(Zero, float b) { return -b; }
+__device__ __forceinline__ Zero sub_(Zero, Zero) { return Zero{}; }
+__device__ __forceinline__ float val_(float a) { return a; }
+__device__ __forceinline__ float val_(Zero) { return 0.f; }
+
+// Möller–Trumbore (triangle.rs:51-80) on one cube triangle: v0 = 0.5 * (SX, SY, SZ),
+// e1 = (A, B, C), e2 = (D, E, F), all compile-time.  Same expression tree as tri_hit.
+template <int SX, int SY, int SZ, int A, int B, int C, int D, int E, int F>
+__device__ __forceinline__ void cube_tri(V3 o, V3 d, uint32_t key, float& bt, uint32_t& bk) {
+    typename Unit<A>::type e1x; typename Unit<B>::type e1y; typename Unit<C>::type e1z;
+    typename Unit<D>::type e2x; typename Unit<E>::type e2y; typename Unit<F>::type e2z;
+    // pvec = d x e2
+    auto px = sub_(mul_(d.y, e2z), mul_(d.z, e2y));
+    auto py = sub_(mul_(d.z, e2x), mul_(d.x, e2z));
+    auto pz = sub_(mul_(d.x, e2y), mul_(d.y, e2x));
+    float det = val_(add_(add_(mul_(e1x, px), mul_(e1y, py)), mul_(e1z, pz)));
+    if (fabsf(det) < RT_EPS) return;
+    // tvec = o - v0
+    float tx = o.x - 0.5f * (float)SX, ty = o.y - 0.5f * (float)SY, tz = o.z - 0.5f * (float)SZ;
+    float un = val_(add_(add_(mul_(tx, px), mul_(ty, py)), mul_(tz, pz)));
+    float adet = fabsf(det);
+    bool opp = (un < 0.f) != (det < 0.f);
+    bool early = (adet <= 1048576.f) &&
+                 ((opp && (un != 0.f) && (fabsf(un) >= 1.17549435e-38f)) || (fabsf(un) > 2.f * adet));
+    if (early) return;
+    float inv_det = 1.0f / det;
+    float u = un * inv_det;
+    if (u < 0.f || u > 1.f) return;
+    // qvec = tvec x e1
+    auto qx = sub_(mul_(ty, e1z), mul_(tz, e1y));
+    auto qy = sub_(mul_(tz, e1x), mul_(tx, e1z));
+    auto qz = sub_(mul_(tx, e1y), mul_(ty, e1x));
+    float v = val_(add_(add_(mul_(d.x, qx), mul_(d.y, qy)), mul_(d.z, qz))) * inv_det;
+    if (v < 0.f || u + v > 1.f) return;
+    float t = val_(add_(add_(mul_(e2x, qx), mul_(e2y, qy)), mul_(e2z, qz))) * inv_det;
+    if (t < 0.f) return;
+    take(t, key, bt, bk);
+}
+
+// The 12 triangles in the inner scene's order (cube.rs:58-69); v0 signs and edges
+// follow Triangle::new(verts) with e1 = v[1]-v[0], e2 = v[2]-v[0].  rt_scene_create
+// checks this table against the host-computed one (rt_cube_table_check).
+#define RT_CUBE_TRIS(X)                                  \
+    X(0, 1, -1, -1, -1, 0, 0, -1, 1, 0)   /* tf1 v1 v2 v3 */ \
+    X(1, 1, 1, -1, 0, -1, 0, -1, 0, 0)    /* tf2 v0 v1 v3 */ \
+    X(2, 1, -1, 1, -1, 1, 0, 0, 1, 0)     /* tk1 v7 v5 v4 */ \
+    X(3, -1, 1, 1, 1, -1, 0, 0, -1, 0)    /* tk2 v5 v7 v6 */ \
+    X(4, 1, 1, -1, 0, 0, 1, 0, -1, 1)     /* tr1 v0 v4 v7 */ \
+    X(5, 1, -1, 1, 0, 0, -1, 0, 1, -1)    /* tr2 v7 v1 v0 */ \
+    X(6, -1, 1, 1, 0, 0, -1, 0, -1, 0)    /* tl1 v5 v3 v6 */ \
+    X(7, -1, -1, 1, 0, 1, -1, 0, 0, -1)   /* tl2 v6 v3 v2 */ \
+    X(8, -1, 1, 1, 1, 0, 0, 1, 0, -1)     /* tt1 v5 v4 v0 */ \
+    X(9, 1, 1, -1, -1, 0, 0, -1, 0, 1)    /* tt2 v0 v3 v5 */ \
+    X(10, 1, -1, -1, 0, 0, 1, -1, 0, 1)   /* tb1 v1 v7 v6 */ \
+    X(11, -1, -1, 1, 0, 0, -1, 1, 0, -1)  /* tb2 v6 v2 v1 */
+
+__device__ __forceinline__ void cube_scan(V3 to, V3 td, uint32_t key0, float& bt, uint32_t& bk) {
+#define RT_CUBE_CALL(k, sx, sy, sz, a, b, c, d_, e, f) \
+    cube_tri<sx, sy, sz, a, b, c, d_, e, f>(to, td, key0 | (uint32_t)(k), bt, bk);
+    RT_CUBE_TRIS(RT_CUBE_CALL)
+#undef RT_CUBE_CALL
+}
+
+// ------------------------------------------------------------------ sphere tail
+// sphere.rs:126-145 after the discriminant: returns t for a non-negative discriminant
+__device__ __forceinline__ bool sphere_finish(float a, float b, float c, float discr, float& t_out) {
+    float t0, t1;
+    if (fabsf(discr) < RT_EPS) {
+        float x = -0.5f * b / a;
+        t0 = x;
+        t1 = x;
+    } else {
+        float sq = sqrtf(discr);
+        float q = (b > 0.f) ? -0.5f * (b + sq) : -0.5f * (b - sq);
+        t0 = q / a;
+        t1 = c / q;
+    }
+    if (t0 > t1) {
+        float tmp = t1;
+        t1 = t0;
+        t0 = tmp;
+    }
+    if (t0 < 0.f && t1 < 0.f) return false;
+    t_out = (t0 < 0.f) ? t1 : t0;
+    return true;
+}
+
+// triangle.rs:61-80 for a lane whose det passed and whose u-numerator survived the
+// pre-test
+__device__ __forceinline__ bool tri_finish(V3 d, V3 tv, V3 e1, V3 e2, float det, float un, float& t_out) {
+    float inv_det = 1.0f / det;
+    float u = un * inv_det;
+    if (u < 0.f || u > 1.f) return false;
+    V3 q = cross(tv, e1);
+    float v = dot(d, q) * inv_det;
+    if (v < 0.f || u + v > 1.f) return false;
+    float t = dot(e2, q) * inv_det;
+    if (t < 0.f) return false;
+    t_out = t;
+    return true;
+}
+
+__device__ __forceinline__ bool tri_early(float det, float un) {
+    float adet = fabsf(det);
+    bool opp = (un < 0.f) != (det < 0.f);
+    return (adet <= 1048576.f) &&
+           ((opp && (un != 0.f) && (fabsf(un) >= 1.17549435e-38f)) || (fabsf(un) > 2.f * adet));
+}
+
+// ------------------------------------------------------------------ record views
+// Pair records (64 B / 96 B) are read as float4 groups from the constant address space.
+struct SphPair {  // 16 floats
+    float4 q0, q1, q2, q3;
+};
+struct TriPair {  // 24 floats
+    float4 q0, q1, q2, q3, q4, q5;
+};
+struct Rec16 {  // a general sphere or cube: inverse rows 0..2 + key
+    float4 r0, r1, r2, rk;
+};
+
+__device__ __forceinline__ SphPair ld_sph(cfloat4* p) { return SphPair{p[0], p[1], p[2], p[3]}; }
+__device__ __forceinline__ TriPair ld_tri(cfloat4* p) { return TriPair{p[0], p[1], p[2], p[3], p[4], p[5]}; }
+__device__ __forceinline__ Rec16 ld_rec(cfloat4* p) { return Rec16{p[0], p[1], p[2], p[3]}; }
+
+// diag sphere pair: {sxA sxB syA syB} {szA szB oxA oxB} {oyA oyB ozA ozB} {keyA keyB - -}
+__device__ __forceinline__ void sph_pair(const SphPair& R, V3 o, V3 d, float& bt, uint32_t& bk) {
+    f2 sx = f2{R.q0.x, R.q0.y}, sy = f2{R.q0.z, R.q0.w}, sz = f2{R.q1.x, R.q1.y};
+    f2 ox = f2{R.q1.z, R.q1.w}, oy = f2{R.q2.x, R.q2.y}, oz = f2{R.q2.z, R.q2.w};
+    // translate*scale inverse: pt_mul / vec3_mul with the zero off-diagonal terms dropped
+    f2 tox = bc(o.x) * sx + ox, toy = bc(o.y) * sy + oy, toz = bc(o.z) * sz + oz;
+    f2 tdx = bc(d.x) * sx, tdy = bc(d.y) * sy, tdz = bc(d.z) * sz;
+    f2 a = (tdx * tdx + tdy * tdy) + tdz * tdz;
+    f2 b = 2.f * ((tdx * tox + tdy * toy) + tdz * toz);
+    f2 c = ((tox * tox + toy * toy) + toz * toz) - 1.f;
+    f2 discr = b * b - (4.f * a) * c;
+    bool hA = !(discr.x < 0.f), hB = !(discr.y < 0.f);
+    if (hA || hB) {
+        float t;
+        if (hA && sphere_finish(a.x, b.x, c.x, discr.x, t)) take(t, keyof(R.q3.x), bt, bk);
+        if (hB && sphere_finish(a.y, b.y, c.y, discr.y, t)) take(t, keyof(R.q3.y), bt, bk);
+    }
+}
+
+// general sphere: full pt_mul / vec3_mul with the inverse rows
+__device__ __forceinline__ void sph_general(const Rec16& R, V3 o, V3 d, float& bt, uint32_t& bk) {
+    V3 to = pt_mul(R.r0, R.r1, R.r2, o);
+    V3 td = vec3_mul(R.r0, R.r1, R.r2, d);
+    float a = len2(td);
+    float b = 2.f * dot(td, to);
+    float c = len2(to) - 1.f;
+    float discr = b * b - 4.f * a * c;
+    float t;
+    if (!(discr < 0.f) && sphere_finish(a, b, c, discr, t)) take(t, keyof(R.rk.x), bt, bk);
+}
+
+// loose triangle pair: {v0xA v0xB v0yA v0yB} {v0zA v0zB e1xA e1xB} {e1yA e1yB e1zA e1zB}
+//                      {e2xA e2xB e2yA e2yB} {e2zA e2zB keyA keyB} {- - - -}
+__device__ __forceinline__ void tri_pair(const TriPair& R, V3 o, V3 d, float& bt, uint32_t& bk) {
+    f2 v0x = f2{R.q0.x, R.q0.y}, v0y = f2{R.q0.z, R.q0.w}, v0z = f2{R.q1.x, R.q1.y};
+    f2 e1x = f2{R.q1.z, R.q1.w}, e1y = f2{R.q2.x, R.q2.y}, e1z = f2{R.q2.z, R.q2.w};
+    f2 e2x = f2{R.q3.x, R.q3.y}, e2y = f2{R.q3.z, R.q3.w}, e2z = f2{R.q4.x, R.q4.y};
+    // pvec = d x e2; det = e1 . pvec; tvec = o - v0; un = tvec . pvec
+    f2 px = bc(d.y) * e2z - bc(d.z) * e2y;
+    f2 py = bc(d.z) * e2x - bc(d.x) * e2z;
+    f2 pz = bc(d.x) * e2y - bc(d.y) * e2x;
+    f2 det = (e1x * px + e1y * py) + e1z * pz;
+    f2 tx = bc(o.x) - v0x, ty = bc(o.y) - v0y, tz = bc(o.z) - v0z;
+    f2 un = (tx * px + ty * py) + tz * pz;
+    bool aA = !(fabsf(det.x) < RT_EPS) && !tri_early(det.x, un.x);
+    bool aB = !(fabsf(det.y) < RT_EPS) && !tri_early(det.y, un.y);
+    if (aA || aB) {
+        float t;
+        if (aA && tri_finish(d, v3(tx.x, ty.x, tz.x), v3(e1x.x, e1y.x, e1z.x), v3(e2x.x, e2y.x, e2z.x), det.x,
+                             un.x, t))
+            take(t, keyof(R.q4.z), bt, bk);
+        if (aB && tri_finish(d, v3(tx.y, ty.y, tz.y), v3(e1x.y, e1y.y, e1z.y), v3(e2x.y, e2y.y, e2z.y), det.y,
+                             un.y, t))
+            take(t, keyof(R.q4.w), bt, bk);
+    }
+}
+
+// plane (plane.rs:59-66) with its own inverse: {inv r0} {inv r1} {inv r2} {n key} {origin -}
+__device__ __forceinline__ void plane_one(cfloat4* r, V3 o, V3 d, float& bt, uint32_t& bk) {
+    float4 r0 = r[0], r1 = r[1], r2 = r[2], rn = r[3], ro = r[4];
+    V3 to = pt_mul(r0, r1, r2, o);
+    V3 td = vec3_mul(r0, r1, r2, d);
+    float t;
+    if (plane_t(to, td, xyz(rn), xyz(ro), t)) take(t, keyof(rn.w), bt, bk);
+}
+
+// One pass over every primitive.  Group loops prefetch record i+1 before testing
+// record i; every section is padded by one group so the look-ahead load stays inside
+// the allocation.
+__device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk) {
+    bt = __builtin_huge_valf();
+    bk = 0xFFFFFFFFu;
+    for (int i = 0; i < S.n_plane; ++i) plane_one(cptr(S.plane) + 5 * i, o, d, bt, bk);
+    {
+        cfloat4* p = cptr(S.dsph);
+        SphPair cur = ld_sph(p);
+        for (int i = 0; i < S.n_dsph; ++i) {
+            SphPair nxt = ld_sph(p + 4 * (i + 1));
+            sph_pair(cur, o, d, bt, bk);
+            cur = nxt;
+        }
+    }
+    {
+        cfloat4* p = cptr(S.gsph);
+        Rec16 cur = ld_rec(p);
+        for (int i = 0; i < S.n_gsph; ++i) {
+            Rec16 nxt = ld_rec(p + 4 * (i + 1));
+            sph_general(cur, o, d, bt, bk);
+            cur = nxt;
+        }
+    }
+    {
+        cfloat4* p = cptr(S.tri);
+        TriPair cur = ld_tri(p);
+        for (int i = 0; i < S.n_tri; ++i) {
+            TriPair nxt = ld_tri(p + 6 * (i + 1));
+            tri_pair(cur, o, d, bt, bk);
+            cur = nxt;
+        }
+    }
+    {
+        cfloat4* p = cptr(S.cube);
+        Rec16 cur = ld_rec(p);
+        for (int i = 0; i < S.n_cube; ++i) {
+            Rec16 nxt = ld_rec(p + 4 * (i + 1));
+            V3 to = pt_mul(cur.r0, cur.r1, cur.r2, o);
+            V3 td = vec3_mul(cur.r0, cur.r1, cur.r2, d);
+            cube_scan(to, td, keyof(cur.rk.x), bt, bk);
+            cur = nxt;
+        }
+    }
+}
+

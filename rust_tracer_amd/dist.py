@@ -1,0 +1,79 @@
+"""Multi-GPU frame tiling: one process per GPU, rows dealt in block-cyclic bands,
+assembled on rank 0 with one RCCL gather over xGMI.
+
+The reference renders serially on one core (src/render.rs:32-37) and has no
+distributed path; this is the MI355X-native scale-out of that loop.  Pixels are
+independent, so the only exchange step is assembling the frame:
+
+  band b (rows [b*B, (b+1)*B)) belongs to rank b % world       (load balance: costly
+  glass-sphere rows are spread over every rank)
+  each rank renders its bands back to back into a [rows_per_rank, W, 3] buffer
+  torch.distributed.gather (backend "nccl" == RCCL) -> rank 0: [world, rows_per_rank, W, 3]
+  rank 0: HIP unpermute kernel -> row-major [H, W, 3] frame
+"""
+import torch
+import torch.distributed as dist
+
+from . import DeviceScene, abi, band_rows_per_rank, unpermute_bands_async
+
+
+def band_rows_per_rank_py(y_res, band_rows, world):
+    """Pure-Python statement of rt_band_rows_per_rank (include/rt_api.h)."""
+    n_bands = (y_res + band_rows - 1) // band_rows
+    return ((n_bands + world - 1) // world) * band_rows
+
+
+def local_rows(y_res, band_rows, rank, world):
+    """Global row index of each local row of `rank` (-1 for padding)."""
+    rpr = band_rows_per_rank_py(y_res, band_rows, world)
+    rows = []
+    for lr in range(rpr):
+        band = lr // band_rows
+        v = (band * world + rank) * band_rows + (lr - band * band_rows)
+        rows.append(v if v < y_res else -1)
+    return rows
+
+
+class FrameTiler:
+    """Renders this rank's share of a frame and gathers the frame on rank 0."""
+
+    def __init__(self, scene: DeviceScene, width, height, depth, band_rows=8, rank=0, world=1,
+                 device=None):
+        self.scene = scene
+        self.w, self.h, self.depth = width, height, depth
+        self.band_rows, self.rank, self.world = band_rows, rank, world
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.rpr = band_rows_per_rank(height, band_rows, world)
+        assert self.rpr == band_rows_per_rank_py(height, band_rows, world)
+        self.cam = abi.camera(width, height)
+        self.local = torch.zeros((self.rpr, width, 3), dtype=torch.float32, device=self.device)
+        self.counters = torch.zeros(3, dtype=torch.int64, device=self.device)
+        self.gathered = None
+        self.frame = None
+        if rank == 0 and world > 1:
+            self.gathered = torch.zeros((world, self.rpr, width, 3), dtype=torch.float32,
+                                        device=self.device)
+            self.frame = torch.zeros((height, width, 3), dtype=torch.float32, device=self.device)
+        elif world == 1:
+            self.frame = self.local[:height]
+
+    def render_local(self):
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        self.scene.render_bands_async(self.cam, self.depth, self.band_rows, self.rank, self.world,
+                                      self.local.data_ptr(), self.counters.data_ptr(), stream)
+
+    def assemble(self):
+        """Gather every rank's bands on rank 0 and restore row order (no-op at world 1)."""
+        if self.world == 1:
+            return self.frame
+        glist = list(self.gathered.unbind(0)) if self.rank == 0 else None
+        dist.gather(self.local, gather_list=glist, dst=0)
+        if self.rank == 0:
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            unpermute_bands_async(self.gathered.data_ptr(), self.w, self.h, self.band_rows,
+                                  self.world, self.frame.data_ptr(), stream)
+        return self.frame
+
+    def step(self):
+        self.render_local()
+        return self.assemble()

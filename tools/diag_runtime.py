@@ -19,4 +19,7 @@ elif mode == "timing":
         s = DeviceScene(SceneDesc.synth_config(cfg))
         for i in range(4):
             img, c, ms, _ = s.render(1920,1080,depth)
-            print(cfg, depth, "kernel_ms %.3f" % ms, c, "Mpix/s %.1f" % (1920*1080/ms/1e3), "flops/scan", s.flops_per_scan, flush=True)
+            util = (c["node_rays"] + c["shadow_rays"]) / (64.0 * max(1, s.last_wave_iterations))
+            tf = (c["node_rays"] + c["shadow_rays"]) * s.flops_per_scan / (ms / 1e3) / 1e12
+            print(cfg, depth, "kernel_ms %.3f" % ms, c, "Mpix/s %.1f" % (1920*1080/ms/1e3),
+                  "lane_util %.3f" % util, "alg TFLOP/s %.2f" % tf, flush=True)
