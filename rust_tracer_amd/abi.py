@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librt_hip.so")
+LIB_PATH = os.environ.get("RT_LIB") or os.path.join(HERE, "librt_hip.so")  # RT_LIB: A/B tooling
 
 RT_OK = 0
 STATUS_NAMES = {

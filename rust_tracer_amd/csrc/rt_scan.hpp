@@ -19,6 +19,19 @@
 #pragma once
 // (included inside namespace rtdev, after the V3 helpers of rt_kernels.hip)
 
+// RT_STATS builds (tools only) count, per wave, how often each divergent hit path of the
+// scan is entered; the counts go to rt_scan_stats (see tools/scan_stats.py).
+#ifndef RT_STATS
+#define RT_STATS 0
+#endif
+#if RT_STATS
+__device__ unsigned long long rt_scan_stats[8];
+#define RT_STAT(i) do { if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == \
+    (uint32_t)__builtin_ctzll(__ballot(1))) atomicAdd(&rt_scan_stats[i], 1ull); } while (0)
+#else
+#define RT_STAT(i) do { } while (0)
+#endif
+
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 bc(float x) { return f2{x, x}; }
@@ -75,6 +88,7 @@ __device__ __forceinline__ void cube_tri(V3 o, V3 d, uint32_t key, float& bt, ui
     bool early = (adet <= 1048576.f) &&
                  ((opp && (un != 0.f) && (fabsf(un) >= 1.17549435e-38f)) || (fabsf(un) > 2.f * adet));
     if (early) return;
+    RT_STAT(4);
     float inv_det = 1.0f / det;
     float u = un * inv_det;
     if (u < 0.f || u > 1.f) return;
@@ -188,6 +202,7 @@ __device__ __forceinline__ void sph_pair(const SphPair& R, V3 o, V3 d, float& bt
     f2 discr = b * b - (4.f * a) * c;
     bool hA = !(discr.x < 0.f), hB = !(discr.y < 0.f);
     if (hA || hB) {
+        RT_STAT(1);
         float t;
         if (hA && sphere_finish(a.x, b.x, c.x, discr.x, t)) take(t, keyof(R.q3.x), bt, bk);
         if (hB && sphere_finish(a.y, b.y, c.y, discr.y, t)) take(t, keyof(R.q3.y), bt, bk);
@@ -203,7 +218,10 @@ __device__ __forceinline__ void sph_general(const Rec16& R, V3 o, V3 d, float& b
     float c = len2(to) - 1.f;
     float discr = b * b - 4.f * a * c;
     float t;
-    if (!(discr < 0.f) && sphere_finish(a, b, c, discr, t)) take(t, keyof(R.rk.x), bt, bk);
+    if (!(discr < 0.f)) {
+        RT_STAT(2);
+        if (sphere_finish(a, b, c, discr, t)) take(t, keyof(R.rk.x), bt, bk);
+    }
 }
 
 // loose triangle pair: {v0xA v0xB v0yA v0yB} {v0zA v0zB e1xA e1xB} {e1yA e1yB e1zA e1zB}
@@ -222,6 +240,7 @@ __device__ __forceinline__ void tri_pair(const TriPair& R, V3 o, V3 d, float& bt
     bool aA = !(fabsf(det.x) < RT_EPS) && !tri_early(det.x, un.x);
     bool aB = !(fabsf(det.y) < RT_EPS) && !tri_early(det.y, un.y);
     if (aA || aB) {
+        RT_STAT(3);
         float t;
         if (aA && tri_finish(d, v3(tx.x, ty.x, tz.x), v3(e1x.x, e1y.x, e1z.x), v3(e2x.x, e2y.x, e2z.x), det.x,
                              un.x, t))
@@ -247,6 +266,7 @@ __device__ __forceinline__ void plane_one(cfloat4* r, V3 o, V3 d, float& bt, uin
 __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk) {
     bt = __builtin_huge_valf();
     bk = 0xFFFFFFFFu;
+    RT_STAT(0);
     for (int i = 0; i < S.n_plane; ++i) plane_one(cptr(S.plane) + 5 * i, o, d, bt, bk);
     {
         cfloat4* p = cptr(S.dsph);

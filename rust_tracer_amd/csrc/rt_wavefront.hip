@@ -304,3 +304,16 @@ hipError_t launch_wave_combine(const WaveParams& p, uint32_t level, int blocks, 
 }
 
 }  // namespace rtdev
+
+#if RT_STATS
+// tools/scan_stats.py: read (and optionally reset) the wavefront pipeline's scan counters
+extern "C" int rt_debug_scan_stats(unsigned long long* out8, int reset) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(rtdev::rt_scan_stats), 8 * sizeof(unsigned long long)) != hipSuccess)
+        return 1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(rtdev::rt_scan_stats), z, sizeof(z)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif

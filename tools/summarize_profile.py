@@ -1,0 +1,118 @@
+"""Turn a gpurun_out/<tag>/ profiling run (tools/gpu_profile.sh) into committed evidence:
+
+  profiles/<tag>/kernel_stats.csv         rocprofv3 --kernel-trace --stats summary
+  profiles/<tag>/kernel_trace_render.csv  per-dispatch durations of the render kernels
+  profiles/<tag>/pmc_*.csv                the render kernels' PMC rows (SQ, FETCH_SIZE, WRITE_SIZE)
+  profiles/<tag>/summary.md               what the numbers say
+  profiles/pmc_traffic.json               HBM bytes per frame, read by bench.py (`traffic`)
+
+usage: python tools/summarize_profile.py TAG
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RENDER = ("trace_level_kernel", "combine_level_kernel", "wave_init_kernel", "render_kernel")
+
+
+def main(tag):
+    src = os.path.join(ROOT, "gpurun_out", tag)
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    rows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))))
+    keep = [r for r in rows if any(k in r["Kernel_Name"] for k in RENDER)]
+    fields = ["Dispatch_Id", "Kernel_Name", "Start_Timestamp", "End_Timestamp", "VGPR_Count", "SGPR_Count",
+              "Scratch_Size", "Grid_Size_X", "Workgroup_Size_X"]
+    with open(os.path.join(dst, "kernel_trace_render.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=fields + ["Duration_ns"])
+        w.writeheader()
+        for r in keep:
+            d = {k: r[k] for k in fields}
+            d["Duration_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            w.writerow(d)
+    bench = json.load(open(os.path.join(src, "bench.json")))
+    steps_prof = 1  # the PMC passes run bench.py --steps 1 --warmup 0: one frame
+    pmc = {}
+    for p in ("pmc_sq", "pmc_fetch", "pmc_write"):
+        rr = list(csv.DictReader(open(os.path.join(src, p, "run_counter_collection.csv"))))
+        kept = [r for r in rr if any(k in r["Kernel_Name"] for k in RENDER)]
+        with open(os.path.join(dst, p + ".csv"), "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+            w.writeheader()
+            for r in kept:
+                w.writerow({k: r[k] for k in ["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"]})
+        agg = defaultdict(float)
+        for r in kept:
+            agg[r["Counter_Name"]] += float(r["Counter_Value"])
+        pmc.update(agg)
+    # kernel-trace: per-frame time of each render kernel family (the trace run did 1 + 3 frames)
+    per = defaultdict(list)
+    for r in keep:
+        name = next(k for k in RENDER if k in r["Kernel_Name"])
+        per[name].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    frames = 4
+    fam_ms = {k: sum(v) / frames / 1e6 for k, v in per.items()}
+    fetch_b = pmc.get("FETCH_SIZE", 0.0) * 1024 / steps_prof
+    write_b = pmc.get("WRITE_SIZE", 0.0) * 1024 / steps_prof
+    traffic = {
+        "workload": bench["config"]["workload"],
+        "bytes_per_launch": fetch_b * 2 + write_b,
+        "launch": "one frame of the render pipeline (all trace + combine dispatches)",
+        "fetch_size_bytes_raw": fetch_b,
+        "fetch_size_bytes_x2": fetch_b * 2,
+        "write_size_bytes": write_b,
+        "correction": "FETCH_SIZE x 2 per MI355X_MICROARCH.md (gfx950 tallies 128-B requests at 64 B); "
+                      "WRITE_SIZE as reported",
+        "source": f"profiles/{tag}/pmc_fetch.csv, pmc_write.csv",
+    }
+    json.dump(traffic, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+    sq = {k: v for k, v in pmc.items() if k.startswith("SQ_")}
+    frame_ms = bench["roofline"]["kernel_ms"]
+    lines = [
+        f"# Profile {tag}: {bench['config']['workload']}",
+        "",
+        f"bench.py: **{bench['value']} Mpixels/s**, {bench['ms_per_step']} ms/frame, render pipeline "
+        f"{frame_ms} ms (HIP events), algorithmic {bench['roofline']['achieved']} TFLOP/s = "
+        f"{bench['roofline']['frac']:.3f} of 157.3 (f32 vector peak).",
+        "",
+        "## rocprofv3 --kernel-trace --stats (4 frames: 1 warm-up + 3 timed)",
+        "",
+        "| kernel family | ms per frame |",
+        "|---|---|",
+    ] + [f"| {k} | {v:.3f} |" for k, v in sorted(fam_ms.items(), key=lambda x: -x[1])] + [
+        "",
+        f"Sum of render kernels per frame: {sum(fam_ms.values()):.3f} ms (bench HIP events: {frame_ms} ms).",
+        "",
+        "## PMC (one frame, separate passes, render kernels only)",
+        "",
+        "| counter | value |",
+        "|---|---|",
+    ] + [f"| {k} | {v:.4g} |" for k, v in sorted(sq.items())] + [
+        f"| FETCH_SIZE (KB) | {pmc.get('FETCH_SIZE', 0):.6g} |",
+        f"| WRITE_SIZE (KB) | {pmc.get('WRITE_SIZE', 0):.6g} |",
+        "",
+        f"HBM traffic per frame: {traffic['bytes_per_launch'] / 1e6:.1f} MB (FETCH x2 + WRITE) -> "
+        f"{traffic['bytes_per_launch'] / (frame_ms / 1e3) / 1e9:.1f} GB/s = "
+        f"{traffic['bytes_per_launch'] / (frame_ms / 1e3) / 8e12 * 100:.3f} % of 8 TB/s.",
+    ]
+    if "SQ_INSTS_VALU" in sq and "SQ_WAVE_CYCLES" in sq:
+        lines += [
+            "",
+            f"VALU instructions per frame: {sq['SQ_INSTS_VALU']:.3g}; SALU {sq.get('SQ_INSTS_SALU', 0):.3g}; "
+            f"SMEM {sq.get('SQ_INSTS_SMEM', 0):.3g}.  Wave-cycle shares: active VALU "
+            f"{sq.get('SQ_ACTIVE_INST_VALU', 0) / sq['SQ_WAVE_CYCLES']:.2f}, waiting (s_waitcnt) "
+            f"{sq.get('SQ_WAIT_ANY', 0) / sq['SQ_WAVE_CYCLES']:.2f}, issue-stalled "
+            f"{sq.get('SQ_WAIT_INST_ANY', 0) / sq['SQ_WAVE_CYCLES']:.2f}.",
+        ]
+    open(os.path.join(dst, "summary.md"), "w").write("\n".join(lines) + "\n")
+    shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, "bench.json"))
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
