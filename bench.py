@@ -47,6 +47,9 @@ def parse():
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU oracle timing")
     p.add_argument("--cpu-rows-step", type=int, default=24,
                    help="CPU baseline renders every k-th row of the frame")
+    p.add_argument("--backend", default="nccl", help="nccl (RCCL) or gloo (CPU rehearsal)")
+    p.add_argument("--check", type=int, default=0,
+                   help="rank 0 compares the assembled frame with a single-launch render")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="rocprofv3 FETCH_SIZE/WRITE_SIZE summary for the render kernel")
     return p.parse_args()
@@ -92,8 +95,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # one process per GPU; ranks share a device only in a --backend gloo rehearsal
+        torch.cuda.set_device(local_rank % torch.cuda.device_count())
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+        else:
+            dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -107,7 +114,10 @@ def main():
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[dev.index])
+            if args.backend == "nccl":
+                dist.barrier(device_ids=[dev.index])
+            else:
+                dist.barrier()
 
     for _ in range(args.warmup):
         tiler.step()
@@ -132,10 +142,21 @@ def main():
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     cnt = tiler.counters.double()
     local_scans = float(cnt[0] + cnt[1]) / args.steps   # this rank's launch (for the roofline)
-    stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    red_dev = dev if args.backend == "nccl" else torch.device("cpu")
+    stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=red_dev)
+    cnt = cnt.to(red_dev)
     if world > 1:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
         dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+    frame_check = None
+    if args.check:
+        frame = tiler.step()
+        torch.cuda.synchronize()
+        if rank == 0:
+            import numpy as np
+            ref, _, _, _ = scene.render(args.width, args.height, args.depth, device=dev.index)
+            got = frame.cpu().numpy()
+            frame_check = bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32)))
     elapsed, kernel_ms_max = stats.tolist()
     node_rays, shadow_rays, pixels = cnt.tolist()
 
@@ -156,7 +177,7 @@ def main():
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_F32_TFLOPS, 4),
             "traffic": traffic["bytes_per_launch"] if traffic else None,
-            "kernel": "render_kernel<7>",
+            "kernel": "trace_level_kernel x depth + combine_level_kernel x depth (one frame)",
             "kernel_ms": round(kernel_ms, 4),
             "flops_per_launch": per_launch_flops,
             "ceilings": {"no_fma_contraction": 0.5},
@@ -186,13 +207,17 @@ def main():
                 "workload": workload,
                 "width": args.width, "height": args.height, "depth": args.depth,
                 "leaf_primitives": 1000, "band_rows": args.band_rows,
-                "parallelism": f"row-bands x{world}" + (" + RCCL gather" if world > 1 else ""),
+                "parallelism": f"row-bands x{world}" + ((" + RCCL gather" if args.backend == "nccl"
+                                                          else f" + {args.backend} gather (rehearsal)")
+                                                         if world > 1 else ""),
                 "node_rays_per_frame": node_rays / steps,
                 "shadow_rays_per_frame": shadow_rays / steps,
             },
             "roofline": roofline,
             "cpu_baseline": None,
         }
+        if frame_check is not None:
+            out["frame_check"] = frame_check
         if world == 1 and args.cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, desc)
         print(json.dumps(out), flush=True)

@@ -66,8 +66,17 @@ class FrameTiler:
         """Gather every rank's bands on rank 0 and restore row order (no-op at world 1)."""
         if self.world == 1:
             return self.frame
-        glist = list(self.gathered.unbind(0)) if self.rank == 0 else None
-        dist.gather(self.local, gather_list=glist, dst=0)
+        if dist.get_backend() == "gloo":
+            # CPU rehearsal of the exchange (several ranks sharing one GPU); RCCL runs the
+            # same gather directly on device buffers
+            host = self.local.cpu()
+            glist = [torch.empty_like(host) for _ in range(self.world)] if self.rank == 0 else None
+            dist.gather(host, gather_list=glist, dst=0)
+            if self.rank == 0:
+                self.gathered.copy_(torch.stack(glist))
+        else:
+            glist = list(self.gathered.unbind(0)) if self.rank == 0 else None
+            dist.gather(self.local, gather_list=glist, dst=0)
         if self.rank == 0:
             stream = torch.cuda.current_stream(self.device).cuda_stream
             unpermute_bands_async(self.gathered.data_ptr(), self.w, self.h, self.band_rows,
