@@ -28,7 +28,8 @@ hipError_t launch_unpermute(const float* in, uint32_t x_res, uint32_t y_res, uin
                             uint32_t world, uint32_t rows_per_rank, float* out, hipStream_t stream);
 hipError_t launch_quantize(const float* in, size_t n, uint8_t* out, hipStream_t stream);
 bool rt_cube_table_check(const float* table);
-hipError_t wave_occupancy(int* trace_blocks, int* combine_blocks);
+hipError_t wave_occupancy(int* trace_blocks, int* shadow_blocks, int* combine_blocks);
+hipError_t launch_wave_shadow(const WaveParams& p, int blocks, hipStream_t stream);
 hipError_t launch_wave_init(uint32_t* levels, uint32_t n_words, uint32_t total_items, uint32_t* overflow,
                             hipStream_t stream);
 hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream);
@@ -141,6 +142,8 @@ struct Workspace {
     Task* tasks = nullptr;
     NodeRec* nodes = nullptr;
     uint32_t capacity = 0;
+    uint32_t* shadow = nullptr;      // shadow queue
+    uint32_t shadow_capacity = 0;
     uint32_t* levels = nullptr;      // 2 * (RT_MAX_DEPTH + 2) words
     uint32_t* overflow = nullptr;
 };
@@ -166,9 +169,10 @@ struct rt_scene {
     size_t dbytes = 0;
     DevScene S;
     uint64_t flops_per_scan = 0;
+    uint32_t n_point_lights = 0;
     int num_cus = 256;
     int occ[3] = {0, 0, 0};  // blocks per CU for the MAXF 7 / 15 / 63 variants
-    int occ_trace = 0, occ_combine = 0;
+    int occ_trace = 0, occ_shadow = 0, occ_combine = 0;
     Workspace ws;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -385,11 +389,14 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
         M.diffuse = TexRec{m.diffuse.kind, m.diffuse.color.r, m.diffuse.color.g, m.diffuse.color.b};
         M.specular = TexRec{m.specular.kind, m.specular.color.r, m.specular.color.g, m.specular.color.b};
     }
+    if (d->n_lights > 32) return RT_ERR_UNSUPPORTED;  // shadow results are a 32-bit mask per node
+    uint32_t n_point = 0;
     std::vector<LightRec> lights(d->n_lights);
     for (uint32_t i = 0; i < d->n_lights; i++) {
         const rt_light& l = d->lights[i];
         if (l.kind != RT_LIGHT_POINT && l.kind != RT_LIGHT_AMBIENT) return RT_ERR_INVALID_ARG;
         lights[i] = LightRec{l.kind, l.pos[0], l.pos[1], l.pos[2], l.color.r, l.color.g, l.color.b, 0.f};
+        if (l.kind == RT_LIGHT_POINT) n_point++;
     }
 
     // ---- one allocation, 256-B aligned sections
@@ -444,6 +451,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     S.amb_g = d->ambient.g;
     S.amb_b = d->ambient.b;
     sc->flops_per_scan = flops;
+    sc->n_point_lights = n_point;
     sc->num_cus = g_num_cus(sc->device);
     HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&sc->ev0));
@@ -461,6 +469,7 @@ rt_status rt_scene_destroy(rt_scene* s) {
     if (s->ws.counters) (void)hipFree(s->ws.counters);
     if (s->ws.work) (void)hipFree(s->ws.work);
     if (s->ws.tasks) (void)hipFree(s->ws.tasks);
+    if (s->ws.shadow) (void)hipFree(s->ws.shadow);
     if (s->ws.nodes) (void)hipFree(s->ws.nodes);
     if (s->ws.levels) (void)hipFree(s->ws.levels);
     if (s->ws.overflow) (void)hipFree(s->ws.overflow);
@@ -575,7 +584,19 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
         HIP_TRY(hipMalloc(&w.levels, 2 * (RT_MAX_DEPTH + 2) * sizeof(uint32_t)));
         HIP_TRY(hipMalloc(&w.overflow, 64));
     }
+    // shadow queue: one entry per point light per hit node
+    uint64_t want_sh = std::min<uint64_t>((uint64_t)w.capacity * s->n_point_lights, 0x7FFFFFFFu);
+    if (want_sh == 0) want_sh = 1;
+    if (w.shadow_capacity < want_sh) {
+        if (w.shadow) (void)hipFree(w.shadow);
+        w.shadow = nullptr;
+        w.shadow_capacity = 0;
+        HIP_TRY(hipMalloc(&w.shadow, want_sh * sizeof(uint32_t)));
+        w.shadow_capacity = (uint32_t)want_sh;
+    }
     p.capacity = w.capacity;
+    p.shadow_capacity = w.shadow_capacity;
+    p.shadow = w.shadow;
     p.tasks = w.tasks;
     p.nodes = w.nodes;
     p.levels = w.levels;
@@ -583,16 +604,19 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
     p.out = d_rgb;
     p.ray_counters = d_counters;
     if (s->occ_trace == 0) {
-        int a = 0, b = 0;
-        HIP_TRY(wave_occupancy(&a, &b));
+        int a = 0, b = 0, c = 0;
+        HIP_TRY(wave_occupancy(&a, &b, &c));
         s->occ_trace = a > 0 ? a : 1;
-        s->occ_combine = b > 0 ? b : 1;
+        s->occ_shadow = b > 0 ? b : 1;
+        s->occ_combine = c > 0 ? c : 1;
     }
     int tb = s->num_cus * s->occ_trace;
+    int sb = s->num_cus * s->occ_shadow;
     int cb = s->num_cus * s->occ_combine;
     uint32_t levels = depth > 0 ? depth : 1;
     HIP_TRY(launch_wave_init(w.levels, 2 * (RT_MAX_DEPTH + 2), p.total_items, w.overflow, stream));
     for (uint32_t k = 0; k < levels; k++) HIP_TRY(launch_wave_trace(p, k, tb, stream));
+    HIP_TRY(launch_wave_shadow(p, sb, stream));
     for (uint32_t k = levels; k-- > 0;) HIP_TRY(launch_wave_combine(p, k, cb, stream));
     return RT_OK;
 }

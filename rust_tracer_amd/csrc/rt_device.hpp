@@ -91,17 +91,23 @@ struct Task {
     uint32_t pad;
 };
 
-// One traced tree node: everything render.rs:100 needs to combine it with the colours
-// its children return, plus where to return its own colour.
+// One traced tree node: the shading inputs of render.rs:57-68 (lights are summed later,
+// once the shadow scans have run), the child weights of render.rs:70-98, the colours its
+// children report, and where to report its own colour.  144 B.
 struct NodeRec {
-    float ax, ay, az;          // ambient + lights
-    float fr, dr, pw, ft;      // reflected: fresnel, rdir.n, (m.h)^power; refracted: 1 - fresnel
+    float ambx, amby, ambz;    // material ambient (tex) * scene ambient (render.rs:57)
+    float psx, psy, psz;       // shadow-ray origin: point + 0.0002 * normal (render.rs:147)
+    float nx, ny, nz;          // hit normal
+    float ex, ey, ez;          // eye_dir
     float kdx, kdy, kdz, ksx, ksy, ksz;
+    float power, n1, n2;
+    float fr, dr, pw, ft;      // reflected: fresnel, rdir.n, (m.h)^power; refracted: 1 - fresnel
     float erx, ery, erz;       // colour of the reflected child (0 until it reports)
     float etx, ety, etz;       // colour of the refracted child
     uint32_t flags;
+    uint32_t litmask;          // bit l: point light l is NOT shadowed (set by the shadow pass)
     uint32_t parent;           // as Task::parent; level 0: unused
-    uint32_t pad[3];
+    uint32_t pad[2];
 };
 
 struct WaveParams {
@@ -112,10 +118,13 @@ struct WaveParams {
     uint32_t band_rows, rank, world, rows_local;
     uint32_t tiles_x, total_items;     // level-0 tasks (8x8 tiles over width x rows_local)
     uint32_t capacity;                 // node / task slots
+    uint32_t shadow_capacity;          // shadow-queue slots
     Task* tasks;                       // [capacity]
     NodeRec* nodes;                    // [capacity]
-    uint32_t* levels;                  // [2 * (RT_MAX_DEPTH + 1)]: offset, count per level
-    uint32_t* overflow;                // set when an append would exceed capacity
+    uint32_t* shadow;                  // [shadow_capacity]: (node << 5) | light
+    uint32_t* levels;                  // [2 * (RT_MAX_DEPTH + 2)]: offset, count per level;
+                                       // levels[2 * (RT_MAX_DEPTH + 1)] = shadow-queue count
+    uint32_t* overflow;                // set when an append would exceed a capacity
     float* out;
     unsigned long long* ray_counters;  // [node, shadow, pixels], added to
 };

@@ -308,3 +308,80 @@ __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, u
     }
 }
 
+
+// ------------------------------------------------------------------ shadow scan
+// PointLight::get_energy (scene/mod.rs:189-206): a FULL nearest-hit scan, then
+// "shadowed iff |hit.point - p|^2 < |pos - p|^2".  Exact early exit:
+//  * planes are scanned first; only planes can return t < 0 (plane.rs:62-83 has no
+//    t >= 0 check; spheres and triangles reject t < 0), so after them a lane whose best
+//    t is negative already holds its nearest hit;
+//  * for t >= 0 the reference's distance |(p + d*t) - p|^2 is non-decreasing in t (each
+//    rounded step is monotone), so once ANY hit has distance^2 < |pos - p|^2 the nearest
+//    one does too.
+// A wave leaves the scan when every active lane is decided.  Returns `shadowed`.
+// "hit nearer than the light" for the current best t (the reference's test)
+__device__ __forceinline__ bool shadow_hit(V3 o, V3 d, float bt, float l2) {
+    if (!(bt < __builtin_huge_valf())) return false;
+    return len2(sub(add(o, mul(d, bt)), o)) < l2;
+}
+// the lane's answer can no longer change
+__device__ __forceinline__ bool shadow_decided(V3 o, V3 d, float bt, float l2) {
+    return bt < 0.f || shadow_hit(o, d, bt, l2);
+}
+
+__device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lpos) {
+    const float l2 = len2(sub(lpos, o));
+    float bt = __builtin_huge_valf();
+    uint32_t bk = 0xFFFFFFFFu;
+    for (int i = 0; i < S.n_plane; ++i) plane_one(cptr(S.plane) + 5 * i, o, d, bt, bk);
+    bool done = shadow_decided(o, d, bt, l2);
+    if (__ballot(!done) == 0) goto finish;
+    {
+        cfloat4* p = cptr(S.cube);
+        Rec16 cur = ld_rec(p);
+        for (int i = 0; i < S.n_cube; ++i) {
+            Rec16 nxt = ld_rec(p + 4 * (i + 1));
+            V3 to = pt_mul(cur.r0, cur.r1, cur.r2, o);
+            V3 td = vec3_mul(cur.r0, cur.r1, cur.r2, d);
+            cube_scan(to, td, keyof(cur.rk.x), bt, bk);
+            cur = nxt;
+            if ((i & 3) == 3) {
+                done = shadow_decided(o, d, bt, l2);
+                if (__ballot(!done) == 0) goto finish;
+            }
+        }
+    }
+    {
+        cfloat4* p = cptr(S.dsph);
+        SphPair cur = ld_sph(p);
+        for (int i = 0; i < S.n_dsph; ++i) {
+            SphPair nxt = ld_sph(p + 4 * (i + 1));
+            sph_pair(cur, o, d, bt, bk);
+            cur = nxt;
+            if ((i & 15) == 15) {
+                done = shadow_decided(o, d, bt, l2);
+                if (__ballot(!done) == 0) goto finish;
+            }
+        }
+    }
+    {
+        cfloat4* p = cptr(S.gsph);
+        Rec16 cur = ld_rec(p);
+        for (int i = 0; i < S.n_gsph; ++i) {
+            Rec16 nxt = ld_rec(p + 4 * (i + 1));
+            sph_general(cur, o, d, bt, bk);
+            cur = nxt;
+        }
+    }
+    {
+        cfloat4* p = cptr(S.tri);
+        TriPair cur = ld_tri(p);
+        for (int i = 0; i < S.n_tri; ++i) {
+            TriPair nxt = ld_tri(p + 6 * (i + 1));
+            tri_pair(cur, o, d, bt, bk);
+            cur = nxt;
+        }
+    }
+finish:
+    return shadow_hit(o, d, bt, l2);
+}

@@ -1,33 +1,33 @@
 // rt_wavefront.hip -- level-synchronous render pipeline (the default device path).
 //
-// The reference recursion (render.rs:40-103) is evaluated one TREE LEVEL at a time over
-// the whole frame:
+// The reference recursion (render.rs:40-103) is evaluated breadth first over the frame:
 //
 //   trace(level 0)  every pixel's primary ray (Camera::get_ray, render.rs:178-185)
-//   trace(level k)  every level-k ray in the compacted queue written by level k-1
-//                   - nearest-hit scan (Scene::intersect, scene/mod.rs:98-116)
-//                   - hit attributes, then one shadow scan per point light
-//                     (PointLight::get_energy, mod.rs:189-206) and Phong/Schlick shading
-//                   - node record (ambient + lights, child weights) -> node pool
-//                   - reflected / refracted child rays (render.rs:105-125) appended to the
-//                     level k+1 queue (one wave-aggregated atomic per wave)
-//   combine(level depth-1 .. 0)
-//                   post-order: every node folds the colours its children reported into
-//                   ((ambient + lights) + reflected) + refracted (render.rs:100) and
-//                   reports its colour to its parent's slot; level 0 writes the pixel.
+//   trace(level k)  every level-k ray of the compacted queue written by level k-1:
+//                   nearest-hit scan (Scene::intersect, scene/mod.rs:98-116), attributes
+//                   of the chosen shape, the node's shading inputs -> node pool, one
+//                   shadow-queue entry per point light, reflected / refracted children
+//                   (render.rs:105-125) -> level k+1 queue (one atomic per wave)
+//   shadow          every shadow ray of every level in ONE launch (PointLight::get_energy,
+//                   mod.rs:189-206), exact per-wave early exit (rt_scan.hpp)
+//   combine(L-1..0) per node: lights (render.rs:59-68) from the shadow bits, then
+//                   ((ambient + lights) + reflected) + refracted (render.rs:100) with the
+//                   colours the children reported; the result goes to the parent's slot,
+//                   level 0 writes the pixel.
 //
 // Why levels and not one per-pixel megakernel (rt_kernels.hip): per-pixel ray trees are
 // ragged (median 1 node, p99 31, max > 80 at depth 8 in config 3), so a lane that owns a
-// pixel serialises up to ~350 scans while the average lane has ~110 to do: the frame
-// becomes critical-path bound.  Per level, every queue entry costs the same (one node scan
-// + one scan per light), so lanes stay ~fully occupied, and the post-order combine keeps
-// the reference's exact operation order (pixel values reach |4000| in config 3, so a
-// reassociated "throughput" formulation would break the 1e-4 tolerance).
+// pixel serialises up to ~350 scans while the average lane has ~110: the frame becomes
+// critical-path bound.  Here every queue entry costs one scan, lanes stay full, and the
+// post-order combine keeps the reference's exact operation order (pixel values reach
+// |4000| in config 3, so a reassociated "throughput" formulation would break 1e-4).
 #include "rt_common.hpp"
 
 namespace rtdev {
 
 enum : uint32_t { NODE_HIT = 1u << 8, NODE_MISS = 1u << 9, NODE_NONE = 1u << 10 };
+
+#define RT_SHADOW_COUNT(P) ((P).levels[2 * (RT_MAX_DEPTH + 1)])
 
 struct PixelRef {
     bool valid;
@@ -51,6 +51,26 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
+// wave-aggregated append of `n` (< 64) consecutive slots per lane to a device counter:
+// one atomic per wave, slots in lane order
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, uint32_t n, uint32_t lane) {
+    uint32_t total = 0, mine = 0;
+    uint64_t lt = lanemask_lt();
+    for (int b = 0; b < 6; b++) {
+        uint64_t m = __ballot((n >> b) & 1u);
+        total += (uint32_t)__builtin_popcountll(m) << b;
+        mine += (uint32_t)__builtin_popcountll(m & lt) << b;
+    }
+    uint32_t base = 0;
+    if (total) {
+        uint64_t any = __ballot(n != 0);
+        uint32_t first = (uint32_t)__builtin_ctzll(any);
+        if (lane == first) base = atomicAdd(counter, total);
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
+    }
+    return base + mine;
+}
+
 __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t level) {
     const DevScene& S = P.S;
     const uint32_t off = P.levels[2 * level];
@@ -58,18 +78,20 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
     const uint32_t next_off = off + count;
     if (blockIdx.x == 0 && threadIdx.x == 0) P.levels[2 * (level + 1)] = next_off;
     const uint32_t lane = lane_id();
-    uint32_t n_shadow = 0, n_node = 0, n_pix = 0;  // per lane, reduced at the end
+    uint32_t n_node = 0, n_pix = 0;
+    // point lights: one shadow ray each per hit (mod.rs:189-206); ambient lights: none
+    uint32_t n_point = 0;
+    for (int li = 0; li < S.n_lights; ++li) n_point += S.lights[li].kind == RT_LIGHT_POINT ? 1u : 0u;
 
     const uint32_t stride = gridDim.x * blockDim.x;
-    // whole waves iterate together (the loop bound is rounded up to a wave multiple) so
-    // the wave-aggregated append below always sees every lane
+    // whole waves iterate together so the wave-aggregated appends see every lane
     const uint32_t wave_base = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u;
     for (uint32_t base = wave_base; base < count; base += stride) {
         const uint32_t t = base + lane;
         bool active = t < count;
         V3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
         uint32_t parent = 0;
-        uint32_t n = off + t;
+        const uint32_t n = off + t;
         if (active) {
             if (level == 0) {
                 PixelRef px = pixel_of(P, t);
@@ -96,7 +118,7 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
                 parent = T.parent;
             }
         }
-        bool want_refl = false, want_refr = false;
+        bool want_refl = false, want_refr = false, hit = false;
         V3 rro = v3(0, 0, 0), rrd = v3(0, 0, 0), tro = v3(0, 0, 0), trd = v3(0, 0, 0);
         if (active) {
             n_node++;
@@ -104,8 +126,9 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
             uint32_t bk;
             scan(S, ro, rd, bt, bk);
             if (bk == 0xFFFFFFFFu) {
-                P.nodes[n].flags = NODE_MISS;  // trace_ray -> BLACK; parent slot stays 0
+                P.nodes[n].flags = NODE_MISS;  // trace_ray -> BLACK; the parent slot stays 0
             } else {
+                hit = true;
                 const MatRec& M = S.mats[S.shapes[bk >> 4].mat];
                 Hit h = hit_attrs(S, bk, ro, rd, M.kind == RT_MAT_TEXTURE_PHONG);
                 float ri = M.refraction_index;
@@ -114,39 +137,22 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
                 V3 ka = tex_eval(M.ambient, h.tu, h.tv);
                 V3 kd = tex_eval(M.diffuse, h.tu, h.tv);
                 V3 ks = tex_eval(M.specular, h.tu, h.tv);
-                // render.rs:59-68 with get_light_energy :142-153
-                V3 ps = add(h.p, mul(h.n, 0.0002f));
-                V3 lsum = v3(0.f, 0.f, 0.f);
-                for (int li = 0; li < S.n_lights; ++li) {
-                    const LightRec& L = S.lights[li];
-                    V3 ldir = v3(0.f, 0.f, 0.f);
-                    V3 E = v3(L.r, L.g, L.b);
-                    if (L.kind == RT_LIGHT_POINT) {
-                        V3 lpos = v3(L.px, L.py, L.pz);
-                        ldir = norm(sub(lpos, ps));
-                        float st;
-                        uint32_t sk;
-                        scan(S, ps, ldir, st, sk);
-                        n_shadow++;
-                        if (sk != 0xFFFFFFFFu && len2(sub(add(ps, mul(ldir, st)), ps)) < len2(sub(lpos, ps)))
-                            E = v3(0.f, 0.f, 0.f);
-                    }
-                    float f = fresnel_reflection(ldir, h.n, n1, n2);
-                    V3 g = reflected_energy(E, ldir, h, kd, ks, M.power);
-                    lsum = add(lsum, v3(f * g.x, f * g.y, f * g.z));
-                }
-                V3 amb = v3(ka.x * S.amb_r, ka.y * S.amb_g, ka.z * S.amb_b);
-                V3 loc = add(amb, lsum);
+                V3 ps = add(h.p, mul(h.n, 0.0002f));  // render.rs:147
                 NodeRec rec;
-                rec.ax = loc.x; rec.ay = loc.y; rec.az = loc.z;
-                rec.fr = 0.f; rec.dr = 0.f; rec.pw = 0.f; rec.ft = 0.f;
+                rec.ambx = ka.x * S.amb_r; rec.amby = ka.y * S.amb_g; rec.ambz = ka.z * S.amb_b;
+                rec.psx = ps.x; rec.psy = ps.y; rec.psz = ps.z;
+                rec.nx = h.n.x; rec.ny = h.n.y; rec.nz = h.n.z;
+                rec.ex = h.eye.x; rec.ey = h.eye.y; rec.ez = h.eye.z;
                 rec.kdx = kd.x; rec.kdy = kd.y; rec.kdz = kd.z;
                 rec.ksx = ks.x; rec.ksy = ks.y; rec.ksz = ks.z;
+                rec.power = M.power; rec.n1 = n1; rec.n2 = n2;
+                rec.fr = 0.f; rec.dr = 0.f; rec.pw = 0.f; rec.ft = 0.f;
                 rec.erx = 0.f; rec.ery = 0.f; rec.erz = 0.f;
                 rec.etx = 0.f; rec.ety = 0.f; rec.etz = 0.f;
                 rec.flags = NODE_HIT;
+                rec.litmask = 0u;
                 rec.parent = parent;
-                rec.pad[0] = rec.pad[1] = rec.pad[2] = 0u;
+                rec.pad[0] = rec.pad[1] = 0u;
                 bool child_ok = level + 1 < P.depth;
                 if (M.reflectivity > RT_EPS) {  // render.rs:70-84, reflect_ray :105-110
                     rec.flags |= F_REFL;
@@ -181,52 +187,93 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
                 P.nodes[n] = rec;
             }
         }
-        // ---- append the children to the level+1 queue: one atomic per wave
-        uint64_t bl = __ballot(want_refl), br = __ballot(want_refr);
-        uint32_t total = (uint32_t)(__builtin_popcountll(bl) + __builtin_popcountll(br));
-        if (total) {
-            uint32_t wbase = 0;
-            uint32_t first = (uint32_t)__builtin_ctzll(bl | br);
-            if (lane == first) wbase = atomicAdd(&P.levels[2 * (level + 1) + 1], total);
-            wbase = (uint32_t)__builtin_amdgcn_readlane((int)wbase, (int)first);
-            uint64_t lt = lanemask_lt();
-            uint32_t my = wbase + (uint32_t)(__builtin_popcountll(bl & lt) + __builtin_popcountll(br & lt));
-            if (want_refl) {
-                uint32_t slot = next_off + my;
-                if (slot < P.capacity) {
-                    Task T = {rro.x, rro.y, rro.z, rrd.x, rrd.y, rrd.z, (n << 1) | 0u, 0u};
-                    P.tasks[slot] = T;
-                } else {
-                    atomicOr(P.overflow, 1u);
-                }
-                my++;
+        // ---- children -> level k+1 queue
+        uint32_t nc = (want_refl ? 1u : 0u) + (want_refr ? 1u : 0u);
+        uint32_t my = wave_append(&P.levels[2 * (level + 1) + 1], nc, lane);
+        if (want_refl) {
+            uint32_t slot = next_off + my;
+            if (slot < P.capacity) {
+                Task T = {rro.x, rro.y, rro.z, rrd.x, rrd.y, rrd.z, (n << 1) | 0u, 0u};
+                P.tasks[slot] = T;
+            } else {
+                atomicOr(P.overflow, 1u);
             }
-            if (want_refr) {
-                uint32_t slot = next_off + my;
-                if (slot < P.capacity) {
-                    Task T = {tro.x, tro.y, tro.z, trd.x, trd.y, trd.z, (n << 1) | 1u, 0u};
-                    P.tasks[slot] = T;
-                } else {
-                    atomicOr(P.overflow, 1u);
+            my++;
+        }
+        if (want_refr) {
+            uint32_t slot = next_off + my;
+            if (slot < P.capacity) {
+                Task T = {tro.x, tro.y, tro.z, trd.x, trd.y, trd.z, (n << 1) | 1u, 0u};
+                P.tasks[slot] = T;
+            } else {
+                atomicOr(P.overflow, 1u);
+            }
+        }
+        // ---- one shadow entry per point light, grouped by light within the wave
+        // ([light a: this wave's hits in lane order][light b: ...]) so that a shadow wave
+        // holds rays from neighbouring points towards ONE light
+        uint64_t hits = __ballot(hit);
+        if (hits) {
+            uint32_t nh = (uint32_t)__builtin_popcountll(hits);
+            uint32_t rank_h = (uint32_t)__builtin_popcountll(hits & lanemask_lt());
+            uint32_t first = (uint32_t)__builtin_ctzll(hits);
+            uint32_t sbase = 0;
+            if (lane == first) sbase = atomicAdd(&RT_SHADOW_COUNT(P), nh * n_point);
+            sbase = (uint32_t)__builtin_amdgcn_readlane((int)sbase, (int)first);
+            if (hit) {
+                uint32_t k = 0;
+                for (int li = 0; li < S.n_lights; ++li) {
+                    if (S.lights[li].kind != RT_LIGHT_POINT) continue;
+                    uint32_t slot = sbase + k * nh + rank_h;
+                    k++;
+                    if (slot < P.shadow_capacity)
+                        P.shadow[slot] = (n << 5) | (uint32_t)li;
+                    else
+                        atomicOr(P.overflow, 2u);
                 }
             }
         }
     }
-    // ---- counters: wave reduction, one atomic per wave
     for (int o = 32; o > 0; o >>= 1) {
         n_node += __shfl_xor(n_node, o);
-        n_shadow += __shfl_xor(n_shadow, o);
         n_pix += __shfl_xor(n_pix, o);
     }
     if (lane == 0 && P.ray_counters) {
         if (n_node) atomicAdd(P.ray_counters + 0, (unsigned long long)n_node);
-        if (n_shadow) atomicAdd(P.ray_counters + 1, (unsigned long long)n_shadow);
         if (n_pix) atomicAdd(P.ray_counters + 2, (unsigned long long)n_pix);
     }
 }
 
-// render.rs:100 for every node of `level`; children (level + 1) have already reported.
+// Every shadow ray of the frame: PointLight::get_energy's scan + distance test, result as
+// a bit in the node record.
+__global__ __launch_bounds__(256) void shadow_kernel(WaveParams P) {
+    const DevScene& S = P.S;
+    const uint32_t count = min(RT_SHADOW_COUNT(P), P.shadow_capacity);
+    const uint32_t lane = lane_id();
+    const uint32_t stride = gridDim.x * blockDim.x;
+    uint32_t n_shadow = 0;
+    const uint32_t wave_base = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u;
+    for (uint32_t base = wave_base; base < count; base += stride) {
+        const uint32_t t = base + lane;
+        if (t < count) {
+            uint32_t e = P.shadow[t];
+            uint32_t n = e >> 5, li = e & 31u;
+            const NodeRec& R = P.nodes[n];
+            V3 ps = v3(R.psx, R.psy, R.psz);
+            const LightRec& L = S.lights[li];
+            V3 lpos = v3(L.px, L.py, L.pz);
+            V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
+            n_shadow++;
+            if (!shadow_scan(S, ps, ldir, lpos)) atomicOr(&P.nodes[n].litmask, 1u << li);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) n_shadow += __shfl_xor(n_shadow, o);
+    if (lane == 0 && P.ray_counters && n_shadow) atomicAdd(P.ray_counters + 1, (unsigned long long)n_shadow);
+}
+
+// render.rs:57-68 + :100 for every node of `level`; children (level + 1) already reported.
 __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32_t level) {
+    const DevScene& S = P.S;
     const uint32_t off = P.levels[2 * level];
     const uint32_t count = min(P.levels[2 * level + 1], off < P.capacity ? P.capacity - off : 0u);
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -246,8 +293,27 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
         }
         V3 c = v3(0.f, 0.f, 0.f);
         if (flags & NODE_HIT) {
+            Hit h;
+            h.n = v3(R.nx, R.ny, R.nz);
+            h.eye = v3(R.ex, R.ey, R.ez);
+            V3 ps = v3(R.psx, R.psy, R.psz);
+            V3 kd = v3(R.kdx, R.kdy, R.kdz), ks = v3(R.ksx, R.ksy, R.ksz);
+            V3 lsum = v3(0.f, 0.f, 0.f);  // Sum starts at BLACK (color.rs:164-167)
+            for (int li = 0; li < S.n_lights; ++li) {
+                const LightRec& L = S.lights[li];
+                V3 ldir = v3(0.f, 0.f, 0.f);
+                V3 E = v3(L.r, L.g, L.b);
+                if (L.kind == RT_LIGHT_POINT) {
+                    ldir = norm(sub(v3(L.px, L.py, L.pz), ps));
+                    if (!((R.litmask >> li) & 1u)) E = v3(0.f, 0.f, 0.f);
+                }
+                float f = fresnel_reflection(ldir, h.n, R.n1, R.n2);
+                V3 g = reflected_energy(E, ldir, h, kd, ks, R.power);
+                lsum = add(lsum, v3(f * g.x, f * g.y, f * g.z));
+            }
+            V3 loc = add(v3(R.ambx, R.amby, R.ambz), lsum);
             Frame f;
-            f.ax = R.ax; f.ay = R.ay; f.az = R.az;
+            f.ax = loc.x; f.ay = loc.y; f.az = loc.z;
             f.fr = R.fr; f.dr = R.dr; f.pw = R.pw; f.ft = R.ft;
             f.kdx = R.kdx; f.kdy = R.kdy; f.kdz = R.kdz;
             f.ksx = R.ksx; f.ksy = R.ksy; f.ksz = R.ksz;
@@ -273,7 +339,7 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
     }
 }
 
-// levels[] = {0, total_items, 0, 0, ...}, overflow = 0
+// levels[] = {0, total_items, 0, ...} (incl. the shadow count), overflow 0
 __global__ void wave_init_kernel(uint32_t* levels, uint32_t n_words, uint32_t total_items, uint32_t* overflow) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n_words) levels[i] = (i == 1) ? total_items : 0u;
@@ -287,14 +353,21 @@ hipError_t launch_wave_init(uint32_t* levels, uint32_t n_words, uint32_t total_i
     return hipGetLastError();
 }
 
-hipError_t wave_occupancy(int* trace_blocks, int* combine_blocks) {
+hipError_t wave_occupancy(int* trace_blocks, int* shadow_blocks, int* combine_blocks) {
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(trace_blocks, trace_level_kernel, 256, 0);
+    if (e != hipSuccess) return e;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel, 256, 0);
     if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(combine_blocks, combine_level_kernel, 256, 0);
 }
 
 hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream) {
     hipLaunchKernelGGL(trace_level_kernel, dim3(blocks), dim3(256), 0, stream, p, level);
+    return hipGetLastError();
+}
+
+hipError_t launch_wave_shadow(const WaveParams& p, int blocks, hipStream_t stream) {
+    hipLaunchKernelGGL(shadow_kernel, dim3(blocks), dim3(256), 0, stream, p);
     return hipGetLastError();
 }
 
