@@ -7,7 +7,7 @@ spheres + 25 cubes (300 triangles) + 100 loose triangles + my_scene's 2 textured
 src/render.rs:43-45).  Synthetic scene, no dataset.
 
 A step = one full frame: every rank renders its block-cyclic row bands with the HIP
-megakernel, then (N > 1) the bands are gathered to rank 0 over RCCL and un-permuted.
+level-synchronous pipeline (culling hierarchy + ordered ray queues), then (N > 1) the bands are gathered to rank 0 over RCCL and un-permuted.
 The frame is fixed as N grows ("scaling": "strong").
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -32,6 +32,13 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "Mpixels/sec (primary+8 bounces) at 1920×1080; fraction of HBM roofline"
 PEAK_F32_TFLOPS = 157.3      # MI355X FP32 vector peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBPS = 8000.0       # MI355X HBM3E peak
+# Algorithmic f32 flops of each test the scans count (rt_scene_scan_ops; DESIGN.md
+# "Roofline"): reference arithmetic of the ray-primitive tests (sphere
+# 57, triangle 52, cube 12 x 52 + 33 for the ray transform, plane 49), 12 FMAs = 24 flops
+# per 2-wide child-box test, 45 flops for a cube's object-space box (its transform shared
+# with the triangles), 6 per triangle for the grazing check.
+OP_FLOPS = {"node_pairs": 24, "dsph_pairs": 2 * 57, "gsph": 57, "tri_pairs": 2 * 52,
+            "cube_boxes": 33 + 12, "cubes": 12 * 52, "graze_pairs": 12, "planes": 49}
 
 
 def parse():
@@ -125,13 +132,14 @@ def main():
     barrier()
     torch.cuda.synchronize()
     tiler.counters.zero_()
+    scene.scan_ops(reset=True)
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record()
-        tiler.render_local()       # the megakernel, on torch's current stream
+        tiler.render_local()       # the render pipeline, on torch's current stream
         ev[k][1].record()
         tiler.assemble()
     torch.cuda.synchronize()
@@ -140,6 +148,7 @@ def main():
     elapsed = time.perf_counter() - t0
 
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    ops = scene.scan_ops()                   # this rank's tests over the timed steps
     cnt = tiler.counters.double()
     local_scans = float(cnt[0] + cnt[1]) / args.steps   # this rank's launch (for the roofline)
     red_dev = dev if args.backend == "nccl" else torch.device("cpu")
@@ -163,10 +172,11 @@ def main():
     if rank == 0:
         steps = args.steps
         mpix = args.width * args.height * steps / elapsed / 1e6
-        scans_per_step = (node_rays + shadow_rays) / steps
-        flops_per_step = scans_per_step * scene.flops_per_scan          # SURVEY.md §8(d) F_alg
-        per_launch_flops = local_scans * scene.flops_per_scan          # rank 0's launch
+        # rank 0's launch: the tests its scans ran (culled), at their algorithmic flops
+        per_launch_flops = sum(ops[k] * OP_FLOPS[k] for k in OP_FLOPS) / steps
         achieved = per_launch_flops / (kernel_ms / 1e3) / 1e12
+        # what the reference's linear scan would need for the same rays (F_alg per scan)
+        brute_flops = local_scans * scene.flops_per_scan
         workload = (f"config{args.config}: synth seed 2 (600 spheres, 25 cubes, 100 triangles, "
                     f"2 planes, 3 point lights), {args.width}x{args.height}, depth {args.depth}")
         traffic = load_traffic(args.traffic_json, workload)
@@ -177,9 +187,14 @@ def main():
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_F32_TFLOPS, 4),
             "traffic": traffic["bytes_per_launch"] if traffic else None,
-            "kernel": "trace_level_kernel x depth + combine_level_kernel x depth (one frame)",
+            "kernel": ("one frame: trace_level_kernel per level + queue sorts + shadow_kernel + "
+                       "combine_level_kernel per level"),
             "kernel_ms": round(kernel_ms, 4),
             "flops_per_launch": per_launch_flops,
+            "tests_per_launch": {k: v / steps for k, v in ops.items()},
+            "culling": {"hierarchy": scene.uses_bvh,
+                        "linear_scan_flops_per_launch": brute_flops,
+                        "linear_scan_equivalent_TFLOPs": round(brute_flops / (kernel_ms / 1e3) / 1e12, 3)},
             "ceilings": {"no_fma_contraction": 0.5},
             "hbm": {
                 "algorithmic_bytes_per_launch": scene.device_bytes + args.width * args.height * 12 / world,

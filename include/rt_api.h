@@ -194,6 +194,18 @@ uint64_t rt_scene_flops_per_scan(const rt_scene* scene);
 /* Bytes of the flattened device scene (for the HBM-traffic accounting). */
 uint64_t rt_scene_device_bytes(const rt_scene* scene);
 
+/* Lane-weighted counts of the ray-primitive and ray-box tests the scene's scans ran
+ * since the last reset, in this order: child-box pairs, diagonal-sphere pairs, general
+ * spheres, triangle pairs, cube boxes, full cubes (12 triangles), grazing checks
+ * (triangle pairs), planes.  Synchronises the device; reset != 0 zeroes the counts
+ * after reading.  `out` may be NULL (reset only). */
+#define RT_SCAN_OPS_N 8
+rt_status rt_scene_scan_ops(rt_scene* scene, uint64_t* out, uint32_t n, int32_t reset);
+
+/* 1 if the scene's scans walk the culling hierarchy (the default; RT_BVH=0 in the
+ * environment at rt_scene_create turns it off), 0 if they test every shape. */
+int32_t rt_scene_uses_bvh(const rt_scene* scene);
+
 const char* rt_status_str(rt_status status);
 int32_t rt_api_version(void);
 

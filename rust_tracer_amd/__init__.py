@@ -244,6 +244,21 @@ class DeviceScene:
     def device_bytes(self):
         return int(self._L.rt_scene_device_bytes(self.h))
 
+    @property
+    def uses_bvh(self):
+        """True when scans walk the culling hierarchy (RT_BVH=0 at creation turns it off)."""
+        return bool(self._L.rt_scene_uses_bvh(self.h))
+
+    SCAN_OPS = ("node_pairs", "dsph_pairs", "gsph", "tri_pairs", "cube_boxes", "cubes", "graze_pairs",
+                "planes")
+
+    def scan_ops(self, reset=False):
+        """Lane-weighted test counts since the last reset (rt_scene_scan_ops)."""
+        out = (C.c_uint64 * len(self.SCAN_OPS))()
+        check(self._L.rt_scene_scan_ops(self.h, out, len(self.SCAN_OPS), 1 if reset else 0),
+              "rt_scene_scan_ops")
+        return dict(zip(self.SCAN_OPS, (int(v) for v in out)))
+
     def render(self, x_res, y_res, depth, want_u8=False, device=-1):
         """render.rs:31-38 -> (rgb float32 [y_res, x_res, 3], counters dict, kernel_ms, rgb8)"""
         cam = camera(x_res, y_res)

@@ -129,6 +129,9 @@ def lib():
     L.rt_scene_flops_per_scan.restype = C.c_uint64
     L.rt_scene_device_bytes.argtypes = [vp]
     L.rt_scene_device_bytes.restype = C.c_uint64
+    L.rt_scene_scan_ops.argtypes = [vp, P(C.c_uint64), C.c_uint32, C.c_int32]
+    L.rt_scene_uses_bvh.argtypes = [vp]
+    L.rt_scene_uses_bvh.restype = C.c_int32
     L.rt_status_str.argtypes = [C.c_int32]
     L.rt_status_str.restype = C.c_char_p
     L.rt_api_version.restype = C.c_int32

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -19,6 +20,7 @@
 #include <vector>
 
 #include "../../include/rt_api.h"
+#include "rt_bvh.hpp"
 #include "rt_device.hpp"
 
 namespace rtdev {
@@ -34,6 +36,9 @@ hipError_t launch_wave_init(uint32_t* levels, uint32_t n_words, uint32_t total_i
                             hipStream_t stream);
 hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream);
 hipError_t launch_wave_combine(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream);
+hipError_t sort_pairs_u32(void* tmp, size_t& bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                          const uint32_t* vals_in, uint32_t* vals_out, uint32_t n, int end_bit,
+                          hipStream_t stream);
 }  // namespace rtdev
 
 using namespace rtdev;
@@ -131,6 +136,365 @@ void cube_triangles(std::vector<float>& out) {
     }
 }
 
+// ---- culling hierarchy (rt_bvh.hpp) and the run layout --------------------------------
+struct SphIn {
+    float inv[12];
+    float key;
+    bool diag;
+};
+struct TriIn {
+    F3 v[3], e1, e2;
+    float key;
+};
+struct CubeIn {
+    float inv[12];
+    float key;
+};
+
+struct RunLayout {
+    std::vector<float> dsph, gsph, tri, cube, nodes, tri_nrm;
+    std::vector<uint32_t> leaves;
+    uint32_t root = BVH_LEAF;
+    bool use = false;
+    int n_dsph_bvh = 0, n_gsph_bvh = 0, n_tri_bvh = 0, n_cube_bvh = 0;
+    float c[3] = {0, 0, 0}, r = 0, g2 = 0, g1 = 0, g0 = 0, m1 = 0, m0 = 0;
+};
+
+// RT_BVH=0 turns the hierarchy off (every shape in the linear pass): A/B parity tests.
+bool bvh_enabled() {
+    const char* e = std::getenv("RT_BVH");
+    return !(e && std::strcmp(e, "0") == 0);
+}
+
+// Safety factors over the largest ratios tools/cull_bounds_check.py measures for each
+// bound (sphere 0.43, cube 1.83, triangle lateral 0.30 / along-ray 0.33 for
+// sin(phi) >= 0.01), and the grazing threshold.
+constexpr double SAFETY_SPHERE = 4.0, SAFETY_CUBE = 32.0, SAFETY_TRI = 16.0, SAFETY_TRI_T = 8.0,
+                 SAFETY_SLAB = 4.0;
+constexpr double GRAZE_SIN = 0.01;          // sin(phi_min): below it, the grazing pass
+constexpr double MAX_COND = 100.0;          // sigma_max(L) sigma_max(A) above it: linear pass
+constexpr double MIN_SIN_ALPHA = 0.02;      // sliver triangles: linear pass
+const double FEPS = (double)std::numeric_limits<float>::epsilon();
+
+float down_f(double x) {
+    float f = (float)x;
+    return ((double)f > x) ? std::nextafter(f, -std::numeric_limits<float>::infinity()) : f;
+}
+float up_f(double x) {
+    float f = (float)x;
+    return ((double)f < x) ? std::nextafter(f, std::numeric_limits<float>::infinity()) : f;
+}
+
+struct Geo {          // f64 view of one hierarchy primitive
+    double lo[3], hi[3], c[3], r;   // box, bounding ball
+    double a2, a1, a0;              // inflation coefficients (D-polynomial)
+};
+
+// upper bound of the spectral norm: sqrt(|M^T M|_inf) >= sigma_max (exact for
+// rotation x diagonal matrices)
+double sig_up(const double m[3][3]) {
+    double best = 0;
+    for (int i = 0; i < 3; i++) {
+        double row = 0;
+        for (int j = 0; j < 3; j++) {
+            double g = 0;
+            for (int k = 0; k < 3; k++) g += m[k][i] * m[k][j];
+            row += std::fabs(g);
+        }
+        best = std::max(best, row);
+    }
+    return std::sqrt(best) * (1 + 1e-9);
+}
+bool inv3(const double m[3][3], double o[3][3]) {
+    double c00 = m[1][1] * m[2][2] - m[1][2] * m[2][1], c01 = m[1][2] * m[2][0] - m[1][0] * m[2][2],
+           c02 = m[1][0] * m[2][1] - m[1][1] * m[2][0];
+    double det = m[0][0] * c00 + m[0][1] * c01 + m[0][2] * c02;
+    if (!(std::fabs(det) > 0) || !std::isfinite(det)) return false;
+    double id = 1.0 / det;
+    o[0][0] = c00 * id;
+    o[1][0] = c01 * id;
+    o[2][0] = c02 * id;
+    o[0][1] = (m[0][2] * m[2][1] - m[0][1] * m[2][2]) * id;
+    o[1][1] = (m[0][0] * m[2][2] - m[0][2] * m[2][0]) * id;
+    o[2][1] = (m[0][1] * m[2][0] - m[0][0] * m[2][1]) * id;
+    o[0][2] = (m[0][1] * m[1][2] - m[0][2] * m[1][1]) * id;
+    o[1][2] = (m[0][2] * m[1][0] - m[0][0] * m[1][2]) * id;
+    o[2][2] = (m[0][0] * m[1][1] - m[0][1] * m[1][0]) * id;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            if (!std::isfinite(o[i][j])) return false;
+    return true;
+}
+
+// Sphere (cube == false) or cube: E = { A u + c : |u| <= 1 } (resp. u in [-1/2, 1/2]^3)
+// with A = L^-1, c = -A s for the stored f32 inverse (L | s).  Returns false when the
+// transform is too ill-conditioned for the hierarchy.
+bool geo_affine(const float* inv, bool is_cube, Geo& g, double& sigL, double& snorm, double& sigA) {
+    double L[3][3], A[3][3], s[3];
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) L[i][j] = inv[i * 4 + j];
+        s[i] = inv[i * 4 + 3];
+    }
+    if (!inv3(L, A)) return false;
+    sigL = sig_up(L);
+    sigA = sig_up(A);
+    snorm = std::sqrt(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
+    if (!(sigL * sigA <= MAX_COND) || !std::isfinite(snorm)) return false;
+    for (int i = 0; i < 3; i++) {
+        g.c[i] = -(A[i][0] * s[0] + A[i][1] * s[1] + A[i][2] * s[2]);
+        double h = is_cube ? 0.5 * (std::fabs(A[i][0]) + std::fabs(A[i][1]) + std::fabs(A[i][2]))
+                           : std::sqrt(A[i][0] * A[i][0] + A[i][1] * A[i][1] + A[i][2] * A[i][2]);
+        h = h * (1 + 1e-9) + 1e-30;
+        g.lo[i] = g.c[i] - h;
+        g.hi[i] = g.c[i] + h;
+    }
+    g.r = (is_cube ? 0.5 * std::sqrt(3.0) : 1.0) * sigA * (1 + 1e-9);
+    return std::isfinite(g.r);
+}
+
+void emit_dsph_pair(std::vector<float>& v, const SphIn& A, const SphIn& B) {
+    put4(v, A.inv[0], B.inv[0], A.inv[5], B.inv[5]);
+    put4(v, A.inv[10], B.inv[10], A.inv[3], B.inv[3]);
+    put4(v, A.inv[7], B.inv[7], A.inv[11], B.inv[11]);
+    put4(v, A.key, B.key, 0.f, 0.f);
+}
+void emit_gsph(std::vector<float>& v, const SphIn& A) {  // a diag sphere's rows hold its zeros
+    for (int r = 0; r < 3; r++) put4(v, A.inv[r * 4], A.inv[r * 4 + 1], A.inv[r * 4 + 2], A.inv[r * 4 + 3]);
+    put4(v, A.key, 0.f, 0.f, 0.f);
+}
+// loose triangle pair; B == nullptr pads with a degenerate triangle (e1 = e2 = 0 ->
+// det = 0 -> |det| < EPS: never a hit)
+void emit_tri_pair(std::vector<float>& v, const TriIn& A, const TriIn* Bp) {
+    TriIn pad;
+    pad.v[0] = pad.e1 = pad.e2 = f3(0, 0, 0);
+    pad.key = keyf(0xFFFFFFF0u);
+    const TriIn& B = Bp ? *Bp : pad;
+    put4(v, A.v[0].x, B.v[0].x, A.v[0].y, B.v[0].y);
+    put4(v, A.v[0].z, B.v[0].z, A.e1.x, B.e1.x);
+    put4(v, A.e1.y, B.e1.y, A.e1.z, B.e1.z);
+    put4(v, A.e2.x, B.e2.x, A.e2.y, B.e2.y);
+    put4(v, A.e2.z, B.e2.z, A.key, B.key);
+    put4(v, 0.f, 0.f, 0.f, 0.f);
+}
+F3 unit_normal(const TriIn& t) {
+    double a[3] = {t.v[0].x, t.v[0].y, t.v[0].z}, b[3] = {t.v[1].x, t.v[1].y, t.v[1].z},
+           c[3] = {t.v[2].x, t.v[2].y, t.v[2].z};
+    double e1[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, e2[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+    double n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+    double l = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    return f3((float)(n[0] / l), (float)(n[1] / l), (float)(n[2] / l));
+}
+void emit_tri_nrm(std::vector<float>& v, const TriIn& A, const TriIn* B) {
+    // a padding partner never hits, so it never needs the grazing pass: huge normal
+    F3 na = unit_normal(A), nb = B ? unit_normal(*B) : f3(1e18f, 1e18f, 1e18f);
+    put4(v, na.x, nb.x, na.y, nb.y);
+    put4(v, na.z, nb.z, 0.f, 0.f);
+}
+void emit_cube(std::vector<float>& v, const CubeIn& A, float lf, float sn) {
+    for (int r = 0; r < 3; r++) put4(v, A.inv[r * 4], A.inv[r * 4 + 1], A.inv[r * 4 + 2], A.inv[r * 4 + 3]);
+    put4(v, A.key, lf, sn, 0.f);
+}
+
+// Lays out the runs: hierarchy primitives leaf by leaf, then the linear rest.  Within
+// a leaf diag spheres pair up (an odd one joins the general run), triangles pair up.
+void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, const std::vector<CubeIn>& cubes,
+                bool enable, RunLayout& L) {
+    using namespace rtbvh;
+    std::vector<Prim> prims;
+    std::vector<Geo> geo;
+    std::vector<char> in_sph(sph.size(), 0), in_tri(tris.size(), 0), in_cube(cubes.size(), 0);
+    std::vector<double> cube_lf(cubes.size(), 0), cube_sn(cubes.size(), 0);
+    // per-primitive bounds as polynomials in D (see rt_scan.hpp): box inflation
+    // h = a2 D^2 + a1 D + a0 + cC |C|, t-margin m = b1 D + b0 + bC |C|
+    struct Coef {
+        double a2, a1, a0, cC, b1, b0, bC;
+    };
+    std::vector<Coef> coef;
+    if (enable) {
+        for (size_t i = 0; i < sph.size(); i++) {
+            Geo g;
+            double sigL, sn, sigA;
+            if (!geo_affine(sph[i].inv, false, g, sigL, sn, sigA)) continue;
+            // basis r_P (7.5 eps (|l|^2 + 1) + eps (|l| + 1 + |L||o| + |s|)), |l| <= sigma(L) D
+            double rP = sigA, S = SAFETY_SPHERE;
+            coef.push_back(Coef{S * 7.5 * FEPS * rP * sigL * sigL, S * rP * FEPS * 2.0 * sigL,
+                                S * rP * FEPS * (8.5 + sn), S * rP * FEPS * sigL, 0, 0, 0});
+            in_sph[i] = 1;
+            Prim p;
+            p.kind = sph[i].diag ? P_DSPH : P_GSPH;
+            p.id = (uint32_t)i;
+            std::memcpy(p.lo, g.lo, sizeof(p.lo));
+            std::memcpy(p.hi, g.hi, sizeof(p.hi));
+            p.cost = sph[i].diag ? 30.0 : 60.0;
+            prims.push_back(p);
+            geo.push_back(g);
+        }
+        for (size_t i = 0; i < tris.size(); i++) {
+            const TriIn& t = tris[i];
+            double v[3][3] = {{t.v[0].x, t.v[0].y, t.v[0].z}, {t.v[1].x, t.v[1].y, t.v[1].z},
+                              {t.v[2].x, t.v[2].y, t.v[2].z}};
+            double e1[3], e2[3];
+            for (int k = 0; k < 3; k++) {
+                e1[k] = v[1][k] - v[0][k];
+                e2[k] = v[2][k] - v[0][k];
+            }
+            double n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
+                           e1[0] * e2[1] - e1[1] * e2[0]};
+            double ln = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+            double l1 = std::sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+            double l2 = std::sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
+            double sin_a = ln / (l1 * l2);
+            if (!(sin_a >= MIN_SIN_ALPHA) || !std::isfinite(sin_a)) continue;
+            Geo g;
+            double rad = 0;
+            for (int k = 0; k < 3; k++) {
+                g.lo[k] = std::min(v[0][k], std::min(v[1][k], v[2][k]));
+                g.hi[k] = std::max(v[0][k], std::max(v[1][k], v[2][k]));
+                g.c[k] = (v[0][k] + v[1][k] + v[2][k]) / 3.0;
+            }
+            for (int j = 0; j < 3; j++) {
+                double dx = v[j][0] - g.c[0], dy = v[j][1] - g.c[1], dz = v[j][2] - g.c[2];
+                rad = std::max(rad, std::sqrt(dx * dx + dy * dy + dz * dz));
+            }
+            g.r = rad * (1 + 1e-9);
+            // basis eps (|o - v0| + |e|max + |o| + |v0|) / sin(alpha): lateral; the same
+            // over sin(phi_min) along the ray (t-margin)
+            double k = SAFETY_TRI * FEPS / sin_a, km = SAFETY_TRI_T * FEPS / (sin_a * GRAZE_SIN);
+            double v0n = std::sqrt(v[0][0] * v[0][0] + v[0][1] * v[0][1] + v[0][2] * v[0][2]);
+            double e = std::max(l1, l2) + v0n;
+            coef.push_back(Coef{0.0, 2.0 * k, k * e, k, 2.0 * km, km * e, km});
+            in_tri[i] = 1;
+            Prim p;
+            p.kind = P_TRI;
+            p.id = (uint32_t)i;
+            std::memcpy(p.lo, g.lo, sizeof(p.lo));
+            std::memcpy(p.hi, g.hi, sizeof(p.hi));
+            p.cost = 26.0;
+            prims.push_back(p);
+            geo.push_back(g);
+        }
+        for (size_t i = 0; i < cubes.size(); i++) {
+            Geo g;
+            double sigL, sn, sigA;
+            if (!geo_affine(cubes[i].inv, true, g, sigL, sn, sigA)) continue;
+            double S = SAFETY_CUBE;
+            // basis sigma(A) eps (|l| + 1 + |L||o| + |s|)
+            coef.push_back(Coef{0.0, S * sigA * FEPS * 2.0 * sigL, S * sigA * FEPS * (1.0 + sn),
+                                S * sigA * FEPS * sigL, 0, 0, 0});
+            cube_lf[i] = sigL;
+            cube_sn[i] = sn;
+            in_cube[i] = 1;
+            Prim p;
+            p.kind = P_CUBE;
+            p.id = (uint32_t)i;
+            std::memcpy(p.lo, g.lo, sizeof(p.lo));
+            std::memcpy(p.hi, g.hi, sizeof(p.hi));
+            p.cost = 300.0;
+            prims.push_back(p);
+            geo.push_back(g);
+        }
+    }
+    Tree T = build(prims);
+    L.use = !prims.empty();
+    if (L.use) {
+        // scene ball (C, R) around every hierarchy primitive's ball
+        for (int k = 0; k < 3; k++) L.c[k] = (float)(0.5 * (T.lo[k] + T.hi[k]));
+        double C[3] = {L.c[0], L.c[1], L.c[2]};
+        double Cn = std::sqrt(C[0] * C[0] + C[1] * C[1] + C[2] * C[2]);
+        double R = 0;
+        for (const Geo& g : geo) {
+            double dx = g.c[0] - C[0], dy = g.c[1] - C[1], dz = g.c[2] - C[2];
+            R = std::max(R, std::sqrt(dx * dx + dy * dy + dz * dz) + g.r);
+        }
+        R *= 1 + 1e-6;
+        double g2 = 0, g1 = 0, g0 = 0, m1 = 0, m0 = 0;
+        for (const Coef& c : coef) {
+            g2 = std::max(g2, c.a2);
+            g1 = std::max(g1, c.a1);
+            g0 = std::max(g0, c.a0 + c.cC * Cn);
+            m1 = std::max(m1, c.b1);
+            m0 = std::max(m0, c.b0 + c.bC * Cn);
+        }
+        L.m1 = up_f(m1 * (1 + 1e-6));
+        L.m0 = up_f(m0 * (1 + 1e-6));
+        g1 += SAFETY_SLAB * 16.0 * FEPS;
+        g0 += SAFETY_SLAB * 8.0 * FEPS * (3.0 * Cn + R);
+        L.r = up_f(R);
+        L.g2 = up_f(g2 * (1 + 1e-6));
+        L.g1 = up_f(g1 * (1 + 1e-6));
+        L.g0 = up_f(g0 * (1 + 1e-6));
+        L.root = T.root;
+        for (const Node& n : T.nodes) {
+            put4(L.nodes, down_f(n.lo[0][0]), down_f(n.lo[1][0]), down_f(n.lo[0][1]), down_f(n.lo[1][1]));
+            put4(L.nodes, down_f(n.lo[0][2]), down_f(n.lo[1][2]), up_f(n.hi[0][0]), up_f(n.hi[1][0]));
+            put4(L.nodes, up_f(n.hi[0][1]), up_f(n.hi[1][1]), up_f(n.hi[0][2]), up_f(n.hi[1][2]));
+            put4(L.nodes, keyf(n.child[0]), keyf(n.child[1]), keyf(n.axis), 0.f);
+        }
+        for (const auto& leaf : T.leaves) {
+            std::vector<const SphIn*> ds, gs;
+            std::vector<const TriIn*> ts;
+            std::vector<uint32_t> cs;
+            for (uint32_t pi : leaf) {
+                const Prim& p = prims[pi];
+                if (p.kind == P_DSPH) ds.push_back(&sph[p.id]);
+                else if (p.kind == P_GSPH) gs.push_back(&sph[p.id]);
+                else if (p.kind == P_TRI) ts.push_back(&tris[p.id]);
+                else cs.push_back(p.id);
+            }
+            if (ds.size() & 1) ds.push_back(ds.back());  // testing a sphere twice changes nothing
+            uint32_t rec[8];
+            rec[0] = (uint32_t)(L.dsph.size() / 16);
+            for (size_t k = 0; k < ds.size(); k += 2) emit_dsph_pair(L.dsph, *ds[k], *ds[k + 1]);
+            rec[1] = (uint32_t)(L.dsph.size() / 16);
+            rec[2] = (uint32_t)(L.gsph.size() / 16);
+            for (const SphIn* q : gs) emit_gsph(L.gsph, *q);
+            rec[3] = (uint32_t)(L.gsph.size() / 16);
+            rec[4] = (uint32_t)(L.tri.size() / 24);
+            for (size_t k = 0; k < ts.size(); k += 2) {
+                const TriIn* b = (k + 1 < ts.size()) ? ts[k + 1] : nullptr;
+                emit_tri_pair(L.tri, *ts[k], b);
+                emit_tri_nrm(L.tri_nrm, *ts[k], b);
+            }
+            rec[5] = (uint32_t)(L.tri.size() / 24);
+            rec[6] = (uint32_t)(L.cube.size() / 16);
+            for (uint32_t ci : cs) emit_cube(L.cube, cubes[ci], (float)cube_lf[ci], up_f(cube_sn[ci]));
+            rec[7] = (uint32_t)(L.cube.size() / 16);
+            L.leaves.insert(L.leaves.end(), rec, rec + 8);
+        }
+        if (std::getenv("RT_BVH_DEBUG")) {
+            size_t kinds[4] = {0, 0, 0, 0}, max_leaf = 0;
+            for (const Prim& p : prims) kinds[p.kind]++;
+            for (const auto& lf : T.leaves) max_leaf = std::max(max_leaf, lf.size());
+            std::fprintf(stderr,
+                         "rt_bvh: prims dsph %zu gsph %zu tri %zu cube %zu (of sph %zu tri %zu cube %zu); "
+                         "nodes %zu leaves %zu depth %d max_leaf %zu; C (%g %g %g) R %g; h = (%g D + %g) D + %g; "
+                         "m = %g D + %g\n",
+                         kinds[0], kinds[1], kinds[2], kinds[3], sph.size(), tris.size(), cubes.size(),
+                         T.nodes.size(), T.leaves.size(), T.depth, max_leaf, L.c[0], L.c[1], L.c[2], L.r, L.g2,
+                         L.g1, L.g0, L.m1, L.m0);
+        }
+        L.n_dsph_bvh = (int)(L.dsph.size() / 16);
+        L.n_gsph_bvh = (int)(L.gsph.size() / 16);
+        L.n_tri_bvh = (int)(L.tri.size() / 24);
+        L.n_cube_bvh = (int)(L.cube.size() / 16);
+    }
+    // ---- the linear rest
+    std::vector<const SphIn*> ds;
+    for (size_t i = 0; i < sph.size(); i++) {
+        if (in_sph[i]) continue;
+        if (sph[i].diag) ds.push_back(&sph[i]);
+        else emit_gsph(L.gsph, sph[i]);
+    }
+    for (size_t k = 0; k + 1 < ds.size(); k += 2) emit_dsph_pair(L.dsph, *ds[k], *ds[k + 1]);
+    if (ds.size() & 1) emit_gsph(L.gsph, *ds.back());
+    std::vector<const TriIn*> ts;
+    for (size_t i = 0; i < tris.size(); i++)
+        if (!in_tri[i]) ts.push_back(&tris[i]);
+    for (size_t k = 0; k < ts.size(); k += 2) emit_tri_pair(L.tri, *ts[k], (k + 1 < ts.size()) ? ts[k + 1] : nullptr);
+    for (size_t i = 0; i < cubes.size(); i++)
+        if (!in_cube[i]) emit_cube(L.cube, cubes[i], 0.f, 0.f);
+}
+
 struct Workspace {
     float* out = nullptr;            // device frame (rt_render)
     size_t out_floats = 0;
@@ -146,7 +510,26 @@ struct Workspace {
     uint32_t shadow_capacity = 0;
     uint32_t* levels = nullptr;      // 2 * (RT_MAX_DEPTH + 2) words
     uint32_t* overflow = nullptr;
+    // queue ordering (rt_sort.hip)
+    uint32_t* task_keys = nullptr;   // [capacity] x4 buffers
+    uint32_t* task_vals = nullptr;
+    uint32_t* perm = nullptr;
+    uint32_t* keys_alt = nullptr;
+    uint32_t sort_capacity = 0;
+    uint32_t* shadow_keys = nullptr; // [shadow_capacity] x3 buffers
+    uint32_t* shadow_keys_alt = nullptr;
+    uint32_t* shadow_sorted = nullptr;
+    uint32_t sort_shadow_capacity = 0;
+    void* sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    uint32_t* h_count = nullptr;     // pinned: a level's (offset, count)
 };
+
+// RT_SORT=0 keeps the queues in production order (A/B measurements).
+bool sort_enabled() {
+    const char* e = std::getenv("RT_SORT");
+    return !(e && std::strcmp(e, "0") == 0);
+}
 
 // Device path: "wave" (level-synchronous, default) or "mega" (per-pixel megakernel),
 // chosen with RT_PIPELINE for A/B measurement.
@@ -264,18 +647,12 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
         return RT_ERR_INVALID_ARG;
     if (d->n_shapes >= (1u << 27)) return RT_ERR_UNSUPPORTED;
 
-    // ---- host preprocessing into per-type runs
+    // ---- host preprocessing: per-shape records
     std::vector<float> dsph, gsph, tri, cube, plane, cubetri;
     std::vector<ShapeRec> shapes(d->n_shapes);
-    struct DiagSph {
-        float s[3], o[3], key;
-    };
-    struct LooseTri {
-        F3 v0, e1, e2;
-        float key;
-    };
-    std::vector<DiagSph> diag_sph;
-    std::vector<LooseTri> loose;
+    std::vector<SphIn> sph_in;
+    std::vector<TriIn> tri_in;
+    std::vector<CubeIn> cube_in;
     uint64_t flops = 0;
     for (uint32_t i = 0; i < d->n_shapes; i++) {
         const rt_shape& s = d->shapes[i];
@@ -291,15 +668,12 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
         float key = keyf(i << 4);
         switch (s.kind) {
             case RT_SHAPE_SPHERE: {
-                bool diag = inv.m[0][1] == 0.f && inv.m[0][2] == 0.f && inv.m[1][0] == 0.f &&
-                            inv.m[1][2] == 0.f && inv.m[2][0] == 0.f && inv.m[2][1] == 0.f;
-                if (diag) {
-                    diag_sph.push_back(DiagSph{{inv.m[0][0], inv.m[1][1], inv.m[2][2]},
-                                           {inv.m[0][3], inv.m[1][3], inv.m[2][3]}, key});
-                } else {
-                    for (int r = 0; r < 3; r++) put4(gsph, inv.m[r][0], inv.m[r][1], inv.m[r][2], inv.m[r][3]);
-                    put4(gsph, key, 0.f, 0.f, 0.f);
-                }
+                SphIn q;
+                std::memcpy(q.inv, R.inv, sizeof(q.inv));
+                q.key = key;
+                q.diag = inv.m[0][1] == 0.f && inv.m[0][2] == 0.f && inv.m[1][0] == 0.f &&
+                         inv.m[1][2] == 0.f && inv.m[2][0] == 0.f && inv.m[2][1] == 0.f;
+                sph_in.push_back(q);
                 flops += 57;
                 break;
             }
@@ -320,19 +694,26 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
                 break;
             }
             case RT_SHAPE_TRIANGLE: {
-                F3 v0 = f3(s.data[0], s.data[1], s.data[2]);
-                F3 v1 = f3(s.data[3], s.data[4], s.data[5]);
-                F3 v2 = f3(s.data[6], s.data[7], s.data[8]);
-                F3 e1 = fsub(v1, v0), e2 = fsub(v2, v0), nn = tri_normal(v0, v1, v2);
-                const float a[12] = {v0.x, v0.y, v0.z, e1.x, e1.y, e1.z, e2.x, e2.y, e2.z, nn.x, nn.y, nn.z};
+                TriIn q;
+                q.v[0] = f3(s.data[0], s.data[1], s.data[2]);
+                q.v[1] = f3(s.data[3], s.data[4], s.data[5]);
+                q.v[2] = f3(s.data[6], s.data[7], s.data[8]);
+                q.e1 = fsub(q.v[1], q.v[0]);
+                q.e2 = fsub(q.v[2], q.v[0]);
+                q.key = key;
+                F3 nn = tri_normal(q.v[0], q.v[1], q.v[2]);
+                const float a[12] = {q.v[0].x, q.v[0].y, q.v[0].z, q.e1.x, q.e1.y, q.e1.z,
+                                     q.e2.x, q.e2.y, q.e2.z, nn.x, nn.y, nn.z};
                 std::memcpy(R.a, a, sizeof(a));
-                loose.push_back(LooseTri{v0, e1, e2, key});
+                tri_in.push_back(q);
                 flops += 52;
                 break;
             }
             case RT_SHAPE_CUBE: {
-                for (int r = 0; r < 3; r++) put4(cube, inv.m[r][0], inv.m[r][1], inv.m[r][2], inv.m[r][3]);
-                put4(cube, key, 0.f, 0.f, 0.f);
+                CubeIn q;
+                std::memcpy(q.inv, R.inv, sizeof(q.inv));
+                q.key = key;
+                cube_in.push_back(q);
                 flops += 33 + 12 * 52;
                 break;
             }
@@ -340,33 +721,13 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
                 return RT_ERR_INVALID_ARG;
         }
     }
-    // diag spheres in pairs (2-wide packed scan); an odd one out joins the general run
-    for (size_t k = 0; k + 1 < diag_sph.size(); k += 2) {
-        const DiagSph &A = diag_sph[k], &B = diag_sph[k + 1];
-        put4(dsph, A.s[0], B.s[0], A.s[1], B.s[1]);
-        put4(dsph, A.s[2], B.s[2], A.o[0], B.o[0]);
-        put4(dsph, A.o[1], B.o[1], A.o[2], B.o[2]);
-        put4(dsph, A.key, B.key, 0.f, 0.f);
-    }
-    if (diag_sph.size() & 1) {
-        const DiagSph& A = diag_sph.back();  // general form of the same inverse (exact formula)
-        put4(gsph, A.s[0], 0.f, 0.f, A.o[0]);
-        put4(gsph, 0.f, A.s[1], 0.f, A.o[1]);
-        put4(gsph, 0.f, 0.f, A.s[2], A.o[2]);
-        put4(gsph, A.key, 0.f, 0.f, 0.f);
-    }
-    // loose triangles in pairs; an odd count is padded with a degenerate triangle
-    // (e1 = e2 = 0 -> det = 0 -> |det| < EPS: never a hit)
-    if (loose.size() & 1) loose.push_back(LooseTri{f3(0, 0, 0), f3(0, 0, 0), f3(0, 0, 0), keyf(0xFFFFFFF0u)});
-    for (size_t k = 0; k < loose.size(); k += 2) {
-        const LooseTri &A = loose[k], &B = loose[k + 1];
-        put4(tri, A.v0.x, B.v0.x, A.v0.y, B.v0.y);
-        put4(tri, A.v0.z, B.v0.z, A.e1.x, B.e1.x);
-        put4(tri, A.e1.y, B.e1.y, A.e1.z, B.e1.z);
-        put4(tri, A.e2.x, B.e2.x, A.e2.y, B.e2.y);
-        put4(tri, A.e2.z, B.e2.z, A.key, B.key);
-        put4(tri, 0.f, 0.f, 0.f, 0.f);
-    }
+    // ---- culling hierarchy and the run layout (leaf order first, then the linear rest)
+    RunLayout lay;
+    build_runs(sph_in, tri_in, cube_in, bvh_enabled(), lay);
+    dsph.swap(lay.dsph);
+    gsph.swap(lay.gsph);
+    tri.swap(lay.tri);
+    cube.swap(lay.cube);
     cube_triangles(cubetri);
     if (!rt_cube_table_check(cubetri.data())) return RT_ERR_UNSUPPORTED;
     std::vector<MatRec> mats(d->n_materials);
@@ -405,12 +766,17 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
         size_t bytes;
         size_t off;
     };
-    Sec secs[9] = {{dsph.data(), dsph.size() * 4, 0},       {gsph.data(), gsph.size() * 4, 0},
-                   {tri.data(), tri.size() * 4, 0},         {cube.data(), cube.size() * 4, 0},
-                   {plane.data(), plane.size() * 4, 0},     {cubetri.data(), cubetri.size() * 4, 0},
-                   {shapes.data(), shapes.size() * sizeof(ShapeRec), 0},
-                   {mats.data(), mats.size() * sizeof(MatRec), 0},
-                   {lights.data(), lights.size() * sizeof(LightRec), 0}};
+    static const unsigned long long zero_ops[RT_OPS_N] = {0};
+    Sec secs[13] = {{dsph.data(), dsph.size() * 4, 0},       {gsph.data(), gsph.size() * 4, 0},
+                    {tri.data(), tri.size() * 4, 0},         {cube.data(), cube.size() * 4, 0},
+                    {plane.data(), plane.size() * 4, 0},     {cubetri.data(), cubetri.size() * 4, 0},
+                    {shapes.data(), shapes.size() * sizeof(ShapeRec), 0},
+                    {mats.data(), mats.size() * sizeof(MatRec), 0},
+                    {lights.data(), lights.size() * sizeof(LightRec), 0},
+                    {lay.nodes.data(), lay.nodes.size() * 4, 0},
+                    {lay.leaves.data(), lay.leaves.size() * 4, 0},
+                    {lay.tri_nrm.data(), lay.tri_nrm.size() * 4, 0},
+                    {zero_ops, sizeof(zero_ops), 0}};
     size_t total = 0;
     for (auto& s : secs) {
         s.off = total;
@@ -447,6 +813,26 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     S.n_shapes = (int32_t)d->n_shapes;
     S.n_lights = (int32_t)d->n_lights;
     S.n_mats = (int32_t)d->n_materials;
+    S.bvh_nodes = (const float4*)at(9);
+    S.bvh_leaves = (const uint4*)at(10);
+    S.tri_nrm = (const float4*)at(11);
+    S.scan_ops = (unsigned long long*)at(12);
+    S.bvh_root = lay.root;
+    S.use_bvh = lay.use ? 1 : 0;
+    S.n_dsph_bvh = lay.n_dsph_bvh;
+    S.n_gsph_bvh = lay.n_gsph_bvh;
+    S.n_tri_bvh = lay.n_tri_bvh;
+    S.n_cube_bvh = lay.n_cube_bvh;
+    S.bvh_cx = lay.c[0];
+    S.bvh_cy = lay.c[1];
+    S.bvh_cz = lay.c[2];
+    S.bvh_r = lay.r;
+    S.bvh_g2 = lay.g2;
+    S.bvh_g1 = lay.g1;
+    S.bvh_g0 = lay.g0;
+    S.bvh_m1 = lay.m1;
+    S.bvh_m0 = lay.m0;
+    S.graze_s2 = (float)(GRAZE_SIN * GRAZE_SIN * 1.0201);  // checked at 1.01 sin(phi_min)
     S.amb_r = d->ambient.r;
     S.amb_g = d->ambient.g;
     S.amb_b = d->ambient.b;
@@ -483,6 +869,24 @@ rt_status rt_scene_destroy(rt_scene* s) {
 
 uint64_t rt_scene_flops_per_scan(const rt_scene* s) { return s ? s->flops_per_scan : 0; }
 uint64_t rt_scene_device_bytes(const rt_scene* s) { return s ? (uint64_t)s->dbytes : 0; }
+
+rt_status rt_scene_scan_ops(rt_scene* s, uint64_t* out, uint32_t n, int32_t reset) {
+    if (!s || (out && n > RT_SCAN_OPS_N)) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipDeviceSynchronize());
+    if (out && n) {
+        unsigned long long h[RT_OPS_N];
+        HIP_TRY(hipMemcpy(h, s->S.scan_ops, sizeof(h), hipMemcpyDeviceToHost));
+        for (uint32_t k = 0; k < n; k++) out[k] = h[k];
+    }
+    if (reset) {
+        HIP_TRY(hipMemset(s->S.scan_ops, 0, RT_OPS_N * sizeof(unsigned long long)));
+        HIP_TRY(hipDeviceSynchronize());
+    }
+    return RT_OK;
+}
+
+int32_t rt_scene_uses_bvh(const rt_scene* s) { return (s && s->S.use_bvh) ? 1 : 0; }
 
 static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
                                    uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
@@ -594,6 +998,49 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
         HIP_TRY(hipMalloc(&w.shadow, want_sh * sizeof(uint32_t)));
         w.shadow_capacity = (uint32_t)want_sh;
     }
+    const bool sort_on = s->S.use_bvh && sort_enabled();
+    const int task_bits = RT_MORTON_BITS + 3, shadow_bits = RT_MORTON_BITS + 5;
+    if (sort_on) {
+        if (w.sort_capacity < w.capacity) {
+            for (uint32_t** b : {&w.task_keys, &w.task_vals, &w.perm, &w.keys_alt}) {
+                if (*b) (void)hipFree(*b);
+                *b = nullptr;
+            }
+            w.sort_capacity = 0;
+            for (uint32_t** b : {&w.task_keys, &w.task_vals, &w.perm, &w.keys_alt})
+                HIP_TRY(hipMalloc(b, (size_t)w.capacity * sizeof(uint32_t)));
+            w.sort_capacity = w.capacity;
+        }
+        if (w.sort_shadow_capacity < w.shadow_capacity) {
+            for (uint32_t** b : {&w.shadow_keys, &w.shadow_keys_alt, &w.shadow_sorted}) {
+                if (*b) (void)hipFree(*b);
+                *b = nullptr;
+            }
+            w.sort_shadow_capacity = 0;
+            for (uint32_t** b : {&w.shadow_keys, &w.shadow_keys_alt, &w.shadow_sorted})
+                HIP_TRY(hipMalloc(b, (size_t)w.shadow_capacity * sizeof(uint32_t)));
+            w.sort_shadow_capacity = w.shadow_capacity;
+        }
+        size_t b1 = 0, b2 = 0;
+        HIP_TRY(sort_pairs_u32(nullptr, b1, w.task_keys, w.keys_alt, w.task_vals, w.perm, w.capacity, task_bits,
+                               stream));
+        HIP_TRY(sort_pairs_u32(nullptr, b2, w.shadow_keys, w.shadow_keys_alt, w.shadow, w.shadow_sorted,
+                               w.shadow_capacity, shadow_bits, stream));
+        size_t need = std::max(b1, b2);
+        if (w.sort_tmp_bytes < need) {
+            if (w.sort_tmp) (void)hipFree(w.sort_tmp);
+            w.sort_tmp = nullptr;
+            w.sort_tmp_bytes = 0;
+            HIP_TRY(hipMalloc(&w.sort_tmp, need));
+            w.sort_tmp_bytes = need;
+        }
+        if (!w.h_count) HIP_TRY(hipHostMalloc((void**)&w.h_count, 16, hipHostMallocDefault));
+    }
+    p.task_keys = sort_on ? w.task_keys : nullptr;
+    p.task_vals = sort_on ? w.task_vals : nullptr;
+    p.shadow_keys = sort_on ? w.shadow_keys : nullptr;
+    p.perm = nullptr;
+    p.shadow_in = w.shadow;
     p.capacity = w.capacity;
     p.shadow_capacity = w.shadow_capacity;
     p.shadow = w.shadow;
@@ -615,9 +1062,43 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
     int cb = s->num_cus * s->occ_combine;
     uint32_t levels = depth > 0 ? depth : 1;
     HIP_TRY(launch_wave_init(w.levels, 2 * (RT_MAX_DEPTH + 2), p.total_items, w.overflow, stream));
-    for (uint32_t k = 0; k < levels; k++) HIP_TRY(launch_wave_trace(p, k, tb, stream));
-    HIP_TRY(launch_wave_shadow(p, sb, stream));
-    for (uint32_t k = levels; k-- > 0;) HIP_TRY(launch_wave_combine(p, k, cb, stream));
+    if (!sort_on) {
+        for (uint32_t k = 0; k < levels; k++) HIP_TRY(launch_wave_trace(p, k, tb, stream));
+        HIP_TRY(launch_wave_shadow(p, sb, stream));
+        for (uint32_t k = levels; k-- > 0;) HIP_TRY(launch_wave_combine(p, k, cb, stream));
+        return RT_OK;
+    }
+    // ordered queues: the host reads each level's size (one small copy + stream sync),
+    // sorts its (key, slot) pairs into `perm` and stops at the first empty level
+    auto read2 = [&](const uint32_t* src) -> hipError_t {
+        hipError_t e = hipMemcpyAsync(w.h_count, src, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream);
+        return e == hipSuccess ? hipStreamSynchronize(stream) : e;
+    };
+    HIP_TRY(launch_wave_trace(p, 0, tb, stream));
+    uint32_t used = 1;  // levels that hold nodes
+    for (uint32_t k = 1; k < levels; k++) {
+        HIP_TRY(read2(w.levels + 2 * k));
+        uint32_t off = w.h_count[0], cnt = w.h_count[1];
+        if (off >= w.capacity) break;  // overflowed: the flag is already set
+        cnt = std::min(cnt, w.capacity - off);
+        if (cnt == 0) break;
+        size_t bytes = w.sort_tmp_bytes;
+        HIP_TRY(sort_pairs_u32(w.sort_tmp, bytes, w.task_keys + off, w.keys_alt, w.task_vals + off, w.perm + off,
+                               cnt, task_bits, stream));
+        p.perm = w.perm;
+        HIP_TRY(launch_wave_trace(p, k, tb, stream));
+        used = k + 1;
+    }
+    HIP_TRY(read2(w.levels + 2 * (RT_MAX_DEPTH + 1)));
+    uint32_t n_sh = std::min(w.h_count[0], w.shadow_capacity);
+    if (n_sh > 0) {
+        size_t bytes = w.sort_tmp_bytes;
+        HIP_TRY(sort_pairs_u32(w.sort_tmp, bytes, w.shadow_keys, w.shadow_keys_alt, w.shadow, w.shadow_sorted, n_sh,
+                               shadow_bits, stream));
+        p.shadow_in = w.shadow_sorted;
+        HIP_TRY(launch_wave_shadow(p, sb, stream));
+    }
+    for (uint32_t k = used; k-- > 0;) HIP_TRY(launch_wave_combine(p, k, cb, stream));
     return RT_OK;
 }
 

@@ -66,6 +66,35 @@ struct DevScene {
     const LightRec* lights;
     int32_t n_dsph, n_gsph, n_tri, n_cube, n_plane, n_shapes, n_lights, n_mats;  // dsph/tri: pairs
     float amb_r, amb_g, amb_b;
+    // ---- culling hierarchy (rt_bvh.hpp; DESIGN.md "Exact culling").  The first
+    // n_*_bvh records of each run are the hierarchy's primitives in leaf order; the rest
+    // (ill-conditioned shapes, or everything when the hierarchy is off) are scanned
+    // linearly for every ray.
+    const float4* bvh_nodes;   // 4 float4 per node: both child boxes + child pointers
+    const uint4* bvh_leaves;   // 2 uint4 per leaf: [dsph b,e gsph b,e] [tri b,e cube b,e]
+    const float4* tri_nrm;     // 2 float4 per hierarchy triangle pair: unit normals (A,B)
+    uint32_t bvh_root;         // child pointer (BVH_LEAF bit: a leaf)
+    int32_t use_bvh;
+    int32_t n_dsph_bvh, n_gsph_bvh, n_tri_bvh, n_cube_bvh;
+    // per ray, D = |o - c| + r: box inflation h(D) = (g2 D + g1) D + g0 and t-margin
+    // m(D) = m1 D + m0 (distance units), see rt_scan.hpp
+    float bvh_cx, bvh_cy, bvh_cz, bvh_r, bvh_g2, bvh_g1, bvh_g0, bvh_m1, bvh_m0;
+    float graze_s2;            // (sin phi_min)^2: below it a ray grazes a triangle plane
+    unsigned long long* scan_ops;  // RT_OPS_* lane-weighted test counts
+};
+
+#define BVH_LEAF 0x80000000u
+// lane-weighted counters of the scan's tests (each += active lanes)
+enum : int {
+    RT_OPS_NODE = 0,    // 2-wide child-box tests
+    RT_OPS_DSPH = 1,    // diag sphere pairs
+    RT_OPS_GSPH = 2,    // general spheres
+    RT_OPS_TRI = 3,     // loose triangle pairs
+    RT_OPS_CUBE_BOX = 4,  // object-space cube box tests
+    RT_OPS_CUBE = 5,    // full cubes (12 triangles)
+    RT_OPS_GRAZE = 6,   // grazing checks (triangle pairs)
+    RT_OPS_PLANE = 7,   // planes
+    RT_OPS_N = 8
 };
 
 // Everything one launch needs.
@@ -127,6 +156,16 @@ struct WaveParams {
     uint32_t* overflow;                // set when an append would exceed a capacity
     float* out;
     unsigned long long* ray_counters;  // [node, shadow, pixels], added to
+    // ray-queue ordering (rt_sort.hip): the producer writes a key and its slot per task /
+    // shadow entry; the host sorts a level's pairs; the consumer reads through `perm`
+    uint32_t* task_keys;               // [capacity]
+    uint32_t* task_vals;               // [capacity]: the slot itself
+    const uint32_t* perm;              // [capacity] or null: level-k slot -> task slot
+    uint32_t* shadow_keys;             // [shadow_capacity]
+    const uint32_t* shadow_in;         // the shadow entries the shadow kernel reads
 };
+
+// 15-bit Morton code of a point in the 32^3 grid over [c - r, c + r]^3 (clamped)
+#define RT_MORTON_BITS 15
 
 }  // namespace rtdev

@@ -37,6 +37,8 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
     const DevScene& S = P.S;
     const V3 cam_o = v3(P.cam_ox, P.cam_oy, P.cam_oz);
     const uint32_t lane = lane_id();
+    ScanCnt cnt;
+    cnt_init(cnt);
 
     Frame st[MAXF > 0 ? MAXF : 1];
 
@@ -65,9 +67,9 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
             uint64_t need = __ballot(item < 0 && !exhausted);
             if (need == 0) break;
             uint32_t first = (uint32_t)__builtin_ctzll(need);
-            uint32_t cnt = (uint32_t)__builtin_popcountll(need);
+            uint32_t n_need = (uint32_t)__builtin_popcountll(need);
             uint32_t base = 0;
-            if (lane == first) base = atomicAdd(P.work_counter, cnt);
+            if (lane == first) base = atomicAdd(P.work_counter, n_need);
             base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
             bool got = false;
             if (item < 0 && !exhausted) {
@@ -117,7 +119,7 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
         V3 sd = (phase == 0) ? rd : ldir;
         float bt;
         uint32_t bk;
-        scan(S, so, sd, bt, bk);
+        scan(S, so, sd, bt, bk, cnt);
         bool hit = bk != 0xFFFFFFFFu;
 
         bool node_done = false;
@@ -279,6 +281,7 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
         atomicAdd(P.ray_counters + 2, n_pix);
     }
     if (lane == 0 && P.iter_counter) atomicAdd(P.iter_counter, n_iter);
+    cnt_flush(cnt, S.scan_ops);
 }
 
 // Scatter gathered per-rank band buffers into the row-major frame (one block row per frame row).

@@ -260,65 +260,208 @@ __device__ __forceinline__ void plane_one(cfloat4* r, V3 o, V3 d, float& bt, uin
     if (plane_t(to, td, xyz(rn), xyz(ro), t)) take(t, keyof(rn.w), bt, bk);
 }
 
-// One pass over every primitive.  Group loops prefetch record i+1 before testing
-// record i; every section is padded by one group so the look-ahead load stays inside
-// the allocation.
-__device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk) {
-    bt = __builtin_huge_valf();
-    bk = 0xFFFFFFFFu;
-    RT_STAT(0);
-    for (int i = 0; i < S.n_plane; ++i) plane_one(cptr(S.plane) + 5 * i, o, d, bt, bk);
-    {
-        cfloat4* p = cptr(S.dsph);
-        SphPair cur = ld_sph(p);
-        for (int i = 0; i < S.n_dsph; ++i) {
-            SphPair nxt = ld_sph(p + 4 * (i + 1));
-            sph_pair(cur, o, d, bt, bk);
-            cur = nxt;
-        }
-    }
-    {
-        cfloat4* p = cptr(S.gsph);
-        Rec16 cur = ld_rec(p);
-        for (int i = 0; i < S.n_gsph; ++i) {
-            Rec16 nxt = ld_rec(p + 4 * (i + 1));
-            sph_general(cur, o, d, bt, bk);
-            cur = nxt;
-        }
-    }
-    {
-        cfloat4* p = cptr(S.tri);
-        TriPair cur = ld_tri(p);
-        for (int i = 0; i < S.n_tri; ++i) {
-            TriPair nxt = ld_tri(p + 6 * (i + 1));
-            tri_pair(cur, o, d, bt, bk);
-            cur = nxt;
-        }
-    }
-    {
-        cfloat4* p = cptr(S.cube);
-        Rec16 cur = ld_rec(p);
-        for (int i = 0; i < S.n_cube; ++i) {
-            Rec16 nxt = ld_rec(p + 4 * (i + 1));
-            V3 to = pt_mul(cur.r0, cur.r1, cur.r2, o);
-            V3 td = vec3_mul(cur.r0, cur.r1, cur.r2, d);
-            cube_scan(to, td, keyof(cur.rk.x), bt, bk);
-            cur = nxt;
-        }
+// ------------------------------------------------------------------ test counters
+// Lane-weighted counts of every test the scan runs (RT_OPS_*): wave-uniform, kept in
+// SGPRs, added to DevScene::scan_ops once per wave when a kernel ends.
+struct ScanCnt {
+    uint32_t node, dsph, gsph, tri, cube_box, cube, graze, plane;
+};
+__device__ __forceinline__ void cnt_init(ScanCnt& c) {
+    c.node = c.dsph = c.gsph = c.tri = c.cube_box = c.cube = c.graze = c.plane = 0;
+}
+__device__ __forceinline__ uint32_t active_lanes() { return (uint32_t)__builtin_popcountll(__ballot(1)); }
+#define RT_OPS(c, f) ((c).f += active_lanes())
+__device__ __forceinline__ void cnt_add(unsigned long long* p, uint32_t v) {
+    if (v) atomicAdd(p, (unsigned long long)v);
+}
+__device__ __forceinline__ void cnt_flush(const ScanCnt& c, unsigned long long* dst) {
+    uint64_t m = __ballot(1);
+    if (m == 0) return;
+    if (__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) == 0) {
+        cnt_add(dst + RT_OPS_NODE, c.node);
+        cnt_add(dst + RT_OPS_DSPH, c.dsph);
+        cnt_add(dst + RT_OPS_GSPH, c.gsph);
+        cnt_add(dst + RT_OPS_TRI, c.tri);
+        cnt_add(dst + RT_OPS_CUBE_BOX, c.cube_box);
+        cnt_add(dst + RT_OPS_CUBE, c.cube);
+        cnt_add(dst + RT_OPS_GRAZE, c.graze);
+        cnt_add(dst + RT_OPS_PLANE, c.plane);
     }
 }
 
+// ------------------------------------------------------------------ linear runs
+// Group loops prefetch record i+1 before testing record i; every section is padded by
+// one group so the look-ahead load stays inside the allocation.
+__device__ __forceinline__ void run_dsph(const DevScene& S, int b, int e, V3 o, V3 d, float& bt, uint32_t& bk,
+                                         ScanCnt& c) {
+    if (b >= e) return;
+    cfloat4* p = cptr(S.dsph) + 4 * b;
+    SphPair cur = ld_sph(p);
+    for (int i = b; i < e; ++i) {
+        p += 4;
+        SphPair nxt = ld_sph(p);
+        RT_OPS(c, dsph);
+        sph_pair(cur, o, d, bt, bk);
+        cur = nxt;
+    }
+}
+__device__ __forceinline__ void run_gsph(const DevScene& S, int b, int e, V3 o, V3 d, float& bt, uint32_t& bk,
+                                         ScanCnt& c) {
+    if (b >= e) return;
+    cfloat4* p = cptr(S.gsph) + 4 * b;
+    Rec16 cur = ld_rec(p);
+    for (int i = b; i < e; ++i) {
+        p += 4;
+        Rec16 nxt = ld_rec(p);
+        RT_OPS(c, gsph);
+        sph_general(cur, o, d, bt, bk);
+        cur = nxt;
+    }
+}
+__device__ __forceinline__ void run_tri(const DevScene& S, int b, int e, V3 o, V3 d, float& bt, uint32_t& bk,
+                                        ScanCnt& c) {
+    if (b >= e) return;
+    cfloat4* p = cptr(S.tri) + 6 * b;
+    TriPair cur = ld_tri(p);
+    for (int i = b; i < e; ++i) {
+        p += 6;
+        TriPair nxt = ld_tri(p);
+        RT_OPS(c, tri);
+        tri_pair(cur, o, d, bt, bk);
+        cur = nxt;
+    }
+}
+__device__ __forceinline__ void run_cube(const DevScene& S, int b, int e, V3 o, V3 d, float& bt, uint32_t& bk,
+                                         ScanCnt& c) {
+    if (b >= e) return;
+    cfloat4* p = cptr(S.cube) + 4 * b;
+    Rec16 cur = ld_rec(p);
+    for (int i = b; i < e; ++i) {
+        p += 4;
+        Rec16 nxt = ld_rec(p);
+        RT_OPS(c, cube);
+        V3 to = pt_mul(cur.r0, cur.r1, cur.r2, o);
+        V3 td = vec3_mul(cur.r0, cur.r1, cur.r2, d);
+        cube_scan(to, td, keyof(cur.rk.x), bt, bk);
+        cur = nxt;
+    }
+}
 
-// ------------------------------------------------------------------ shadow scan
-// PointLight::get_energy (scene/mod.rs:189-206): a FULL nearest-hit scan, then
-// "shadowed iff |hit.point - p|^2 < |pos - p|^2".  Exact early exit:
-//  * planes are scanned first; only planes can return t < 0 (plane.rs:62-83 has no
-//    t >= 0 check; spheres and triangles reject t < 0), so after them a lane whose best
-//    t is negative already holds its nearest hit;
-//  * for t >= 0 the reference's distance |(p + d*t) - p|^2 is non-decreasing in t (each
-//    rounded step is monotone), so once ANY hit has distance^2 < |pos - p|^2 the nearest
-//    one does too.
-// A wave leaves the scan when every active lane is decided.  Returns `shadowed`.
+// ------------------------------------------------------------------ culling hierarchy
+// DESIGN.md "Exact culling".  For a ray (o, d) and D = |o - c| + r (the ball (c, r)
+// holds every hierarchy primitive), every hit the reference's f32 tests can report at t'
+// satisfies: the point o + t*d lies within h(D) = (g2 D + g1) D + g0 of the primitive for
+// some t* with |t' - t*| <= m(D)/|d|.  Spheres and cubes: t* = t' (their reported points
+// themselves are that close); triangles: h bounds how far the LINE passes and m how far
+// the f32 t' slides along it, for rays meeting the plane at sin(phi) >= sin(phi_min).
+// h also covers the rounding of this slab test.  A child box is skipped for a lane only
+// when its box grown by h misses the ray on [-m, t_max + m] (t_max = the lane's best t,
+// or the shadow limit); the wave skips it only when every lane does.  Spheres,
+// triangles and cubes never report t < 0; a lane already holding a plane hit at t < 0
+// votes for nothing (nothing can beat a negative t).  Grazing rays: the grazing pass
+// below tests exactly every hierarchy triangle whose plane some lane grazes.
+__shared__ uint32_t rt_bvh_stack[4 * 32];  // one 32-entry stack per wave (256-thread blocks)
+
+__device__ __forceinline__ float safe_rcp(float x) {
+    float s = (fabsf(x) < 1e-30f) ? copysignf(1e-30f, x) : x;
+    return __builtin_amdgcn_rcpf(s);
+}
+__device__ __forceinline__ float rfl(float x) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+__device__ __forceinline__ uint32_t rfl(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
+struct BvhRay {
+    float ix, iy, iz;      // 1/d
+    float pax, pay, paz;   // (o + h) / d
+    float pbx, pby, pbz;   // (o - h) / d
+    float on;              // |o|
+    float m;               // t-margin m(D) / |d|
+};
+
+__device__ __forceinline__ BvhRay bvh_ray(const DevScene& S, V3 o, V3 d) {
+    BvhRay R;
+    float dx = o.x - S.bvh_cx, dy = o.y - S.bvh_cy, dz = o.z - S.bvh_cz;
+    float D = sqrtf(dx * dx + dy * dy + dz * dz) + S.bvh_r;
+    float h = fmaf(fmaf(S.bvh_g2, D, S.bvh_g1), D, S.bvh_g0);
+    R.ix = safe_rcp(d.x);
+    R.iy = safe_rcp(d.y);
+    R.iz = safe_rcp(d.z);
+    R.pax = (o.x + h) * R.ix;
+    R.pay = (o.y + h) * R.iy;
+    R.paz = (o.z + h) * R.iz;
+    R.pbx = (o.x - h) * R.ix;
+    R.pby = (o.y - h) * R.iy;
+    R.pbz = (o.z - h) * R.iz;
+    R.on = sqrtf(o.x * o.x + o.y * o.y + o.z * o.z);
+    R.m = fmaf(S.bvh_m1, D, S.bvh_m0) / sqrtf(d.x * d.x + d.y * d.y + d.z * d.z) * 1.0001f;
+    return R;
+}
+
+// both children of a node, 2-wide: {loA.x loB.x loA.y loB.y} {loA.z loB.z hiA.x hiB.x}
+// {hiA.y hiB.y hiA.z hiB.z}
+__device__ __forceinline__ void node_test(float4 q0, float4 q1, float4 q2, BvhRay R, float tmax, bool& hA,
+                                          bool& hB) {
+    f2 lx = f2{q0.x, q0.y}, ly = f2{q0.z, q0.w}, lz = f2{q1.x, q1.y};
+    f2 ux = f2{q1.z, q1.w}, uy = f2{q2.x, q2.y}, uz = f2{q2.z, q2.w};
+    f2 ax = __builtin_elementwise_fma(lx, bc(R.ix), -bc(R.pax));
+    f2 ay = __builtin_elementwise_fma(ly, bc(R.iy), -bc(R.pay));
+    f2 az = __builtin_elementwise_fma(lz, bc(R.iz), -bc(R.paz));
+    f2 bx = __builtin_elementwise_fma(ux, bc(R.ix), -bc(R.pbx));
+    f2 by = __builtin_elementwise_fma(uy, bc(R.iy), -bc(R.pby));
+    f2 bz = __builtin_elementwise_fma(uz, bc(R.iz), -bc(R.pbz));
+    const float tmin = -R.m;
+    float enA = fmaxf(fmaxf(fminf(ax.x, bx.x), fminf(ay.x, by.x)), fmaxf(fminf(az.x, bz.x), tmin));
+    float exA = fminf(fminf(fmaxf(ax.x, bx.x), fmaxf(ay.x, by.x)), fminf(fmaxf(az.x, bz.x), tmax));
+    float enB = fmaxf(fmaxf(fminf(ax.y, bx.y), fminf(ay.y, by.y)), fmaxf(fminf(az.y, bz.y), tmin));
+    float exB = fminf(fminf(fmaxf(ax.y, bx.y), fmaxf(ay.y, by.y)), fminf(fmaxf(az.y, bz.y), tmax));
+    hA = enA <= exA;
+    hB = enB <= exB;
+}
+
+// A cube of a leaf: its object-space box [-1/2 - hc, 1/2 + hc]^3 first (hc bounds how
+// far a reported object-space hit point can lie outside the unit cube, measured by
+// tools/cull_bounds_check.py, x32), then the 12 triangles if any lane can hit.
+__device__ __forceinline__ void cube_culled(const Rec16& Rc, V3 o, V3 d, float on, float tmax, float& bt,
+                                            uint32_t& bk, ScanCnt& c) {
+    V3 to = pt_mul(Rc.r0, Rc.r1, Rc.r2, o);
+    V3 td = vec3_mul(Rc.r0, Rc.r1, Rc.r2, d);
+    float m = fmaxf(fabsf(to.x), fmaxf(fabsf(to.y), fabsf(to.z)));
+    float hc = 32.f * RT_EPS * (2.f * m + 1.f + fmaf(Rc.rk.y, on, Rc.rk.z));
+    float b = 0.5f + hc;
+    float ix = safe_rcp(td.x), iy = safe_rcp(td.y), iz = safe_rcp(td.z);
+    float ax = (-b - to.x) * ix, bx = (b - to.x) * ix;
+    float ay = (-b - to.y) * iy, by = (b - to.y) * iy;
+    float az = (-b - to.z) * iz, bz = (b - to.z) * iz;
+    float en = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.f));
+    float ex = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tmax));
+    RT_OPS(c, cube_box);
+    if (__ballot(en <= ex)) {
+        RT_OPS(c, cube);
+        cube_scan(to, td, keyof(Rc.rk.x), bt, bk);
+    }
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(4))) uint4 cuint4;
+#else
+typedef const uint4 cuint4;
+#endif
+
+// One leaf: its runs of pairs / general spheres / triangle pairs / cubes.
+__device__ __forceinline__ void bvh_leaf(const DevScene& S, uint32_t li, V3 o, V3 d, float on, float tmax,
+                                         float& bt, uint32_t& bk, ScanCnt& c) {
+    cuint4* lp = (cuint4*)S.bvh_leaves + 2 * li;
+    uint4 a = lp[0], b = lp[1];
+    run_dsph(S, (int)a.x, (int)a.y, o, d, bt, bk, c);
+    run_gsph(S, (int)a.z, (int)a.w, o, d, bt, bk, c);
+    run_tri(S, (int)b.x, (int)b.y, o, d, bt, bk, c);
+    if (b.z < b.w) {
+        cfloat4* p = cptr(S.cube) + 4 * b.z;
+        for (uint32_t i = b.z; i < b.w; ++i, p += 4) cube_culled(ld_rec(p), o, d, on, tmax, bt, bk, c);
+    }
+}
+
 // "hit nearer than the light" for the current best t (the reference's test)
 __device__ __forceinline__ bool shadow_hit(V3 o, V3 d, float bt, float l2) {
     if (!(bt < __builtin_huge_valf())) return false;
@@ -329,59 +472,136 @@ __device__ __forceinline__ bool shadow_decided(V3 o, V3 d, float bt, float l2) {
     return bt < 0.f || shadow_hit(o, d, bt, l2);
 }
 
-__device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lpos) {
+// Walk the hierarchy.  SHADOW: t_max also stops at the light (tlim) and decided lanes
+// stop voting; the walk ends when every lane is decided.
+template <bool SHADOW>
+__device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, float tlim,
+                                         float l2, ScanCnt& c) {
+    const BvhRay R = bvh_ray(S, o, d);
+    uint32_t* stk = rt_bvh_stack + ((threadIdx.x >> 6) << 5);
+    uint32_t sp = 0;
+    uint32_t cur = S.bvh_root;
+    bool done = SHADOW ? shadow_decided(o, d, bt, l2) : false;
+    for (;;) {
+        // the lane's limit: its best t (a plane's t < 0 beats everything: no votes), the
+        // light for shadow rays, nothing once decided
+        float tmax = SHADOW ? (done ? -1.f : fminf(bt, tlim)) : bt;
+        float tnode = (tmax < 0.f) ? -__builtin_huge_valf() : tmax + R.m;
+        if (cur & BVH_LEAF) {
+            bvh_leaf(S, cur & ~BVH_LEAF, o, d, R.on, tmax, bt, bk, c);
+            if (SHADOW) {
+                done = shadow_decided(o, d, bt, l2);
+                if (__ballot(!done) == 0) break;
+            }
+        } else {
+            cfloat4* q = cptr(S.bvh_nodes) + 4 * cur;
+            float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+            bool hA, hB;
+            node_test(q0, q1, q2, R, tnode, hA, hB);
+            RT_OPS(c, node);
+            bool anyA = __ballot(hA) != 0, anyB = __ballot(hB) != 0;
+            uint32_t cA = __float_as_uint(q3.x), cB = __float_as_uint(q3.y);
+            if (anyA && anyB) {
+                uint32_t axis = __float_as_uint(q3.z);
+                float da = rfl(axis == 0 ? d.x : (axis == 1 ? d.y : d.z));
+                bool b_first = da < 0.f;  // child A holds the lower centroids
+                stk[sp++] = b_first ? cA : cB;
+                cur = b_first ? cB : cA;
+                continue;
+            }
+            if (anyA) {
+                cur = cA;
+                continue;
+            }
+            if (anyB) {
+                cur = cB;
+                continue;
+            }
+        }
+        if (sp == 0) break;
+        cur = rfl(stk[--sp]);
+    }
+}
+
+// Grazing pass: a hierarchy triangle whose plane some lane's ray meets at
+// sin(phi) < 1.01 sin(phi_min) is tested exactly for the wave (the hierarchy's bound
+// does not cover it).  Normals: {nAx nBx nAy nBy} {nAz nBz - -} per pair.
+__device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, ScanCnt& c) {
+    if (S.n_tri_bvh == 0) return;
+    float lim = S.graze_s2 * len2(d);
+    cfloat4* np = cptr(S.tri_nrm);
+    cfloat4* tp = cptr(S.tri);
+    for (int i = 0; i < S.n_tri_bvh; ++i, np += 2, tp += 6) {
+        float4 n0 = np[0], n1 = np[1];
+        f2 dn = (bc(d.x) * f2{n0.x, n0.y} + bc(d.y) * f2{n0.z, n0.w}) + bc(d.z) * f2{n1.x, n1.y};
+        f2 dn2 = dn * dn;
+        RT_OPS(c, graze);
+        if (__ballot(dn2.x < lim || dn2.y < lim)) {
+            RT_OPS(c, tri);
+            tri_pair(ld_tri(tp), o, d, bt, bk);
+        }
+    }
+}
+
+__device__ __forceinline__ void planes(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, ScanCnt& c) {
+    for (int i = 0; i < S.n_plane; ++i) {
+        RT_OPS(c, plane);
+        plane_one(cptr(S.plane) + 5 * i, o, d, bt, bk);
+    }
+}
+
+// the primitives outside the hierarchy (all of them when it is off)
+__device__ __forceinline__ void linear_rest(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, ScanCnt& c) {
+    run_dsph(S, S.n_dsph_bvh, S.n_dsph, o, d, bt, bk, c);
+    run_gsph(S, S.n_gsph_bvh, S.n_gsph, o, d, bt, bk, c);
+    run_tri(S, S.n_tri_bvh, S.n_tri, o, d, bt, bk, c);
+    run_cube(S, S.n_cube_bvh, S.n_cube, o, d, bt, bk, c);
+}
+
+// Scene::intersect (scene/mod.rs:98-116): the nearest (t, key) over every shape.
+__device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, ScanCnt& c) {
+    bt = __builtin_huge_valf();
+    bk = 0xFFFFFFFFu;
+    RT_STAT(0);
+    planes(S, o, d, bt, bk, c);
+    if (S.use_bvh) {
+        bvh_walk<false>(S, o, d, bt, bk, 0.f, 0.f, c);
+        graze_pass(S, o, d, bt, bk, c);
+    }
+    linear_rest(S, o, d, bt, bk, c);
+}
+
+// ------------------------------------------------------------------ shadow scan
+// PointLight::get_energy (scene/mod.rs:189-206): a FULL nearest-hit scan, then
+// "shadowed iff |hit.point - p|^2 < |pos - p|^2".  Exact early exit:
+//  * planes are scanned first; only planes can return t < 0 (plane.rs:62-83 has no
+//    t >= 0 check; spheres and triangles reject t < 0), so after them a lane whose best
+//    t is negative already holds its nearest hit;
+//  * for t >= 0 the reference's distance |(p + d*t) - p|^2 is non-decreasing in t (each
+//    rounded step is monotone), so once ANY hit has distance^2 < |pos - p|^2 the nearest
+//    one does too;
+//  * hits at t > tlim = ((1 + 2^-10) |pos - p| + 1e-5 (|p| + 1)) / |d| have a rounded
+//    distance^2 >= |pos - p|^2 (the margin covers the rounding of p + d t and of the
+//    norms) and can neither shadow nor hide a nearer hit: the walk stops at tlim.
+// A wave leaves the scan when every active lane is decided.  Returns `shadowed`.
+__device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lpos, ScanCnt& c) {
     const float l2 = len2(sub(lpos, o));
     float bt = __builtin_huge_valf();
     uint32_t bk = 0xFFFFFFFFu;
-    for (int i = 0; i < S.n_plane; ++i) plane_one(cptr(S.plane) + 5 * i, o, d, bt, bk);
+    planes(S, o, d, bt, bk, c);
     bool done = shadow_decided(o, d, bt, l2);
     if (__ballot(!done) == 0) goto finish;
-    {
-        cfloat4* p = cptr(S.cube);
-        Rec16 cur = ld_rec(p);
-        for (int i = 0; i < S.n_cube; ++i) {
-            Rec16 nxt = ld_rec(p + 4 * (i + 1));
-            V3 to = pt_mul(cur.r0, cur.r1, cur.r2, o);
-            V3 td = vec3_mul(cur.r0, cur.r1, cur.r2, d);
-            cube_scan(to, td, keyof(cur.rk.x), bt, bk);
-            cur = nxt;
-            if ((i & 3) == 3) {
-                done = shadow_decided(o, d, bt, l2);
-                if (__ballot(!done) == 0) goto finish;
-            }
-        }
+    if (S.use_bvh) {
+        float on = sqrtf(len2(o));
+        float tlim = (sqrtf(l2) * (1.f + 0.0009765625f) + 1e-5f * (on + 1.f)) / sqrtf(len2(d));
+        bvh_walk<true>(S, o, d, bt, bk, tlim, l2, c);
+        done = shadow_decided(o, d, bt, l2);
+        if (__ballot(!done) == 0) goto finish;
+        graze_pass(S, o, d, bt, bk, c);
+        done = shadow_decided(o, d, bt, l2);
+        if (__ballot(!done) == 0) goto finish;
     }
-    {
-        cfloat4* p = cptr(S.dsph);
-        SphPair cur = ld_sph(p);
-        for (int i = 0; i < S.n_dsph; ++i) {
-            SphPair nxt = ld_sph(p + 4 * (i + 1));
-            sph_pair(cur, o, d, bt, bk);
-            cur = nxt;
-            if ((i & 15) == 15) {
-                done = shadow_decided(o, d, bt, l2);
-                if (__ballot(!done) == 0) goto finish;
-            }
-        }
-    }
-    {
-        cfloat4* p = cptr(S.gsph);
-        Rec16 cur = ld_rec(p);
-        for (int i = 0; i < S.n_gsph; ++i) {
-            Rec16 nxt = ld_rec(p + 4 * (i + 1));
-            sph_general(cur, o, d, bt, bk);
-            cur = nxt;
-        }
-    }
-    {
-        cfloat4* p = cptr(S.tri);
-        TriPair cur = ld_tri(p);
-        for (int i = 0; i < S.n_tri; ++i) {
-            TriPair nxt = ld_tri(p + 6 * (i + 1));
-            tri_pair(cur, o, d, bt, bk);
-            cur = nxt;
-        }
-    }
+    linear_rest(S, o, d, bt, bk, c);
 finish:
     return shadow_hit(o, d, bt, l2);
 }

@@ -46,6 +46,23 @@ __device__ __forceinline__ PixelRef pixel_of(const WaveParams& P, uint32_t item)
     return r;
 }
 
+__device__ __forceinline__ uint32_t spread5(uint32_t v) {  // abcde -> a..b..c..d..e
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+__device__ __forceinline__ uint32_t morton15(const DevScene& S, V3 p) {
+    float sc = 16.f / S.bvh_r;
+    int x = (int)fminf(fmaxf((p.x - S.bvh_cx) * sc + 16.f, 0.f), 31.f);
+    int y = (int)fminf(fmaxf((p.y - S.bvh_cy) * sc + 16.f, 0.f), 31.f);
+    int z = (int)fminf(fmaxf((p.z - S.bvh_cz) * sc + 16.f, 0.f), 31.f);
+    return (spread5((uint32_t)x) << 2) | (spread5((uint32_t)y) << 1) | spread5((uint32_t)z);
+}
+__device__ __forceinline__ uint32_t octant(V3 d) {
+    return (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u);
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
     uint32_t lane = lane_id();
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -79,6 +96,8 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
     if (blockIdx.x == 0 && threadIdx.x == 0) P.levels[2 * (level + 1)] = next_off;
     const uint32_t lane = lane_id();
     uint32_t n_node = 0, n_pix = 0;
+    ScanCnt cnt;
+    cnt_init(cnt);
     // point lights: one shadow ray each per hit (mod.rs:189-206); ambient lights: none
     uint32_t n_point = 0;
     for (int li = 0; li < S.n_lights; ++li) n_point += S.lights[li].kind == RT_LIGHT_POINT ? 1u : 0u;
@@ -112,19 +131,20 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
                     }
                 }
             } else {
-                const Task& T = P.tasks[n];
+                const Task& T = P.tasks[P.perm ? P.perm[n] : n];
                 ro = v3(T.ox, T.oy, T.oz);
                 rd = v3(T.dx, T.dy, T.dz);
                 parent = T.parent;
             }
         }
         bool want_refl = false, want_refr = false, hit = false;
+        uint32_t mort = 0;  // Morton code of the shadow-ray origin (queue ordering key)
         V3 rro = v3(0, 0, 0), rrd = v3(0, 0, 0), tro = v3(0, 0, 0), trd = v3(0, 0, 0);
         if (active) {
             n_node++;
             float bt;
             uint32_t bk;
-            scan(S, ro, rd, bt, bk);
+            scan(S, ro, rd, bt, bk, cnt);
             if (bk == 0xFFFFFFFFu) {
                 P.nodes[n].flags = NODE_MISS;  // trace_ray -> BLACK; the parent slot stays 0
             } else {
@@ -138,6 +158,7 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
                 V3 kd = tex_eval(M.diffuse, h.tu, h.tv);
                 V3 ks = tex_eval(M.specular, h.tu, h.tv);
                 V3 ps = add(h.p, mul(h.n, 0.0002f));  // render.rs:147
+                if (P.shadow_keys) mort = morton15(S, ps);
                 NodeRec rec;
                 rec.ambx = ka.x * S.amb_r; rec.amby = ka.y * S.amb_g; rec.ambz = ka.z * S.amb_b;
                 rec.psx = ps.x; rec.psy = ps.y; rec.psz = ps.z;
@@ -195,6 +216,10 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
             if (slot < P.capacity) {
                 Task T = {rro.x, rro.y, rro.z, rrd.x, rrd.y, rrd.z, (n << 1) | 0u, 0u};
                 P.tasks[slot] = T;
+                if (P.task_keys) {
+                    P.task_keys[slot] = (octant(rrd) << RT_MORTON_BITS) | morton15(S, rro);
+                    P.task_vals[slot] = slot;
+                }
             } else {
                 atomicOr(P.overflow, 1u);
             }
@@ -205,6 +230,10 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
             if (slot < P.capacity) {
                 Task T = {tro.x, tro.y, tro.z, trd.x, trd.y, trd.z, (n << 1) | 1u, 0u};
                 P.tasks[slot] = T;
+                if (P.task_keys) {
+                    P.task_keys[slot] = (octant(trd) << RT_MORTON_BITS) | morton15(S, tro);
+                    P.task_vals[slot] = slot;
+                }
             } else {
                 atomicOr(P.overflow, 1u);
             }
@@ -226,14 +255,16 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
                     if (S.lights[li].kind != RT_LIGHT_POINT) continue;
                     uint32_t slot = sbase + k * nh + rank_h;
                     k++;
-                    if (slot < P.shadow_capacity)
+                    if (slot < P.shadow_capacity) {
                         P.shadow[slot] = (n << 5) | (uint32_t)li;
-                    else
+                        if (P.shadow_keys) P.shadow_keys[slot] = ((uint32_t)li << RT_MORTON_BITS) | mort;
+                    } else
                         atomicOr(P.overflow, 2u);
                 }
             }
         }
     }
+    cnt_flush(cnt, S.scan_ops);
     for (int o = 32; o > 0; o >>= 1) {
         n_node += __shfl_xor(n_node, o);
         n_pix += __shfl_xor(n_pix, o);
@@ -252,11 +283,13 @@ __global__ __launch_bounds__(256) void shadow_kernel(WaveParams P) {
     const uint32_t lane = lane_id();
     const uint32_t stride = gridDim.x * blockDim.x;
     uint32_t n_shadow = 0;
+    ScanCnt cnt;
+    cnt_init(cnt);
     const uint32_t wave_base = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u;
     for (uint32_t base = wave_base; base < count; base += stride) {
         const uint32_t t = base + lane;
         if (t < count) {
-            uint32_t e = P.shadow[t];
+            uint32_t e = P.shadow_in[t];
             uint32_t n = e >> 5, li = e & 31u;
             const NodeRec& R = P.nodes[n];
             V3 ps = v3(R.psx, R.psy, R.psz);
@@ -264,9 +297,10 @@ __global__ __launch_bounds__(256) void shadow_kernel(WaveParams P) {
             V3 lpos = v3(L.px, L.py, L.pz);
             V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
             n_shadow++;
-            if (!shadow_scan(S, ps, ldir, lpos)) atomicOr(&P.nodes[n].litmask, 1u << li);
+            if (!shadow_scan(S, ps, ldir, lpos, cnt)) atomicOr(&P.nodes[n].litmask, 1u << li);
         }
     }
+    cnt_flush(cnt, S.scan_ops);
     for (int o = 32; o > 0; o >>= 1) n_shadow += __shfl_xor(n_shadow, o);
     if (lane == 0 && P.ray_counters && n_shadow) atomicAdd(P.ray_counters + 1, (unsigned long long)n_shadow);
 }

@@ -1,0 +1,36 @@
+"""Per-frame test counts of the scans (rt_scene_scan_ops), hierarchy on vs off.
+
+usage: python tools/scan_ops.py [config=3] [width=1920] [height=1080] [depth=8]
+Prints, per mode, the lane-weighted counts of each test kind, per traced ray (node +
+shadow), and the frame's kernel time.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from rust_tracer_amd import DeviceScene, SceneDesc
+
+
+def run(config, w, h, depth, bvh):
+    if not bvh:
+        os.environ["RT_BVH"] = "0"
+    try:
+        s = DeviceScene(SceneDesc.synth_config(config))
+    finally:
+        os.environ.pop("RT_BVH", None)
+    s.render(w, h, depth)
+    s.scan_ops(reset=True)
+    _, cnt, ms, _ = s.render(w, h, depth)
+    ops = s.scan_ops()
+    rays = cnt["node_rays"] + cnt["shadow_rays"]
+    print(f"bvh={bvh} kernel {ms:.2f} ms  node rays {cnt['node_rays']} shadow rays {cnt['shadow_rays']}")
+    for k, v in ops.items():
+        print(f"   {k:12s} {v:14d}  per ray {v / rays:9.2f}")
+    s.close()
+
+
+if __name__ == "__main__":
+    a = [int(x) for x in sys.argv[1:]]
+    config, w, h, depth = (a + [3, 1920, 1080, 8][len(a):])[:4]
+    run(config, w, h, depth, True)
+    run(config, w, h, depth, False)
