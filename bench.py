@@ -36,9 +36,10 @@ PEAK_HBM_GBPS = 8000.0       # MI355X HBM3E peak
 # "Roofline"): reference arithmetic of the ray-primitive tests (sphere
 # 57, triangle 52, cube 12 x 52 + 33 for the ray transform, plane 49), 12 FMAs = 24 flops
 # per 2-wide child-box test, 45 flops for a cube's object-space box (its transform shared
-# with the triangles), 6 per triangle for the grazing check.
+# with the triangles), 6 per grazing cone test and 48 per 8-normal grazing test.
 OP_FLOPS = {"node_pairs": 24, "dsph_pairs": 2 * 57, "gsph": 57, "tri_pairs": 2 * 52,
-            "cube_boxes": 33 + 12, "cubes": 12 * 52, "graze_pairs": 12, "planes": 49}
+            "cube_boxes": 33 + 12, "cubes": 12 * 52, "graze_cones": 6, "planes": 49,
+            "graze_normals": 48}
 
 
 def parse():

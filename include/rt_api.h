@@ -196,10 +196,10 @@ uint64_t rt_scene_device_bytes(const rt_scene* scene);
 
 /* Lane-weighted counts of the ray-primitive and ray-box tests the scene's scans ran
  * since the last reset, in this order: child-box pairs, diagonal-sphere pairs, general
- * spheres, triangle pairs, cube boxes, full cubes (12 triangles), grazing checks
- * (triangle pairs), planes.  Synchronises the device; reset != 0 zeroes the counts
- * after reading.  `out` may be NULL (reset only). */
-#define RT_SCAN_OPS_N 8
+ * spheres, triangle pairs, cube boxes, full cubes (12 triangles), grazing cone tests
+ * (blocks of 8 triangles), planes, grazing normal tests (blocks of 8).  Synchronises
+ * the device; reset != 0 zeroes the counts after reading.  `out` may be NULL. */
+#define RT_SCAN_OPS_N 9
 rt_status rt_scene_scan_ops(rt_scene* scene, uint64_t* out, uint32_t n, int32_t reset);
 
 /* 1 if the scene's scans walk the culling hierarchy (the default; RT_BVH=0 in the

@@ -249,8 +249,8 @@ class DeviceScene:
         """True when scans walk the culling hierarchy (RT_BVH=0 at creation turns it off)."""
         return bool(self._L.rt_scene_uses_bvh(self.h))
 
-    SCAN_OPS = ("node_pairs", "dsph_pairs", "gsph", "tri_pairs", "cube_boxes", "cubes", "graze_pairs",
-                "planes")
+    SCAN_OPS = ("node_pairs", "dsph_pairs", "gsph", "tri_pairs", "cube_boxes", "cubes", "graze_cones",
+                "planes", "graze_normals")
 
     def scan_ops(self, reset=False):
         """Lane-weighted test counts since the last reset (rt_scene_scan_ops)."""

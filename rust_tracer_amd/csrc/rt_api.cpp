@@ -152,7 +152,7 @@ struct CubeIn {
 };
 
 struct RunLayout {
-    std::vector<float> dsph, gsph, tri, cube, nodes, tri_nrm;
+    std::vector<float> dsph, gsph, tri, cube, nodes, graze_blk, graze_tri;
     std::vector<uint32_t> leaves;
     uint32_t root = BVH_LEAF;
     bool use = false;
@@ -284,15 +284,97 @@ F3 unit_normal(const TriIn& t) {
     double l = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
     return f3((float)(n[0] / l), (float)(n[1] / l), (float)(n[2] / l));
 }
-void emit_tri_nrm(std::vector<float>& v, const TriIn& A, const TriIn* B) {
-    // a padding partner never hits, so it never needs the grazing pass: huge normal
-    F3 na = unit_normal(A), nb = B ? unit_normal(*B) : f3(1e18f, 1e18f, 1e18f);
-    put4(v, na.x, nb.x, na.y, nb.y);
-    put4(v, na.z, nb.z, 0.f, 0.f);
-}
 void emit_cube(std::vector<float>& v, const CubeIn& A, float lf, float sn) {
     for (int r = 0; r < 3; r++) put4(v, A.inv[r * 4], A.inv[r * 4 + 1], A.inv[r * 4 + 2], A.inv[r * 4 + 3]);
     put4(v, A.key, lf, sn, 0.f);
+}
+
+// Grazing pass data (rt_scan.hpp graze_pass): the hierarchy's triangles ordered by
+// normal direction (sign-free) in blocks of 8, each with a cone {axis, s^2}: a ray with
+// (d.axis)^2 > s^2 |d|^2 meets every plane of the block at sin(phi) > 1.01 sin(phi_min).
+// Block: {ax ay az s^2} {nx0-3} {nx4-7} {ny0-3} {ny4-7} {nz0-3} {nz4-7} {-}; its triangles
+// as 4 pairs in graze_tri.
+void build_graze(const std::vector<TriIn>& tris, const std::vector<char>& in_tri, RunLayout& L) {
+    struct G {
+        const TriIn* t;
+        double n[3];
+        uint32_t code;
+    };
+    std::vector<G> g;
+    for (size_t i = 0; i < tris.size(); i++) {
+        if (!in_tri[i]) continue;
+        F3 u = unit_normal(tris[i]);
+        double n[3] = {u.x, u.y, u.z};
+        int big = 0;
+        for (int k = 1; k < 3; k++)
+            if (std::fabs(n[k]) > std::fabs(n[big])) big = k;
+        if (n[big] < 0)
+            for (double& x : n) x = -x;
+        // octahedral map of the (sign-free) normal -> 2 x 8 bits, Morton order
+        double l1 = std::fabs(n[0]) + std::fabs(n[1]) + std::fabs(n[2]);
+        double px = n[0] / l1, py = n[1] / l1;
+        if (n[2] < 0) {
+            double qx = (1 - std::fabs(py)) * (px >= 0 ? 1 : -1), qy = (1 - std::fabs(px)) * (py >= 0 ? 1 : -1);
+            px = qx;
+            py = qy;
+        }
+        uint32_t ix = (uint32_t)std::min(255.0, std::max(0.0, (px * 0.5 + 0.5) * 256.0));
+        uint32_t iy = (uint32_t)std::min(255.0, std::max(0.0, (py * 0.5 + 0.5) * 256.0));
+        uint32_t code = 0;
+        for (int b = 0; b < 8; b++) code |= (((ix >> b) & 1u) << (2 * b)) | (((iy >> b) & 1u) << (2 * b + 1));
+        g.push_back(G{&tris[i], {n[0], n[1], n[2]}, code});
+    }
+    std::stable_sort(g.begin(), g.end(), [](const G& a, const G& b) { return a.code < b.code; });
+    const double phi = std::asin(1.01 * GRAZE_SIN) + 1e-4;
+    for (size_t b0 = 0; b0 < g.size(); b0 += 8) {
+        size_t b1 = std::min(g.size(), b0 + 8);
+        double a[3] = {0, 0, 0};
+        for (size_t i = b0; i < b1; i++)
+            for (int k = 0; k < 3; k++) a[k] += g[i].n[k];
+        double la = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+        double s2 = 1.0;  // no usable cone: always test the normals
+        if (la > 1e-6) {
+            for (double& x : a) x /= la;
+            double cmin = 1.0;
+            for (size_t i = b0; i < b1; i++)
+                cmin = std::min(cmin, std::fabs(a[0] * g[i].n[0] + a[1] * g[i].n[1] + a[2] * g[i].n[2]));
+            double theta = std::acos(std::min(1.0, cmin)) + 1e-4;
+            if (theta + phi < 1.5707) s2 = std::pow(std::sin(theta + phi), 2) * (1 + 1e-4);
+        } else {
+            a[0] = 1;
+            a[1] = a[2] = 0;
+        }
+        float nx[8], ny[8], nz[8];
+        for (int k = 0; k < 8; k++) {
+            if (b0 + k < b1) {
+                F3 u = unit_normal(*g[b0 + k].t);
+                nx[k] = u.x;
+                ny[k] = u.y;
+                nz[k] = u.z;
+            } else {  // padding: never grazes (and its pair slot is a degenerate triangle)
+                nx[k] = ny[k] = nz[k] = 1e18f;
+            }
+        }
+        put4(L.graze_blk, (float)a[0], (float)a[1], (float)a[2], up_f(std::min(1.0, s2)));
+        put4(L.graze_blk, nx[0], nx[1], nx[2], nx[3]);
+        put4(L.graze_blk, nx[4], nx[5], nx[6], nx[7]);
+        put4(L.graze_blk, ny[0], ny[1], ny[2], ny[3]);
+        put4(L.graze_blk, ny[4], ny[5], ny[6], ny[7]);
+        put4(L.graze_blk, nz[0], nz[1], nz[2], nz[3]);
+        put4(L.graze_blk, nz[4], nz[5], nz[6], nz[7]);
+        put4(L.graze_blk, 0.f, 0.f, 0.f, 0.f);
+        for (int k = 0; k < 8; k += 2) {
+            const TriIn* A = (b0 + k < b1) ? g[b0 + k].t : nullptr;
+            const TriIn* B = (b0 + k + 1 < b1) ? g[b0 + k + 1].t : nullptr;
+            if (A) emit_tri_pair(L.graze_tri, *A, B);
+            else {
+                TriIn pad;
+                pad.v[0] = pad.e1 = pad.e2 = f3(0, 0, 0);
+                pad.key = keyf(0xFFFFFFF0u);
+                emit_tri_pair(L.graze_tri, pad, nullptr);
+            }
+        }
+    }
 }
 
 // Lays out the runs: hierarchy primitives leaf by leaf, then the linear rest.  Within
@@ -419,6 +501,16 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
         L.m0 = up_f(m0 * (1 + 1e-6));
         g1 += SAFETY_SLAB * 16.0 * FEPS;
         g0 += SAFETY_SLAB * 8.0 * FEPS * (3.0 * Cn + R);
+        if (const char* hs = std::getenv("RT_DEBUG_H_SCALE")) {  // measurement only: NOT conservative
+            double k = std::atof(hs);
+            g2 *= k;
+            g1 *= k;
+            g0 *= k;
+            m1 *= k;
+            m0 *= k;
+            L.m1 = up_f(m1);
+            L.m0 = up_f(m0);
+        }
         L.r = up_f(R);
         L.g2 = up_f(g2 * (1 + 1e-6));
         L.g1 = up_f(g1 * (1 + 1e-6));
@@ -453,7 +545,6 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
             for (size_t k = 0; k < ts.size(); k += 2) {
                 const TriIn* b = (k + 1 < ts.size()) ? ts[k + 1] : nullptr;
                 emit_tri_pair(L.tri, *ts[k], b);
-                emit_tri_nrm(L.tri_nrm, *ts[k], b);
             }
             rec[5] = (uint32_t)(L.tri.size() / 24);
             rec[6] = (uint32_t)(L.cube.size() / 16);
@@ -473,6 +564,7 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
                          T.nodes.size(), T.leaves.size(), T.depth, max_leaf, L.c[0], L.c[1], L.c[2], L.r, L.g2,
                          L.g1, L.g0, L.m1, L.m0);
         }
+        build_graze(tris, in_tri, L);
         L.n_dsph_bvh = (int)(L.dsph.size() / 16);
         L.n_gsph_bvh = (int)(L.gsph.size() / 16);
         L.n_tri_bvh = (int)(L.tri.size() / 24);
@@ -525,10 +617,22 @@ struct Workspace {
     uint32_t* h_count = nullptr;     // pinned: a level's (offset, count)
 };
 
-// RT_SORT=0 keeps the queues in production order (A/B measurements).
+// RT_SORT=0 keeps the queues in production order, RT_SORT=shadow orders only the
+// shadow queue (A/B measurements).
 bool sort_enabled() {
     const char* e = std::getenv("RT_SORT");
     return !(e && std::strcmp(e, "0") == 0);
+}
+bool sort_tasks_enabled() {
+    const char* e = std::getenv("RT_SORT");
+    return !(e && std::strcmp(e, "shadow") == 0);
+}
+// Task ordering key (16 bits): 1 (default) = cube-map face of the direction x 2x2 cells
+// | 11-bit Morton origin; 0 = octant | 13-bit Morton; 2 = face x 4x4 | 9-bit Morton.
+// RT_TASK_KEY overrides (A/B): config 3 1080p frame 10.35 / 10.77 / 10.39 ms.
+uint32_t task_key_mode() {
+    const char* e = std::getenv("RT_TASK_KEY");
+    return e ? (uint32_t)std::atoi(e) : 1u;
 }
 
 // Device path: "wave" (level-synchronous, default) or "mega" (per-pixel megakernel),
@@ -767,7 +871,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
         size_t off;
     };
     static const unsigned long long zero_ops[RT_OPS_N] = {0};
-    Sec secs[13] = {{dsph.data(), dsph.size() * 4, 0},       {gsph.data(), gsph.size() * 4, 0},
+    Sec secs[14] = {{dsph.data(), dsph.size() * 4, 0},       {gsph.data(), gsph.size() * 4, 0},
                     {tri.data(), tri.size() * 4, 0},         {cube.data(), cube.size() * 4, 0},
                     {plane.data(), plane.size() * 4, 0},     {cubetri.data(), cubetri.size() * 4, 0},
                     {shapes.data(), shapes.size() * sizeof(ShapeRec), 0},
@@ -775,8 +879,9 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
                     {lights.data(), lights.size() * sizeof(LightRec), 0},
                     {lay.nodes.data(), lay.nodes.size() * 4, 0},
                     {lay.leaves.data(), lay.leaves.size() * 4, 0},
-                    {lay.tri_nrm.data(), lay.tri_nrm.size() * 4, 0},
-                    {zero_ops, sizeof(zero_ops), 0}};
+                    {lay.graze_blk.data(), lay.graze_blk.size() * 4, 0},
+                    {zero_ops, sizeof(zero_ops), 0},
+                    {lay.graze_tri.data(), lay.graze_tri.size() * 4, 0}};
     size_t total = 0;
     for (auto& s : secs) {
         s.off = total;
@@ -815,9 +920,12 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     S.n_mats = (int32_t)d->n_materials;
     S.bvh_nodes = (const float4*)at(9);
     S.bvh_leaves = (const uint4*)at(10);
-    S.tri_nrm = (const float4*)at(11);
+    S.graze_blk = (const float4*)at(11);
     S.scan_ops = (unsigned long long*)at(12);
+    S.graze_tri = (const float4*)at(13);
+    S.n_graze_blk = (int32_t)(lay.graze_blk.size() / 32);
     S.bvh_root = lay.root;
+    S.n_bvh_nodes = (int32_t)(lay.nodes.size() / 16);
     S.use_bvh = lay.use ? 1 : 0;
     S.n_dsph_bvh = lay.n_dsph_bvh;
     S.n_gsph_bvh = lay.n_gsph_bvh;
@@ -999,7 +1107,14 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
         w.shadow_capacity = (uint32_t)want_sh;
     }
     const bool sort_on = s->S.use_bvh && sort_enabled();
-    const int task_bits = RT_MORTON_BITS + 3, shadow_bits = RT_MORTON_BITS + 5;
+    const bool sort_tasks = sort_tasks_enabled();
+    p.key_mode = task_key_mode();
+    // 16-bit keys (two 8-bit radix passes): task = octant | 13 Morton bits; shadow =
+    // light index | the Morton bits that fit (all 15 above 16 lights' worth of bits)
+    uint32_t lbits = 0;
+    while ((1u << lbits) < s->S.n_lights) lbits++;
+    p.light_shift = lbits <= 1 ? 15u : (16u - lbits > 15u ? 15u : 16u - lbits);
+    const int task_bits = 16, shadow_bits = (int)(p.light_shift + lbits);
     if (sort_on) {
         if (w.sort_capacity < w.capacity) {
             for (uint32_t** b : {&w.task_keys, &w.task_vals, &w.perm, &w.keys_alt}) {
@@ -1082,10 +1197,12 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
         if (off >= w.capacity) break;  // overflowed: the flag is already set
         cnt = std::min(cnt, w.capacity - off);
         if (cnt == 0) break;
-        size_t bytes = w.sort_tmp_bytes;
-        HIP_TRY(sort_pairs_u32(w.sort_tmp, bytes, w.task_keys + off, w.keys_alt, w.task_vals + off, w.perm + off,
-                               cnt, task_bits, stream));
-        p.perm = w.perm;
+        if (sort_tasks) {
+            size_t bytes = w.sort_tmp_bytes;
+            HIP_TRY(sort_pairs_u32(w.sort_tmp, bytes, w.task_keys + off, w.keys_alt, w.task_vals + off,
+                                   w.perm + off, cnt, task_bits, stream));
+            p.perm = w.perm;
+        }
         HIP_TRY(launch_wave_trace(p, k, tb, stream));
         used = k + 1;
     }

@@ -72,8 +72,11 @@ struct DevScene {
     // linearly for every ray.
     const float4* bvh_nodes;   // 4 float4 per node: both child boxes + child pointers
     const uint4* bvh_leaves;   // 2 uint4 per leaf: [dsph b,e gsph b,e] [tri b,e cube b,e]
-    const float4* tri_nrm;     // 2 float4 per hierarchy triangle pair: unit normals (A,B)
+    const float4* graze_blk;   // grazing pass: 8 float4 per block of 8 triangles (cone + normals)
+    const float4* graze_tri;   // ... and the block's triangles as 4 pairs
+    int32_t n_graze_blk;
     uint32_t bvh_root;         // child pointer (BVH_LEAF bit: a leaf)
+    int32_t n_bvh_nodes;
     int32_t use_bvh;
     int32_t n_dsph_bvh, n_gsph_bvh, n_tri_bvh, n_cube_bvh;
     // per ray, D = |o - c| + r: box inflation h(D) = (g2 D + g1) D + g0 and t-margin
@@ -92,9 +95,10 @@ enum : int {
     RT_OPS_TRI = 3,     // loose triangle pairs
     RT_OPS_CUBE_BOX = 4,  // object-space cube box tests
     RT_OPS_CUBE = 5,    // full cubes (12 triangles)
-    RT_OPS_GRAZE = 6,   // grazing checks (triangle pairs)
+    RT_OPS_GRAZE = 6,   // grazing cone tests (blocks of 8 triangles)
     RT_OPS_PLANE = 7,   // planes
-    RT_OPS_N = 8
+    RT_OPS_GRAZE_N = 8, // grazing normal tests (blocks of 8 whose cone some lane meets)
+    RT_OPS_N = 9
 };
 
 // Everything one launch needs.
@@ -163,6 +167,8 @@ struct WaveParams {
     const uint32_t* perm;              // [capacity] or null: level-k slot -> task slot
     uint32_t* shadow_keys;             // [shadow_capacity]
     const uint32_t* shadow_in;         // the shadow entries the shadow kernel reads
+    uint32_t key_mode;                 // task key variant (A/B)
+    uint32_t light_shift;              // shadow key = (light << light_shift) | (Morton >> (15 - light_shift))
 };
 
 // 15-bit Morton code of a point in the 32^3 grid over [c - r, c + r]^3 (clamped)

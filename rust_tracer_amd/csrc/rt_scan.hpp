@@ -264,10 +264,10 @@ __device__ __forceinline__ void plane_one(cfloat4* r, V3 o, V3 d, float& bt, uin
 // Lane-weighted counts of every test the scan runs (RT_OPS_*): wave-uniform, kept in
 // SGPRs, added to DevScene::scan_ops once per wave when a kernel ends.
 struct ScanCnt {
-    uint32_t node, dsph, gsph, tri, cube_box, cube, graze, plane;
+    uint32_t node, dsph, gsph, tri, cube_box, cube, graze, plane, graze_n;
 };
 __device__ __forceinline__ void cnt_init(ScanCnt& c) {
-    c.node = c.dsph = c.gsph = c.tri = c.cube_box = c.cube = c.graze = c.plane = 0;
+    c.node = c.dsph = c.gsph = c.tri = c.cube_box = c.cube = c.graze = c.plane = c.graze_n = 0;
 }
 __device__ __forceinline__ uint32_t active_lanes() { return (uint32_t)__builtin_popcountll(__ballot(1)); }
 #define RT_OPS(c, f) ((c).f += active_lanes())
@@ -286,6 +286,7 @@ __device__ __forceinline__ void cnt_flush(const ScanCnt& c, unsigned long long* 
         cnt_add(dst + RT_OPS_CUBE, c.cube);
         cnt_add(dst + RT_OPS_GRAZE, c.graze);
         cnt_add(dst + RT_OPS_PLANE, c.plane);
+        cnt_add(dst + RT_OPS_GRAZE_N, c.graze_n);
     }
 }
 
@@ -474,9 +475,16 @@ __device__ __forceinline__ bool shadow_decided(V3 o, V3 d, float bt, float l2) {
 
 // Walk the hierarchy.  SHADOW: t_max also stops at the light (tlim) and decided lanes
 // stop voting; the walk ends when every lane is decided.
-template <bool SHADOW>
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(3))) float4 lfloat4;
+#else
+typedef const float4 lfloat4;
+#endif
+
+// LDS: node records staged in LDS by the kernel (lnodes != null), else read via SMEM
+template <bool SHADOW, bool LDS>
 __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, float tlim,
-                                         float l2, ScanCnt& c) {
+                                         float l2, ScanCnt& c, lfloat4* lnodes) {
     const BvhRay R = bvh_ray(S, o, d);
     uint32_t* stk = rt_bvh_stack + ((threadIdx.x >> 6) << 5);
     uint32_t sp = 0;
@@ -494,8 +502,20 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
                 if (__ballot(!done) == 0) break;
             }
         } else {
-            cfloat4* q = cptr(S.bvh_nodes) + 4 * cur;
-            float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+            float4 q0, q1, q2, q3;
+            if (LDS) {
+                lfloat4* q = lnodes + 4 * cur;
+                q0 = q[0];
+                q1 = q[1];
+                q2 = q[2];
+                q3 = q[3];
+            } else {
+                cfloat4* q = cptr(S.bvh_nodes) + 4 * cur;
+                q0 = q[0];
+                q1 = q[1];
+                q2 = q[2];
+                q3 = q[3];
+            }
             bool hA, hB;
             node_test(q0, q1, q2, R, tnode, hA, hB);
             RT_OPS(c, node);
@@ -523,22 +543,46 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
     }
 }
 
-// Grazing pass: a hierarchy triangle whose plane some lane's ray meets at
-// sin(phi) < 1.01 sin(phi_min) is tested exactly for the wave (the hierarchy's bound
-// does not cover it).  Normals: {nAx nBx nAy nBy} {nAz nBz - -} per pair.
+// Grazing pass: every hierarchy triangle whose plane some lane's ray meets at
+// sin(phi) < 1.01 sin(phi_min) is tested exactly for the wave (the hierarchy's bounds
+// do not cover it).  Triangles come in blocks of 8 with similar normals; a block whose
+// normal cone no lane's direction can graze is skipped after one dot product.
 __device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, ScanCnt& c) {
-    if (S.n_tri_bvh == 0) return;
-    float lim = S.graze_s2 * len2(d);
-    cfloat4* np = cptr(S.tri_nrm);
-    cfloat4* tp = cptr(S.tri);
-    for (int i = 0; i < S.n_tri_bvh; ++i, np += 2, tp += 6) {
-        float4 n0 = np[0], n1 = np[1];
-        f2 dn = (bc(d.x) * f2{n0.x, n0.y} + bc(d.y) * f2{n0.z, n0.w}) + bc(d.z) * f2{n1.x, n1.y};
-        f2 dn2 = dn * dn;
+    if (S.n_graze_blk == 0) return;
+    const float dd = len2(d);
+    const float lim = S.graze_s2 * dd;
+    cfloat4* g = cptr(S.graze_blk);
+    cfloat4* tp = cptr(S.graze_tri);
+    for (int b = 0; b < S.n_graze_blk; ++b, g += 8, tp += 24) {
+        float4 a = g[0];
+        float ca = (d.x * a.x + d.y * a.y) + d.z * a.z;
         RT_OPS(c, graze);
-        if (__ballot(dn2.x < lim || dn2.y < lim)) {
+        if (!__ballot(ca * ca <= a.w * dd)) continue;
+        RT_OPS(c, graze_n);
+        float4 x0 = g[1], x1 = g[2], y0 = g[3], y1 = g[4], z0 = g[5], z1 = g[6];
+        f2 n01 = (bc(d.x) * f2{x0.x, x0.y} + bc(d.y) * f2{y0.x, y0.y}) + bc(d.z) * f2{z0.x, z0.y};
+        f2 n23 = (bc(d.x) * f2{x0.z, x0.w} + bc(d.y) * f2{y0.z, y0.w}) + bc(d.z) * f2{z0.z, z0.w};
+        f2 n45 = (bc(d.x) * f2{x1.x, x1.y} + bc(d.y) * f2{y1.x, y1.y}) + bc(d.z) * f2{z1.x, z1.y};
+        f2 n67 = (bc(d.x) * f2{x1.z, x1.w} + bc(d.y) * f2{y1.z, y1.w}) + bc(d.z) * f2{z1.z, z1.w};
+        n01 *= n01;
+        n23 *= n23;
+        n45 *= n45;
+        n67 *= n67;
+        if (__ballot(n01.x < lim || n01.y < lim)) {
             RT_OPS(c, tri);
             tri_pair(ld_tri(tp), o, d, bt, bk);
+        }
+        if (__ballot(n23.x < lim || n23.y < lim)) {
+            RT_OPS(c, tri);
+            tri_pair(ld_tri(tp + 6), o, d, bt, bk);
+        }
+        if (__ballot(n45.x < lim || n45.y < lim)) {
+            RT_OPS(c, tri);
+            tri_pair(ld_tri(tp + 12), o, d, bt, bk);
+        }
+        if (__ballot(n67.x < lim || n67.y < lim)) {
+            RT_OPS(c, tri);
+            tri_pair(ld_tri(tp + 18), o, d, bt, bk);
         }
     }
 }
@@ -565,7 +609,7 @@ __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, u
     RT_STAT(0);
     planes(S, o, d, bt, bk, c);
     if (S.use_bvh) {
-        bvh_walk<false>(S, o, d, bt, bk, 0.f, 0.f, c);
+        bvh_walk<false, false>(S, o, d, bt, bk, 0.f, 0.f, c, nullptr);
         graze_pass(S, o, d, bt, bk, c);
     }
     linear_rest(S, o, d, bt, bk, c);
@@ -584,7 +628,8 @@ __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, u
 //    distance^2 >= |pos - p|^2 (the margin covers the rounding of p + d t and of the
 //    norms) and can neither shadow nor hide a nearer hit: the walk stops at tlim.
 // A wave leaves the scan when every active lane is decided.  Returns `shadowed`.
-__device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lpos, ScanCnt& c) {
+template <bool LDS>
+__device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lpos, ScanCnt& c, lfloat4* lnodes) {
     const float l2 = len2(sub(lpos, o));
     float bt = __builtin_huge_valf();
     uint32_t bk = 0xFFFFFFFFu;
@@ -594,7 +639,7 @@ __device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lp
     if (S.use_bvh) {
         float on = sqrtf(len2(o));
         float tlim = (sqrtf(l2) * (1.f + 0.0009765625f) + 1e-5f * (on + 1.f)) / sqrtf(len2(d));
-        bvh_walk<true>(S, o, d, bt, bk, tlim, l2, c);
+        bvh_walk<true, LDS>(S, o, d, bt, bk, tlim, l2, c, lnodes);
         done = shadow_decided(o, d, bt, l2);
         if (__ballot(!done) == 0) goto finish;
         graze_pass(S, o, d, bt, bk, c);

@@ -62,6 +62,27 @@ __device__ __forceinline__ uint32_t morton15(const DevScene& S, V3 p) {
 __device__ __forceinline__ uint32_t octant(V3 d) {
     return (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u);
 }
+// task ordering key: 16 bits
+__device__ __forceinline__ uint32_t task_key(const WaveParams& P, V3 o, V3 d) {
+    if (P.key_mode == 0) return (octant(d) << 13) | (morton15(P.S, o) >> 2);  // 16 bits: 2 radix passes
+    // cube-map face of d (3 bits) x 2x2 cells of the face (2 bits) | 13-bit coarse origin
+    float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    uint32_t face;
+    float u, v, m;
+    if (ax >= ay && ax >= az) { face = d.x < 0.f; u = d.y; v = d.z; m = ax; }
+    else if (ay >= az) { face = 2u + (d.y < 0.f); u = d.x; v = d.z; m = ay; }
+    else { face = 4u + (d.z < 0.f); u = d.x; v = d.y; m = az; }
+    if (P.key_mode == 2) {  // face x 4x4 cells (< 96) | 9-bit coarse origin
+        float iu = u / m, iv = v / m;  // in [-1, 1]
+        uint32_t qu = (uint32_t)fminf(fmaxf((iu + 1.f) * 2.f, 0.f), 3.f);
+        uint32_t qv = (uint32_t)fminf(fmaxf((iv + 1.f) * 2.f, 0.f), 3.f);
+        uint32_t dir = (face << 4) | (qu << 2) | qv;
+        return (dir << 9) | (morton15(P.S, o) >> 6);
+    }
+    uint32_t cu = u > 0.f ? 1u : 0u, cv = v > 0.f ? 1u : 0u;
+    uint32_t dir = (face << 2) | (cu << 1) | cv;   // < 24
+    return (dir << 11) | (morton15(P.S, o) >> 4);
+}
 
 __device__ __forceinline__ uint64_t lanemask_lt() {
     uint32_t lane = lane_id();
@@ -217,7 +238,7 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
                 Task T = {rro.x, rro.y, rro.z, rrd.x, rrd.y, rrd.z, (n << 1) | 0u, 0u};
                 P.tasks[slot] = T;
                 if (P.task_keys) {
-                    P.task_keys[slot] = (octant(rrd) << RT_MORTON_BITS) | morton15(S, rro);
+                    P.task_keys[slot] = task_key(P, rro, rrd);
                     P.task_vals[slot] = slot;
                 }
             } else {
@@ -231,7 +252,7 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
                 Task T = {tro.x, tro.y, tro.z, trd.x, trd.y, trd.z, (n << 1) | 1u, 0u};
                 P.tasks[slot] = T;
                 if (P.task_keys) {
-                    P.task_keys[slot] = (octant(trd) << RT_MORTON_BITS) | morton15(S, tro);
+                    P.task_keys[slot] = task_key(P, tro, trd);
                     P.task_vals[slot] = slot;
                 }
             } else {
@@ -257,7 +278,8 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
                     k++;
                     if (slot < P.shadow_capacity) {
                         P.shadow[slot] = (n << 5) | (uint32_t)li;
-                        if (P.shadow_keys) P.shadow_keys[slot] = ((uint32_t)li << RT_MORTON_BITS) | mort;
+                        if (P.shadow_keys)
+                            P.shadow_keys[slot] = ((uint32_t)li << P.light_shift) | (mort >> (15u - P.light_shift));
                     } else
                         atomicOr(P.overflow, 2u);
                 }
@@ -277,8 +299,16 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
 
 // Every shadow ray of the frame: PointLight::get_energy's scan + distance test, result as
 // a bit in the node record.
+extern __shared__ float4 rt_dyn_lds[];
+
+template <bool LDS>
 __global__ __launch_bounds__(256) void shadow_kernel(WaveParams P) {
     const DevScene& S = P.S;
+    if (LDS) {  // stage the hierarchy's node records in LDS
+        for (int i = threadIdx.x; i < 4 * S.n_bvh_nodes; i += blockDim.x) rt_dyn_lds[i] = S.bvh_nodes[i];
+        __syncthreads();
+    }
+    lfloat4* lnodes = (lfloat4*)rt_dyn_lds;
     const uint32_t count = min(RT_SHADOW_COUNT(P), P.shadow_capacity);
     const uint32_t lane = lane_id();
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -297,7 +327,7 @@ __global__ __launch_bounds__(256) void shadow_kernel(WaveParams P) {
             V3 lpos = v3(L.px, L.py, L.pz);
             V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
             n_shadow++;
-            if (!shadow_scan(S, ps, ldir, lpos, cnt)) atomicOr(&P.nodes[n].litmask, 1u << li);
+            if (!shadow_scan<LDS>(S, ps, ldir, lpos, cnt, lnodes)) atomicOr(&P.nodes[n].litmask, 1u << li);
         }
     }
     cnt_flush(cnt, S.scan_ops);
@@ -390,7 +420,7 @@ hipError_t launch_wave_init(uint32_t* levels, uint32_t n_words, uint32_t total_i
 hipError_t wave_occupancy(int* trace_blocks, int* shadow_blocks, int* combine_blocks) {
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(trace_blocks, trace_level_kernel, 256, 0);
     if (e != hipSuccess) return e;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel, 256, 0);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<false>, 256, 0);
     if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(combine_blocks, combine_level_kernel, 256, 0);
 }
@@ -401,7 +431,13 @@ hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hi
 }
 
 hipError_t launch_wave_shadow(const WaveParams& p, int blocks, hipStream_t stream) {
-    hipLaunchKernelGGL(shadow_kernel, dim3(blocks), dim3(256), 0, stream, p);
+    size_t lds = (size_t)p.S.n_bvh_nodes * 64;
+    const char* e = getenv("RT_LDS_NODES");
+    bool use = p.S.use_bvh && lds > 0 && lds <= 36 * 1024 && !(e && e[0] == '0');
+    if (use)
+        hipLaunchKernelGGL(shadow_kernel<true>, dim3(blocks), dim3(256), lds, stream, p);
+    else
+        hipLaunchKernelGGL(shadow_kernel<false>, dim3(blocks), dim3(256), 0, stream, p);
     return hipGetLastError();
 }
 

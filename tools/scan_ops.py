@@ -33,4 +33,5 @@ if __name__ == "__main__":
     a = [int(x) for x in sys.argv[1:]]
     config, w, h, depth = (a + [3, 1920, 1080, 8][len(a):])[:4]
     run(config, w, h, depth, True)
-    run(config, w, h, depth, False)
+    if not os.environ.get("SKIP_LINEAR"):
+        run(config, w, h, depth, False)
