@@ -597,6 +597,8 @@ struct Workspace {
     // level-synchronous pipeline
     Task* tasks = nullptr;
     NodeRec* nodes = nullptr;
+    float4* node_ps = nullptr;       // [capacity] shadow-ray origins
+    uint32_t* node_lit = nullptr;    // [capacity] unshadowed-light bits
     uint32_t capacity = 0;
     uint32_t* shadow = nullptr;      // shadow queue
     uint32_t shadow_capacity = 0;
@@ -715,6 +717,27 @@ rt_status ensure_ws(rt_scene* s, size_t out_floats, size_t out8_bytes) {
         HIP_TRY(hipMalloc(&w.out8, out8_bytes));
         w.out8_bytes = out8_bytes;
     }
+    return RT_OK;
+}
+
+// (Re)allocates every per-node array with `cap` slots: tasks, node records, shadow-ray
+// origins, unshadowed-light bits.  The per-node sort buffers follow lazily
+// (sort_capacity < capacity), the shadow queue from capacity * point lights.
+rt_status grow_node_pool(Workspace& w, uint32_t cap) {
+    (void)hipFree(w.tasks);
+    (void)hipFree(w.nodes);
+    (void)hipFree(w.node_ps);
+    (void)hipFree(w.node_lit);
+    w.tasks = nullptr;
+    w.nodes = nullptr;
+    w.node_ps = nullptr;
+    w.node_lit = nullptr;
+    w.capacity = 0;
+    HIP_TRY(hipMalloc(&w.tasks, (size_t)cap * sizeof(Task)));
+    HIP_TRY(hipMalloc(&w.nodes, (size_t)cap * sizeof(NodeRec)));
+    HIP_TRY(hipMalloc(&w.node_ps, (size_t)cap * sizeof(float4)));
+    HIP_TRY(hipMalloc(&w.node_lit, (size_t)cap * sizeof(uint32_t)));
+    w.capacity = cap;
     return RT_OK;
 }
 
@@ -967,6 +990,11 @@ rt_status rt_scene_destroy(rt_scene* s) {
     if (s->ws.nodes) (void)hipFree(s->ws.nodes);
     if (s->ws.levels) (void)hipFree(s->ws.levels);
     if (s->ws.overflow) (void)hipFree(s->ws.overflow);
+    for (void* b : {(void*)s->ws.node_ps, (void*)s->ws.node_lit, (void*)s->ws.task_keys, (void*)s->ws.task_vals,
+                    (void*)s->ws.perm, (void*)s->ws.keys_alt, (void*)s->ws.shadow_keys,
+                    (void*)s->ws.shadow_keys_alt, (void*)s->ws.shadow_sorted, s->ws.sort_tmp})
+        if (b) (void)hipFree(b);
+    if (s->ws.h_count) (void)hipHostFree(s->ws.h_count);
     if (s->dmem) (void)hipFree(s->dmem);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -1083,14 +1111,8 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
     if (want > 0x7FFFFFFFu) want = 0x7FFFFFFFu;
     Workspace& w = s->ws;
     if (w.capacity < want) {  // grows only (rt_render may have grown it after an overflow)
-        if (w.tasks) (void)hipFree(w.tasks);
-        if (w.nodes) (void)hipFree(w.nodes);
-        w.tasks = nullptr;
-        w.nodes = nullptr;
-        w.capacity = 0;
-        HIP_TRY(hipMalloc(&w.tasks, want * sizeof(Task)));
-        HIP_TRY(hipMalloc(&w.nodes, want * sizeof(NodeRec)));
-        w.capacity = (uint32_t)want;
+        rt_status st = grow_node_pool(w, (uint32_t)want);
+        if (st != RT_OK) return st;
     }
     if (!w.levels) {
         HIP_TRY(hipMalloc(&w.levels, 2 * (RT_MAX_DEPTH + 2) * sizeof(uint32_t)));
@@ -1161,6 +1183,8 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
     p.shadow = w.shadow;
     p.tasks = w.tasks;
     p.nodes = w.nodes;
+    p.node_ps = w.node_ps;
+    p.node_lit = w.node_lit;
     p.levels = w.levels;
     p.overflow = w.overflow;
     p.out = d_rgb;
@@ -1269,15 +1293,8 @@ rt_status rt_render(const rt_scene* scene, const rt_camera* cam, uint32_t depth,
         if (!ovf) break;
         // node pool too small for this scene's ray trees: grow it and render again
         if (attempt >= 6 || s->ws.capacity >= 0x40000000u) return RT_ERR_OUT_OF_MEMORY;
-        uint32_t cap = s->ws.capacity * 2u;
-        (void)hipFree(s->ws.tasks);
-        (void)hipFree(s->ws.nodes);
-        s->ws.tasks = nullptr;
-        s->ws.nodes = nullptr;
-        s->ws.capacity = 0;
-        HIP_TRY(hipMalloc(&s->ws.tasks, (size_t)cap * sizeof(Task)));
-        HIP_TRY(hipMalloc(&s->ws.nodes, (size_t)cap * sizeof(NodeRec)));
-        s->ws.capacity = cap;
+        rt_status st = grow_node_pool(s->ws, s->ws.capacity * 2u);
+        if (st != RT_OK) return st;
     }
     if (rgb8) HIP_TRY(launch_quantize(s->ws.out, n, s->ws.out8, stream));
     HIP_TRY(hipMemcpyAsync(rgb, s->ws.out, n * sizeof(float), hipMemcpyDeviceToHost, stream));

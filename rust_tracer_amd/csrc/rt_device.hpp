@@ -126,7 +126,10 @@ struct Task {
 
 // One traced tree node: the shading inputs of render.rs:57-68 (lights are summed later,
 // once the shadow scans have run), the child weights of render.rs:70-98, the colours its
-// children report, and where to report its own colour.  144 B.
+// children report, and where to report its own colour.  144 B.  The shadow pass reads a
+// node's shadow-ray origin from the compact `node_ps` array and reports into `node_lit`
+// (bit l: point light l is NOT shadowed), so its randomly ordered accesses touch 16 + 4
+// bytes per entry instead of the record's cache lines.
 struct NodeRec {
     float ambx, amby, ambz;    // material ambient (tex) * scene ambient (render.rs:57)
     float psx, psy, psz;       // shadow-ray origin: point + 0.0002 * normal (render.rs:147)
@@ -138,9 +141,8 @@ struct NodeRec {
     float erx, ery, erz;       // colour of the reflected child (0 until it reports)
     float etx, ety, etz;       // colour of the refracted child
     uint32_t flags;
-    uint32_t litmask;          // bit l: point light l is NOT shadowed (set by the shadow pass)
     uint32_t parent;           // as Task::parent; level 0: unused
-    uint32_t pad[2];
+    uint32_t pad[3];
 };
 
 struct WaveParams {
@@ -154,6 +156,8 @@ struct WaveParams {
     uint32_t shadow_capacity;          // shadow-queue slots
     Task* tasks;                       // [capacity]
     NodeRec* nodes;                    // [capacity]
+    float4* node_ps;                   // [capacity]: shadow-ray origin (w unused)
+    uint32_t* node_lit;                // [capacity]: unshadowed-light bits
     uint32_t* shadow;                  // [shadow_capacity]: (node << 5) | light
     uint32_t* levels;                  // [2 * (RT_MAX_DEPTH + 2)]: offset, count per level;
                                        // levels[2 * (RT_MAX_DEPTH + 1)] = shadow-queue count

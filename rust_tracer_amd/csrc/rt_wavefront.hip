@@ -192,9 +192,10 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
                 rec.erx = 0.f; rec.ery = 0.f; rec.erz = 0.f;
                 rec.etx = 0.f; rec.ety = 0.f; rec.etz = 0.f;
                 rec.flags = NODE_HIT;
-                rec.litmask = 0u;
+                P.node_ps[n] = make_float4(ps.x, ps.y, ps.z, 0.f);
+                P.node_lit[n] = 0u;
                 rec.parent = parent;
-                rec.pad[0] = rec.pad[1] = 0u;
+                rec.pad[0] = rec.pad[1] = rec.pad[2] = 0u;
                 bool child_ok = level + 1 < P.depth;
                 if (M.reflectivity > RT_EPS) {  // render.rs:70-84, reflect_ray :105-110
                     rec.flags |= F_REFL;
@@ -321,13 +322,13 @@ __global__ __launch_bounds__(256) void shadow_kernel(WaveParams P) {
         if (t < count) {
             uint32_t e = P.shadow_in[t];
             uint32_t n = e >> 5, li = e & 31u;
-            const NodeRec& R = P.nodes[n];
-            V3 ps = v3(R.psx, R.psy, R.psz);
+            const float4 q = P.node_ps[n];
+            V3 ps = v3(q.x, q.y, q.z);
             const LightRec& L = S.lights[li];
             V3 lpos = v3(L.px, L.py, L.pz);
             V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
             n_shadow++;
-            if (!shadow_scan<LDS>(S, ps, ldir, lpos, cnt, lnodes)) atomicOr(&P.nodes[n].litmask, 1u << li);
+            if (!shadow_scan<LDS>(S, ps, ldir, lpos, cnt, lnodes)) atomicOr(&P.node_lit[n], 1u << li);
         }
     }
     cnt_flush(cnt, S.scan_ops);
@@ -363,13 +364,14 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
             V3 ps = v3(R.psx, R.psy, R.psz);
             V3 kd = v3(R.kdx, R.kdy, R.kdz), ks = v3(R.ksx, R.ksy, R.ksz);
             V3 lsum = v3(0.f, 0.f, 0.f);  // Sum starts at BLACK (color.rs:164-167)
+            const uint32_t litmask = P.node_lit[n];
             for (int li = 0; li < S.n_lights; ++li) {
                 const LightRec& L = S.lights[li];
                 V3 ldir = v3(0.f, 0.f, 0.f);
                 V3 E = v3(L.r, L.g, L.b);
                 if (L.kind == RT_LIGHT_POINT) {
                     ldir = norm(sub(v3(L.px, L.py, L.pz), ps));
-                    if (!((R.litmask >> li) & 1u)) E = v3(0.f, 0.f, 0.f);
+                    if (!((litmask >> li) & 1u)) E = v3(0.f, 0.f, 0.f);
                 }
                 float f = fresnel_reflection(ldir, h.n, R.n1, R.n2);
                 V3 g = reflected_energy(E, ldir, h, kd, ks, R.power);

@@ -16,7 +16,20 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-RENDER = ("trace_level_kernel", "combine_level_kernel", "wave_init_kernel", "render_kernel")
+RENDER = ("trace_level_kernel", "shadow_kernel", "combine_level_kernel", "wave_init_kernel", "render_kernel",
+          "rocprim", "fillBufferAligned")
+
+
+def family(kernel_name):
+    """short family name of a render-pipeline dispatch (None if not one)"""
+    for k in RENDER:
+        if k in kernel_name:
+            if k == "rocprim":
+                return "queue sort (rocPRIM onesweep)"
+            if k == "fillBufferAligned":
+                return "sort lookback reset (fill)"
+            return k
+    return None
 
 
 def main(tag):
@@ -33,6 +46,7 @@ def main(tag):
         w.writeheader()
         for r in keep:
             d = {k: r[k] for k in fields}
+            d["Kernel_Name"] = family(r["Kernel_Name"]) if "rocprim" in r["Kernel_Name"] else r["Kernel_Name"]
             d["Duration_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             w.writerow(d)
     bench = json.load(open(os.path.join(src, "bench.json")))
@@ -53,8 +67,7 @@ def main(tag):
     # kernel-trace: per-frame time of each render kernel family (the trace run did 1 + 3 frames)
     per = defaultdict(list)
     for r in keep:
-        name = next(k for k in RENDER if k in r["Kernel_Name"])
-        per[name].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        per[family(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     frames = 4
     fam_ms = {k: sum(v) / frames / 1e6 for k, v in per.items()}
     fetch_b = pmc.get("FETCH_SIZE", 0.0) * 1024 / steps_prof
