@@ -893,7 +893,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
         size_t bytes;
         size_t off;
     };
-    static const unsigned long long zero_ops[RT_OPS_N] = {0};
+    static const unsigned long long zero_ops[RT_OPS_SLOTS * RT_OPS_STRIDE] = {0};
     Sec secs[14] = {{dsph.data(), dsph.size() * 4, 0},       {gsph.data(), gsph.size() * 4, 0},
                     {tri.data(), tri.size() * 4, 0},         {cube.data(), cube.size() * 4, 0},
                     {plane.data(), plane.size() * 4, 0},     {cubetri.data(), cubetri.size() * 4, 0},
@@ -1011,12 +1011,15 @@ rt_status rt_scene_scan_ops(rt_scene* s, uint64_t* out, uint32_t n, int32_t rese
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipDeviceSynchronize());
     if (out && n) {
-        unsigned long long h[RT_OPS_N];
-        HIP_TRY(hipMemcpy(h, s->S.scan_ops, sizeof(h), hipMemcpyDeviceToHost));
-        for (uint32_t k = 0; k < n; k++) out[k] = h[k];
+        std::vector<unsigned long long> h(RT_OPS_SLOTS * RT_OPS_STRIDE);
+        HIP_TRY(hipMemcpy(h.data(), s->S.scan_ops, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        for (uint32_t k = 0; k < n; k++) {
+            out[k] = 0;
+            for (int b = 0; b < RT_OPS_SLOTS; b++) out[k] += h[b * RT_OPS_STRIDE + k];
+        }
     }
     if (reset) {
-        HIP_TRY(hipMemset(s->S.scan_ops, 0, RT_OPS_N * sizeof(unsigned long long)));
+        HIP_TRY(hipMemset(s->S.scan_ops, 0, RT_OPS_SLOTS * RT_OPS_STRIDE * sizeof(unsigned long long)));
         HIP_TRY(hipDeviceSynchronize());
     }
     return RT_OK;
@@ -1131,6 +1134,10 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
     const bool sort_on = s->S.use_bvh && sort_enabled();
     const bool sort_tasks = sort_tasks_enabled();
     p.key_mode = task_key_mode();
+    {  // RT_COUNT=trace|shadow: count only that kernel's tests (tools/scan_ops.py)
+        const char* e = std::getenv("RT_COUNT");
+        p.count_mask = !e ? 3u : (std::strcmp(e, "trace") == 0 ? 1u : (std::strcmp(e, "shadow") == 0 ? 2u : 3u));
+    }
     // 16-bit keys (two 8-bit radix passes): task = octant | 13 Morton bits; shadow =
     // light index | the Morton bits that fit (all 15 above 16 lights' worth of bits)
     uint32_t lbits = 0;

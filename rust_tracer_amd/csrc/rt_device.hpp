@@ -98,7 +98,11 @@ enum : int {
     RT_OPS_GRAZE = 6,   // grazing cone tests (blocks of 8 triangles)
     RT_OPS_PLANE = 7,   // planes
     RT_OPS_GRAZE_N = 8, // grazing normal tests (blocks of 8 whose cone some lane meets)
-    RT_OPS_N = 9
+    RT_OPS_N = 9,
+    // scan_ops is RT_OPS_SLOTS x RT_OPS_STRIDE u64: block b adds to slot b % RT_OPS_SLOTS
+    // (same-address global atomics from every block would serialise in L2)
+    RT_OPS_SLOTS = 64,
+    RT_OPS_STRIDE = 16
 };
 
 // Everything one launch needs.
@@ -173,6 +177,7 @@ struct WaveParams {
     const uint32_t* shadow_in;         // the shadow entries the shadow kernel reads
     uint32_t key_mode;                 // task key variant (A/B)
     uint32_t light_shift;              // shadow key = (light << light_shift) | (Morton >> (15 - light_shift))
+    uint32_t count_mask;               // bit 0: trace kernels add to scan_ops, bit 1: shadow kernel
 };
 
 // 15-bit Morton code of a point in the 32^3 grid over [c - r, c + r]^3 (clamped)

@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
         atomicAdd(P.ray_counters + 2, n_pix);
     }
     if (lane == 0 && P.iter_counter) atomicAdd(P.iter_counter, n_iter);
-    cnt_flush(cnt, S.scan_ops);
+    cnt_flush(cnt, ops_slot(S));
 }
 
 // Scatter gathered per-rank band buffers into the row-major frame (one block row per frame row).

@@ -274,6 +274,7 @@ __device__ __forceinline__ uint32_t active_lanes() { return (uint32_t)__builtin_
 __device__ __forceinline__ void cnt_add(unsigned long long* p, uint32_t v) {
     if (v) atomicAdd(p, (unsigned long long)v);
 }
+// Adds the wave's counts to `dst` (RT_OPS_N counters) from one lane.
 __device__ __forceinline__ void cnt_flush(const ScanCnt& c, unsigned long long* dst) {
     uint64_t m = __ballot(1);
     if (m == 0) return;
@@ -288,6 +289,9 @@ __device__ __forceinline__ void cnt_flush(const ScanCnt& c, unsigned long long* 
         cnt_add(dst + RT_OPS_PLANE, c.plane);
         cnt_add(dst + RT_OPS_GRAZE_N, c.graze_n);
     }
+}
+__device__ __forceinline__ unsigned long long* ops_slot(const DevScene& S) {
+    return S.scan_ops + (blockIdx.x % RT_OPS_SLOTS) * RT_OPS_STRIDE;
 }
 
 // ------------------------------------------------------------------ linear runs

@@ -84,6 +84,45 @@ __device__ __forceinline__ uint32_t task_key(const WaveParams& P, V3 o, V3 d) {
     return (dir << 11) | (morton15(P.S, o) >> 4);
 }
 
+// Per-block accumulation of the kernels' counters: each wave adds into LDS, then the
+// block adds once per counter to global memory (RT_OPS_N scan counters in the block's
+// scan_ops slot, then node / shadow / pixel ray counts).  Every wave of a frame adding
+// to the same few addresses serialised in L2 (~2 ms per 1080p frame).
+constexpr int RT_BC_N = RT_OPS_N + 3;
+__shared__ unsigned long long rt_block_counts[RT_BC_N];
+
+__device__ __forceinline__ void bc_init() {
+    if (threadIdx.x < RT_BC_N) rt_block_counts[threadIdx.x] = 0ull;
+    __syncthreads();
+}
+__device__ __forceinline__ void bc_add(int i, uint32_t v) {  // one lane per wave
+    if (v) atomicAdd(&rt_block_counts[i], (unsigned long long)v);
+}
+__device__ __forceinline__ void bc_flush(unsigned long long* ops, unsigned long long* rays) {
+    __syncthreads();
+    if (threadIdx.x < RT_BC_N) {
+        unsigned long long v = rt_block_counts[threadIdx.x];
+        if (v) {
+            if (threadIdx.x < RT_OPS_N) {
+                if (ops) atomicAdd(ops + threadIdx.x, v);
+            } else if (rays) {
+                atomicAdd(rays + (threadIdx.x - RT_OPS_N), v);
+            }
+        }
+    }
+}
+__device__ __forceinline__ void bc_scan(const ScanCnt& c) {
+    bc_add(RT_OPS_NODE, c.node);
+    bc_add(RT_OPS_DSPH, c.dsph);
+    bc_add(RT_OPS_GSPH, c.gsph);
+    bc_add(RT_OPS_TRI, c.tri);
+    bc_add(RT_OPS_CUBE_BOX, c.cube_box);
+    bc_add(RT_OPS_CUBE, c.cube);
+    bc_add(RT_OPS_GRAZE, c.graze);
+    bc_add(RT_OPS_PLANE, c.plane);
+    bc_add(RT_OPS_GRAZE_N, c.graze_n);
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
     uint32_t lane = lane_id();
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -119,6 +158,7 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
     uint32_t n_node = 0, n_pix = 0;
     ScanCnt cnt;
     cnt_init(cnt);
+    bc_init();
     // point lights: one shadow ray each per hit (mod.rs:189-206); ambient lights: none
     uint32_t n_point = 0;
     for (int li = 0; li < S.n_lights; ++li) n_point += S.lights[li].kind == RT_LIGHT_POINT ? 1u : 0u;
@@ -287,15 +327,16 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
             }
         }
     }
-    cnt_flush(cnt, S.scan_ops);
     for (int o = 32; o > 0; o >>= 1) {
         n_node += __shfl_xor(n_node, o);
         n_pix += __shfl_xor(n_pix, o);
     }
-    if (lane == 0 && P.ray_counters) {
-        if (n_node) atomicAdd(P.ray_counters + 0, (unsigned long long)n_node);
-        if (n_pix) atomicAdd(P.ray_counters + 2, (unsigned long long)n_pix);
+    if (lane == 0) {
+        if (P.count_mask & 1u) bc_scan(cnt);
+        bc_add(RT_OPS_N + 0, n_node);
+        bc_add(RT_OPS_N + 2, n_pix);
     }
+    bc_flush(ops_slot(S), P.ray_counters);
 }
 
 // Every shadow ray of the frame: PointLight::get_energy's scan + distance test, result as
@@ -316,6 +357,7 @@ __global__ __launch_bounds__(256) void shadow_kernel(WaveParams P) {
     uint32_t n_shadow = 0;
     ScanCnt cnt;
     cnt_init(cnt);
+    bc_init();
     const uint32_t wave_base = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u;
     for (uint32_t base = wave_base; base < count; base += stride) {
         const uint32_t t = base + lane;
@@ -331,9 +373,12 @@ __global__ __launch_bounds__(256) void shadow_kernel(WaveParams P) {
             if (!shadow_scan<LDS>(S, ps, ldir, lpos, cnt, lnodes)) atomicOr(&P.node_lit[n], 1u << li);
         }
     }
-    cnt_flush(cnt, S.scan_ops);
     for (int o = 32; o > 0; o >>= 1) n_shadow += __shfl_xor(n_shadow, o);
-    if (lane == 0 && P.ray_counters && n_shadow) atomicAdd(P.ray_counters + 1, (unsigned long long)n_shadow);
+    if (lane == 0) {
+        if (P.count_mask & 2u) bc_scan(cnt);
+        bc_add(RT_OPS_N + 1, n_shadow);
+    }
+    bc_flush(ops_slot(S), P.ray_counters);
 }
 
 // render.rs:57-68 + :100 for every node of `level`; children (level + 1) already reported.
