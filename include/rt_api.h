@@ -202,6 +202,11 @@ uint64_t rt_scene_device_bytes(const rt_scene* scene);
 #define RT_SCAN_OPS_N 9
 rt_status rt_scene_scan_ops(rt_scene* scene, uint64_t* out, uint32_t n, int32_t reset);
 
+/* Counting is instrumentation: renders after rt_scene_set_scan_counting(scene, 1) run
+ * the counting variants of the level-synchronous kernels (the per-pixel megakernel
+ * always counts); the default (0) runs uncounted kernels.  Frames are identical. */
+rt_status rt_scene_set_scan_counting(rt_scene* scene, int32_t enable);
+
 /* 1 if the scene's scans walk the culling hierarchy (the default; RT_BVH=0 in the
  * environment at rt_scene_create turns it off), 0 if they test every shape. */
 int32_t rt_scene_uses_bvh(const rt_scene* scene);

@@ -252,6 +252,10 @@ class DeviceScene:
     SCAN_OPS = ("node_pairs", "dsph_pairs", "gsph", "tri_pairs", "cube_boxes", "cubes", "graze_cones",
                 "planes", "graze_normals")
 
+    def set_scan_counting(self, enable=True):
+        """Run the instrumented (counting) kernels from now on (rt_scene_set_scan_counting)."""
+        check(self._L.rt_scene_set_scan_counting(self.h, 1 if enable else 0), "rt_scene_set_scan_counting")
+
     def scan_ops(self, reset=False):
         """Lane-weighted test counts since the last reset (rt_scene_scan_ops)."""
         out = (C.c_uint64 * len(self.SCAN_OPS))()

@@ -130,6 +130,7 @@ def lib():
     L.rt_scene_device_bytes.argtypes = [vp]
     L.rt_scene_device_bytes.restype = C.c_uint64
     L.rt_scene_scan_ops.argtypes = [vp, P(C.c_uint64), C.c_uint32, C.c_int32]
+    L.rt_scene_set_scan_counting.argtypes = [vp, C.c_int32]
     L.rt_scene_uses_bvh.argtypes = [vp]
     L.rt_scene_uses_bvh.restype = C.c_int32
     L.rt_status_str.argtypes = [C.c_int32]

@@ -662,6 +662,7 @@ struct rt_scene {
     int num_cus = 256;
     int occ[3] = {0, 0, 0};  // blocks per CU for the MAXF 7 / 15 / 63 variants
     int occ_trace = 0, occ_shadow = 0, occ_combine = 0;
+    bool count_ops = false;  // rt_scene_set_scan_counting
     Workspace ws;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -1027,6 +1028,12 @@ rt_status rt_scene_scan_ops(rt_scene* s, uint64_t* out, uint32_t n, int32_t rese
 
 int32_t rt_scene_uses_bvh(const rt_scene* s) { return (s && s->S.use_bvh) ? 1 : 0; }
 
+rt_status rt_scene_set_scan_counting(rt_scene* s, int32_t enable) {
+    if (!s) return RT_ERR_INVALID_ARG;
+    s->count_ops = enable != 0;
+    return RT_OK;
+}
+
 static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
                                    uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
                                    hipStream_t stream);
@@ -1134,9 +1141,11 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
     const bool sort_on = s->S.use_bvh && sort_enabled();
     const bool sort_tasks = sort_tasks_enabled();
     p.key_mode = task_key_mode();
-    {  // RT_COUNT=trace|shadow: count only that kernel's tests (tools/scan_ops.py)
+    if (s->count_ops) {  // instrumented kernels; RT_COUNT=trace|shadow: only that kernel's tests
         const char* e = std::getenv("RT_COUNT");
         p.count_mask = !e ? 3u : (std::strcmp(e, "trace") == 0 ? 1u : (std::strcmp(e, "shadow") == 0 ? 2u : 3u));
+    } else {
+        p.count_mask = 0u;
     }
     // 16-bit keys (two 8-bit radix passes): task = octant | 13 Morton bits; shadow =
     // light index | the Morton bits that fit (all 15 above 16 lights' worth of bits)

@@ -266,6 +266,13 @@ __device__ __forceinline__ void plane_one(cfloat4* r, V3 o, V3 d, float& bt, uin
 struct ScanCnt {
     uint32_t node, dsph, gsph, tri, cube_box, cube, graze, plane, graze_n;
 };
+// The uncounted variant: the same expressions, every `+=` a no-op (compiled away).
+struct NoCntField {
+    __device__ NoCntField& operator+=(uint32_t) { return *this; }
+};
+struct NoCnt {
+    NoCntField node, dsph, gsph, tri, cube_box, cube, graze, plane, graze_n;
+};
 __device__ __forceinline__ void cnt_init(ScanCnt& c) {
     c.node = c.dsph = c.gsph = c.tri = c.cube_box = c.cube = c.graze = c.plane = c.graze_n = 0;
 }
@@ -297,8 +304,9 @@ __device__ __forceinline__ unsigned long long* ops_slot(const DevScene& S) {
 // ------------------------------------------------------------------ linear runs
 // Group loops prefetch record i+1 before testing record i; every section is padded by
 // one group so the look-ahead load stays inside the allocation.
+template <class C>
 __device__ __forceinline__ void run_dsph(const DevScene& S, int b, int e, V3 o, V3 d, float& bt, uint32_t& bk,
-                                         ScanCnt& c) {
+                                         C& c) {
     if (b >= e) return;
     cfloat4* p = cptr(S.dsph) + 4 * b;
     SphPair cur = ld_sph(p);
@@ -310,8 +318,9 @@ __device__ __forceinline__ void run_dsph(const DevScene& S, int b, int e, V3 o, 
         cur = nxt;
     }
 }
+template <class C>
 __device__ __forceinline__ void run_gsph(const DevScene& S, int b, int e, V3 o, V3 d, float& bt, uint32_t& bk,
-                                         ScanCnt& c) {
+                                         C& c) {
     if (b >= e) return;
     cfloat4* p = cptr(S.gsph) + 4 * b;
     Rec16 cur = ld_rec(p);
@@ -323,8 +332,9 @@ __device__ __forceinline__ void run_gsph(const DevScene& S, int b, int e, V3 o, 
         cur = nxt;
     }
 }
+template <class C>
 __device__ __forceinline__ void run_tri(const DevScene& S, int b, int e, V3 o, V3 d, float& bt, uint32_t& bk,
-                                        ScanCnt& c) {
+                                        C& c) {
     if (b >= e) return;
     cfloat4* p = cptr(S.tri) + 6 * b;
     TriPair cur = ld_tri(p);
@@ -336,8 +346,9 @@ __device__ __forceinline__ void run_tri(const DevScene& S, int b, int e, V3 o, V
         cur = nxt;
     }
 }
+template <class C>
 __device__ __forceinline__ void run_cube(const DevScene& S, int b, int e, V3 o, V3 d, float& bt, uint32_t& bk,
-                                         ScanCnt& c) {
+                                         C& c) {
     if (b >= e) return;
     cfloat4* p = cptr(S.cube) + 4 * b;
     Rec16 cur = ld_rec(p);
@@ -427,8 +438,9 @@ __device__ __forceinline__ void node_test(float4 q0, float4 q1, float4 q2, BvhRa
 // A cube of a leaf: its object-space box [-1/2 - hc, 1/2 + hc]^3 first (hc bounds how
 // far a reported object-space hit point can lie outside the unit cube, measured by
 // tools/cull_bounds_check.py, x32), then the 12 triangles if any lane can hit.
+template <class C>
 __device__ __forceinline__ void cube_culled(const Rec16& Rc, V3 o, V3 d, float on, float tmax, float& bt,
-                                            uint32_t& bk, ScanCnt& c) {
+                                            uint32_t& bk, C& c) {
     V3 to = pt_mul(Rc.r0, Rc.r1, Rc.r2, o);
     V3 td = vec3_mul(Rc.r0, Rc.r1, Rc.r2, d);
     float m = fmaxf(fabsf(to.x), fmaxf(fabsf(to.y), fabsf(to.z)));
@@ -454,8 +466,9 @@ typedef const uint4 cuint4;
 #endif
 
 // One leaf: its runs of pairs / general spheres / triangle pairs / cubes.
+template <class C>
 __device__ __forceinline__ void bvh_leaf(const DevScene& S, uint32_t li, V3 o, V3 d, float on, float tmax,
-                                         float& bt, uint32_t& bk, ScanCnt& c) {
+                                         float& bt, uint32_t& bk, C& c) {
     cuint4* lp = (cuint4*)S.bvh_leaves + 2 * li;
     uint4 a = lp[0], b = lp[1];
     run_dsph(S, (int)a.x, (int)a.y, o, d, bt, bk, c);
@@ -486,9 +499,9 @@ typedef const float4 lfloat4;
 #endif
 
 // LDS: node records staged in LDS by the kernel (lnodes != null), else read via SMEM
-template <bool SHADOW, bool LDS>
+template <bool SHADOW, bool LDS, class C>
 __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, float tlim,
-                                         float l2, ScanCnt& c, lfloat4* lnodes) {
+                                         float l2, C& c, lfloat4* lnodes) {
     const BvhRay R = bvh_ray(S, o, d);
     uint32_t* stk = rt_bvh_stack + ((threadIdx.x >> 6) << 5);
     uint32_t sp = 0;
@@ -551,7 +564,8 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
 // sin(phi) < 1.01 sin(phi_min) is tested exactly for the wave (the hierarchy's bounds
 // do not cover it).  Triangles come in blocks of 8 with similar normals; a block whose
 // normal cone no lane's direction can graze is skipped after one dot product.
-__device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, ScanCnt& c) {
+template <class C>
+__device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c) {
     if (S.n_graze_blk == 0) return;
     const float dd = len2(d);
     const float lim = S.graze_s2 * dd;
@@ -591,7 +605,8 @@ __device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float&
     }
 }
 
-__device__ __forceinline__ void planes(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, ScanCnt& c) {
+template <class C>
+__device__ __forceinline__ void planes(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c) {
     for (int i = 0; i < S.n_plane; ++i) {
         RT_OPS(c, plane);
         plane_one(cptr(S.plane) + 5 * i, o, d, bt, bk);
@@ -599,7 +614,8 @@ __device__ __forceinline__ void planes(const DevScene& S, V3 o, V3 d, float& bt,
 }
 
 // the primitives outside the hierarchy (all of them when it is off)
-__device__ __forceinline__ void linear_rest(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, ScanCnt& c) {
+template <class C>
+__device__ __forceinline__ void linear_rest(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c) {
     run_dsph(S, S.n_dsph_bvh, S.n_dsph, o, d, bt, bk, c);
     run_gsph(S, S.n_gsph_bvh, S.n_gsph, o, d, bt, bk, c);
     run_tri(S, S.n_tri_bvh, S.n_tri, o, d, bt, bk, c);
@@ -607,7 +623,8 @@ __device__ __forceinline__ void linear_rest(const DevScene& S, V3 o, V3 d, float
 }
 
 // Scene::intersect (scene/mod.rs:98-116): the nearest (t, key) over every shape.
-__device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, ScanCnt& c) {
+template <class C>
+__device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c) {
     bt = __builtin_huge_valf();
     bk = 0xFFFFFFFFu;
     RT_STAT(0);
@@ -632,8 +649,8 @@ __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, u
 //    distance^2 >= |pos - p|^2 (the margin covers the rounding of p + d t and of the
 //    norms) and can neither shadow nor hide a nearer hit: the walk stops at tlim.
 // A wave leaves the scan when every active lane is decided.  Returns `shadowed`.
-template <bool LDS>
-__device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lpos, ScanCnt& c, lfloat4* lnodes) {
+template <bool LDS, class C>
+__device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lpos, C& c, lfloat4* lnodes) {
     const float l2 = len2(sub(lpos, o));
     float bt = __builtin_huge_valf();
     uint32_t bk = 0xFFFFFFFFu;

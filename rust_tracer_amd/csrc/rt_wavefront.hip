@@ -21,6 +21,8 @@
 // critical-path bound.  Here every queue entry costs one scan, lanes stay full, and the
 // post-order combine keeps the reference's exact operation order (pixel values reach
 // |4000| in config 3, so a reassociated "throughput" formulation would break 1e-4).
+#include <type_traits>
+
 #include "rt_common.hpp"
 
 namespace rtdev {
@@ -148,6 +150,7 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, uint32_t n, u
     return base + mine;
 }
 
+template <bool COUNT>
 __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t level) {
     const DevScene& S = P.S;
     const uint32_t off = P.levels[2 * level];
@@ -156,8 +159,8 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
     if (blockIdx.x == 0 && threadIdx.x == 0) P.levels[2 * (level + 1)] = next_off;
     const uint32_t lane = lane_id();
     uint32_t n_node = 0, n_pix = 0;
-    ScanCnt cnt;
-    cnt_init(cnt);
+    typename std::conditional<COUNT, ScanCnt, NoCnt>::type cnt;
+    if constexpr (COUNT) cnt_init(cnt);
     bc_init();
     // point lights: one shadow ray each per hit (mod.rs:189-206); ambient lights: none
     uint32_t n_point = 0;
@@ -332,7 +335,7 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
         n_pix += __shfl_xor(n_pix, o);
     }
     if (lane == 0) {
-        if (P.count_mask & 1u) bc_scan(cnt);
+        if constexpr (COUNT) bc_scan(cnt);
         bc_add(RT_OPS_N + 0, n_node);
         bc_add(RT_OPS_N + 2, n_pix);
     }
@@ -343,8 +346,11 @@ __global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t
 // a bit in the node record.
 extern __shared__ float4 rt_dyn_lds[];
 
-template <bool LDS>
-__global__ __launch_bounds__(256) void shadow_kernel(WaveParams P) {
+#ifndef RT_SHADOW_WAVES
+#define RT_SHADOW_WAVES 5  // 96 VGPRs (measured: 4 -> 8.36 ms, 5 -> 8.04, 6 -> 11.2 with spills)
+#endif
+template <bool LDS, bool COUNT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_WAVES, 8))) void shadow_kernel(WaveParams P) {
     const DevScene& S = P.S;
     if (LDS) {  // stage the hierarchy's node records in LDS
         for (int i = threadIdx.x; i < 4 * S.n_bvh_nodes; i += blockDim.x) rt_dyn_lds[i] = S.bvh_nodes[i];
@@ -355,8 +361,8 @@ __global__ __launch_bounds__(256) void shadow_kernel(WaveParams P) {
     const uint32_t lane = lane_id();
     const uint32_t stride = gridDim.x * blockDim.x;
     uint32_t n_shadow = 0;
-    ScanCnt cnt;
-    cnt_init(cnt);
+    typename std::conditional<COUNT, ScanCnt, NoCnt>::type cnt;
+    if constexpr (COUNT) cnt_init(cnt);
     bc_init();
     const uint32_t wave_base = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u;
     for (uint32_t base = wave_base; base < count; base += stride) {
@@ -375,7 +381,7 @@ __global__ __launch_bounds__(256) void shadow_kernel(WaveParams P) {
     }
     for (int o = 32; o > 0; o >>= 1) n_shadow += __shfl_xor(n_shadow, o);
     if (lane == 0) {
-        if (P.count_mask & 2u) bc_scan(cnt);
+        if constexpr (COUNT) bc_scan(cnt);
         bc_add(RT_OPS_N + 1, n_shadow);
     }
     bc_flush(ops_slot(S), P.ray_counters);
@@ -465,15 +471,18 @@ hipError_t launch_wave_init(uint32_t* levels, uint32_t n_words, uint32_t total_i
 }
 
 hipError_t wave_occupancy(int* trace_blocks, int* shadow_blocks, int* combine_blocks) {
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(trace_blocks, trace_level_kernel, 256, 0);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(trace_blocks, trace_level_kernel<false>, 256, 0);
     if (e != hipSuccess) return e;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<false>, 256, 0);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<false, false>, 256, 0);
     if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(combine_blocks, combine_level_kernel, 256, 0);
 }
 
 hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream) {
-    hipLaunchKernelGGL(trace_level_kernel, dim3(blocks), dim3(256), 0, stream, p, level);
+    if (p.count_mask & 1u)
+        hipLaunchKernelGGL(trace_level_kernel<true>, dim3(blocks), dim3(256), 0, stream, p, level);
+    else
+        hipLaunchKernelGGL(trace_level_kernel<false>, dim3(blocks), dim3(256), 0, stream, p, level);
     return hipGetLastError();
 }
 
@@ -481,10 +490,15 @@ hipError_t launch_wave_shadow(const WaveParams& p, int blocks, hipStream_t strea
     size_t lds = (size_t)p.S.n_bvh_nodes * 64;
     const char* e = getenv("RT_LDS_NODES");
     bool use = p.S.use_bvh && lds > 0 && lds <= 36 * 1024 && !(e && e[0] == '0');
-    if (use)
-        hipLaunchKernelGGL(shadow_kernel<true>, dim3(blocks), dim3(256), lds, stream, p);
+    const bool count = (p.count_mask & 2u) != 0;
+    if (use && count)
+        hipLaunchKernelGGL((shadow_kernel<true, true>), dim3(blocks), dim3(256), lds, stream, p);
+    else if (use)
+        hipLaunchKernelGGL((shadow_kernel<true, false>), dim3(blocks), dim3(256), lds, stream, p);
+    else if (count)
+        hipLaunchKernelGGL((shadow_kernel<false, true>), dim3(blocks), dim3(256), 0, stream, p);
     else
-        hipLaunchKernelGGL(shadow_kernel<false>, dim3(blocks), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL((shadow_kernel<false, false>), dim3(blocks), dim3(256), 0, stream, p);
     return hipGetLastError();
 }
 

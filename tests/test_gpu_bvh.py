@@ -30,6 +30,7 @@ def render(desc, w, h, depth, bvh=True):
         os.environ.pop("RT_BVH", None)
     try:
         assert s.uses_bvh == bvh or (bvh and desc.n_shapes == 0)
+        s.set_scan_counting(True)
         s.scan_ops(reset=True)
         img, cnt, _, _ = s.render(w, h, depth)
         ops = s.scan_ops()
@@ -123,3 +124,24 @@ def test_grazing_scene_identical_and_matches_oracle():
 def test_custom_scene_identical():
     from .test_gpu_parity import _custom_scene
     same_both_ways(_custom_scene(), 320, 240, 12)
+
+
+def test_counting_kernels_render_the_same_frame():
+    """rt_scene_set_scan_counting switches to instrumented kernels; frames must not move."""
+    s = DeviceScene(SceneDesc.synth_config(3))
+    try:
+        a, ca, _, _ = s.render(320, 180, 8)
+        s.set_scan_counting(True)
+        s.scan_ops(reset=True)
+        b, cb, _, _ = s.render(320, 180, 8)
+        ops = s.scan_ops()
+        s.set_scan_counting(False)
+        s.scan_ops(reset=True)
+        c, cc, _, _ = s.render(320, 180, 8)
+        assert s.scan_ops()["node_pairs"] == 0      # uncounted kernels add nothing
+    finally:
+        s.close()
+    assert ops["node_pairs"] > 0 and ops["dsph_pairs"] > 0
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert np.array_equal(a.view(np.uint32), c.view(np.uint32))
+    assert ca == cb == cc

@@ -19,6 +19,7 @@ def run(config, w, h, depth, bvh):
     finally:
         os.environ.pop("RT_BVH", None)
     s.render(w, h, depth)
+    s.set_scan_counting(True)
     s.scan_ops(reset=True)
     _, cnt, ms, _ = s.render(w, h, depth)
     ops = s.scan_ops()
