@@ -197,9 +197,11 @@ uint64_t rt_scene_device_bytes(const rt_scene* scene);
 /* Lane-weighted counts of the ray-primitive and ray-box tests the scene's scans ran
  * since the last reset, in this order: child-box pairs, diagonal-sphere pairs, general
  * spheres, triangle pairs, cube boxes, full cubes (12 triangles), grazing cone tests
- * (blocks of 8 triangles), planes, grazing normal tests (blocks of 8).  Synchronises
- * the device; reset != 0 zeroes the counts after reading.  `out` may be NULL. */
-#define RT_SCAN_OPS_N 9
+ * (blocks of 8 triangles), planes, grazing normal tests (blocks of 8); then shader-clock
+ * cycles per wave in child-box tests, leaf tests, the grazing pass and whole scans.
+ * Synchronises the device; reset != 0 zeroes the counts after reading.  `out` may be
+ * NULL. */
+#define RT_SCAN_OPS_N 13
 rt_status rt_scene_scan_ops(rt_scene* scene, uint64_t* out, uint32_t n, int32_t reset);
 
 /* Counting is instrumentation: renders after rt_scene_set_scan_counting(scene, 1) run

@@ -250,7 +250,7 @@ class DeviceScene:
         return bool(self._L.rt_scene_uses_bvh(self.h))
 
     SCAN_OPS = ("node_pairs", "dsph_pairs", "gsph", "tri_pairs", "cube_boxes", "cubes", "graze_cones",
-                "planes", "graze_normals")
+                "planes", "graze_normals", "cycles_nodes", "cycles_leaves", "cycles_graze", "cycles_scans")
 
     def set_scan_counting(self, enable=True):
         """Run the instrumented (counting) kernels from now on (rt_scene_set_scan_counting)."""

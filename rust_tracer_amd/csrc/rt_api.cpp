@@ -411,7 +411,9 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
             prims.push_back(p);
             geo.push_back(g);
         }
-        for (size_t i = 0; i < tris.size(); i++) {
+        const char* bt_env = std::getenv("RT_BVH_TRIS");  // "0": loose triangles stay linear (A/B)
+        const bool tris_in_bvh = !(bt_env && bt_env[0] == '0');
+        for (size_t i = 0; i < tris.size() && tris_in_bvh; i++) {
             const TriIn& t = tris[i];
             double v[3][3] = {{t.v[0].x, t.v[0].y, t.v[0].z}, {t.v[1].x, t.v[1].y, t.v[1].z},
                               {t.v[2].x, t.v[2].y, t.v[2].z}};

@@ -98,7 +98,12 @@ enum : int {
     RT_OPS_GRAZE = 6,   // grazing cone tests (blocks of 8 triangles)
     RT_OPS_PLANE = 7,   // planes
     RT_OPS_GRAZE_N = 8, // grazing normal tests (blocks of 8 whose cone some lane meets)
-    RT_OPS_N = 9,
+    // instrumented kernels only: shader-clock cycles (s_memtime) per wave spent in
+    RT_OPS_CYC_NODE = 9,   // ... child-box tests and their stack / branch bookkeeping
+    RT_OPS_CYC_LEAF = 10,  // ... leaf primitive tests
+    RT_OPS_CYC_GRAZE = 11, // ... the grazing pass
+    RT_OPS_CYC_SCAN = 12,  // ... whole scans (planes, walk, grazing pass, linear rest)
+    RT_OPS_N = 13,
     // scan_ops is RT_OPS_SLOTS x RT_OPS_STRIDE u64: block b adds to slot b % RT_OPS_SLOTS
     // (same-address global atomics from every block would serialise in L2)
     RT_OPS_SLOTS = 64,

@@ -264,17 +264,26 @@ __device__ __forceinline__ void plane_one(cfloat4* r, V3 o, V3 d, float& bt, uin
 // Lane-weighted counts of every test the scan runs (RT_OPS_*): wave-uniform, kept in
 // SGPRs, added to DevScene::scan_ops once per wave when a kernel ends.
 struct ScanCnt {
+    static constexpr bool kCount = true;
     uint32_t node, dsph, gsph, tri, cube_box, cube, graze, plane, graze_n;
+    uint32_t cyc_node, cyc_leaf, cyc_graze, cyc_scan;
 };
+__device__ __forceinline__ uint32_t rt_clock() { return (uint32_t)__builtin_amdgcn_s_memtime(); }
 // The uncounted variant: the same expressions, every `+=` a no-op (compiled away).
 struct NoCntField {
     __device__ NoCntField& operator+=(uint32_t) { return *this; }
 };
 struct NoCnt {
+    static constexpr bool kCount = false;
     NoCntField node, dsph, gsph, tri, cube_box, cube, graze, plane, graze_n;
+    NoCntField cyc_node, cyc_leaf, cyc_graze, cyc_scan;
 };
+// cycle accounting of the instrumented variant (compiled away otherwise)
+#define RT_T0(C, v) uint32_t v = 0; if constexpr (C::kCount) v = rt_clock()
+#define RT_T1(C, c, f, v) do { if constexpr (C::kCount) (c).f += rt_clock() - (v); } while (0)
 __device__ __forceinline__ void cnt_init(ScanCnt& c) {
     c.node = c.dsph = c.gsph = c.tri = c.cube_box = c.cube = c.graze = c.plane = c.graze_n = 0;
+    c.cyc_node = c.cyc_leaf = c.cyc_graze = c.cyc_scan = 0;
 }
 __device__ __forceinline__ uint32_t active_lanes() { return (uint32_t)__builtin_popcountll(__ballot(1)); }
 #define RT_OPS(c, f) ((c).f += active_lanes())
@@ -512,8 +521,10 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
         // light for shadow rays, nothing once decided
         float tmax = SHADOW ? (done ? -1.f : fminf(bt, tlim)) : bt;
         float tnode = (tmax < 0.f) ? -__builtin_huge_valf() : tmax + R.m;
+        RT_T0(C, t_it);
         if (cur & BVH_LEAF) {
             bvh_leaf(S, cur & ~BVH_LEAF, o, d, R.on, tmax, bt, bk, c);
+            RT_T1(C, c, cyc_leaf, t_it);
             if (SHADOW) {
                 done = shadow_decided(o, d, bt, l2);
                 if (__ballot(!done) == 0) break;
@@ -538,6 +549,7 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
             RT_OPS(c, node);
             bool anyA = __ballot(hA) != 0, anyB = __ballot(hB) != 0;
             uint32_t cA = __float_as_uint(q3.x), cB = __float_as_uint(q3.y);
+            RT_T1(C, c, cyc_node, t_it);
             if (anyA && anyB) {
                 uint32_t axis = __float_as_uint(q3.z);
                 float da = rfl(axis == 0 ? d.x : (axis == 1 ? d.y : d.z));
@@ -567,6 +579,7 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
 template <class C>
 __device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c) {
     if (S.n_graze_blk == 0) return;
+    RT_T0(C, t_g);
     const float dd = len2(d);
     const float lim = S.graze_s2 * dd;
     cfloat4* g = cptr(S.graze_blk);
@@ -603,6 +616,7 @@ __device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float&
             tri_pair(ld_tri(tp + 18), o, d, bt, bk);
         }
     }
+    RT_T1(C, c, cyc_graze, t_g);
 }
 
 template <class C>
@@ -625,6 +639,7 @@ __device__ __forceinline__ void linear_rest(const DevScene& S, V3 o, V3 d, float
 // Scene::intersect (scene/mod.rs:98-116): the nearest (t, key) over every shape.
 template <class C>
 __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c) {
+    RT_T0(C, t_s);
     bt = __builtin_huge_valf();
     bk = 0xFFFFFFFFu;
     RT_STAT(0);
@@ -634,6 +649,7 @@ __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, u
         graze_pass(S, o, d, bt, bk, c);
     }
     linear_rest(S, o, d, bt, bk, c);
+    RT_T1(C, c, cyc_scan, t_s);
 }
 
 // ------------------------------------------------------------------ shadow scan
@@ -651,6 +667,7 @@ __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, u
 // A wave leaves the scan when every active lane is decided.  Returns `shadowed`.
 template <bool LDS, class C>
 __device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lpos, C& c, lfloat4* lnodes) {
+    RT_T0(C, t_s);
     const float l2 = len2(sub(lpos, o));
     float bt = __builtin_huge_valf();
     uint32_t bk = 0xFFFFFFFFu;
@@ -669,5 +686,6 @@ __device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lp
     }
     linear_rest(S, o, d, bt, bk, c);
 finish:
+    RT_T1(C, c, cyc_scan, t_s);
     return shadow_hit(o, d, bt, l2);
 }

@@ -123,6 +123,10 @@ __device__ __forceinline__ void bc_scan(const ScanCnt& c) {
     bc_add(RT_OPS_GRAZE, c.graze);
     bc_add(RT_OPS_PLANE, c.plane);
     bc_add(RT_OPS_GRAZE_N, c.graze_n);
+    bc_add(RT_OPS_CYC_NODE, c.cyc_node);
+    bc_add(RT_OPS_CYC_LEAF, c.cyc_leaf);
+    bc_add(RT_OPS_CYC_GRAZE, c.cyc_graze);
+    bc_add(RT_OPS_CYC_SCAN, c.cyc_scan);
 }
 
 __device__ __forceinline__ uint64_t lanemask_lt() {
@@ -150,8 +154,12 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, uint32_t n, u
     return base + mine;
 }
 
+#ifndef RT_TRACE_WAVES
+#define RT_TRACE_WAVES 5  // 96 VGPRs, 20 B scratch (measured: 4 -> 8.02 ms, 5 -> 7.89, 6 -> 7.85 with 84 B)
+#endif
 template <bool COUNT>
-__global__ __launch_bounds__(256) void trace_level_kernel(WaveParams P, uint32_t level) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES, 8))) void trace_level_kernel(
+    WaveParams P, uint32_t level) {
     const DevScene& S = P.S;
     const uint32_t off = P.levels[2 * level];
     const uint32_t count = min(P.levels[2 * level + 1], off < P.capacity ? P.capacity - off : 0u);

@@ -26,7 +26,11 @@ def run(config, w, h, depth, bvh):
     rays = cnt["node_rays"] + cnt["shadow_rays"]
     print(f"bvh={bvh} kernel {ms:.2f} ms  node rays {cnt['node_rays']} shadow rays {cnt['shadow_rays']}")
     for k, v in ops.items():
-        print(f"   {k:12s} {v:14d}  per ray {v / rays:9.2f}")
+        if k.startswith("cycles"):
+            share = v / max(1, ops["cycles_scans"])
+            print(f"   {k:14s} {v:14d}  share of scan cycles {share:6.3f}")
+        else:
+            print(f"   {k:14s} {v:14d}  per ray {v / rays:9.2f}")
     s.close()
 
 
