@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--backend", default="nccl", help="nccl (RCCL) or gloo (CPU rehearsal)")
     p.add_argument("--check", type=int, default=0,
                    help="rank 0 compares the assembled frame with a single-launch render")
+    p.add_argument("--count-frame", type=int, default=1,
+                   help="0: skip the instrumented (counting) frame; roofline test counts are then null "
+                        "(used by the rocprofv3 counter passes so they see only the default kernels)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="rocprofv3 FETCH_SIZE/WRITE_SIZE summary for the render kernel")
     return p.parse_args()
@@ -134,12 +137,14 @@ def main():
     torch.cuda.synchronize()
     # one instrumented frame (untimed) counts the scans' tests; frames are deterministic,
     # so every timed frame runs exactly these tests, uncounted
-    scene.set_scan_counting(True)
-    scene.scan_ops(reset=True)
-    tiler.step()
-    torch.cuda.synchronize()
-    ops = scene.scan_ops()
-    scene.set_scan_counting(False)
+    ops = None
+    if args.count_frame:
+        scene.set_scan_counting(True)
+        scene.scan_ops(reset=True)
+        tiler.step()
+        torch.cuda.synchronize()
+        ops = scene.scan_ops()
+        scene.set_scan_counting(False)
     tiler.counters.zero_()
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -180,8 +185,8 @@ def main():
         steps = args.steps
         mpix = args.width * args.height * steps / elapsed / 1e6
         # rank 0's launch: the tests its scans ran (culled), at their algorithmic flops
-        per_launch_flops = sum(ops[k] * OP_FLOPS[k] for k in OP_FLOPS)
-        achieved = per_launch_flops / (kernel_ms / 1e3) / 1e12
+        per_launch_flops = sum(ops[k] * OP_FLOPS[k] for k in OP_FLOPS) if ops else None
+        achieved = per_launch_flops / (kernel_ms / 1e3) / 1e12 if ops else None
         # what the reference's linear scan would need for the same rays (F_alg per scan)
         brute_flops = local_scans * scene.flops_per_scan
         workload = (f"config{args.config}: synth seed 2 (600 spheres, 25 cubes, 100 triangles, "
@@ -189,16 +194,17 @@ def main():
         traffic = load_traffic(args.traffic_json, workload)
         roofline = {
             "bound": "valu",
-            "achieved": round(achieved, 3),
+            "achieved": round(achieved, 3) if ops else None,
             "peak": PEAK_F32_TFLOPS,
             "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_F32_TFLOPS, 4),
+            "frac": round(achieved / PEAK_F32_TFLOPS, 4) if ops else None,
             "traffic": traffic["bytes_per_launch"] if traffic else None,
             "kernel": ("one frame: trace_level_kernel per level + queue sorts + shadow_kernel + "
                        "combine_level_kernel per level"),
             "kernel_ms": round(kernel_ms, 4),
             "flops_per_launch": per_launch_flops,
-            "tests_per_launch": ops,
+            "tests_per_launch": {k: v for k, v in ops.items() if not k.startswith("cycles")} if ops else None,
+            "cycles_per_launch": {k: v for k, v in ops.items() if k.startswith("cycles")} if ops else None,
             "culling": {"hierarchy": scene.uses_bvh,
                         "linear_scan_flops_per_launch": brute_flops,
                         "linear_scan_equivalent_TFLOPs": round(brute_flops / (kernel_ms / 1e3) / 1e12, 3)},

@@ -22,6 +22,9 @@ RENDER = ("trace_level_kernel", "shadow_kernel", "combine_level_kernel", "wave_i
 
 def family(kernel_name):
     """short family name of a render-pipeline dispatch (None if not one)"""
+    if ("trace_level_kernel<true>" in kernel_name or "shadow_kernel<true, true>" in kernel_name
+            or "shadow_kernel<false, true>" in kernel_name):
+        return "instrumented variant (counted frame only)"
     for k in RENDER:
         if k in kernel_name:
             if k == "rocprim":
@@ -50,8 +53,8 @@ def main(tag):
             d["Duration_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             w.writerow(d)
     bench = json.load(open(os.path.join(src, "bench.json")))
-    steps_prof = 1  # the PMC passes run bench.py --steps 1 --warmup 0: one frame
     pmc = {}
+    pmc_frames = {}
     for p in ("pmc_sq", "pmc_fetch", "pmc_write"):
         rr = list(csv.DictReader(open(os.path.join(src, p, "run_counter_collection.csv"))))
         kept = [r for r in rr if any(k in r["Kernel_Name"] for k in RENDER)]
@@ -63,15 +66,28 @@ def main(tag):
         agg = defaultdict(float)
         for r in kept:
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
-        pmc.update(agg)
+        # frames in this pass (bench.py --steps 2 --warmup 0 --count-frame 0: 2 default frames)
+        inits = {r["Dispatch_Id"] for r in kept if "wave_init_kernel" in r["Kernel_Name"]}
+        for k in agg:
+            pmc_frames[k] = max(1, len(inits))
+        pmc.update({k: v / pmc_frames[k] for k, v in agg.items()})
     # kernel-trace: per-frame time of each render kernel family (the trace run did 1 + 3 frames)
-    per = defaultdict(list)
-    for r in keep:
-        per[family(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-    frames = 4
-    fam_ms = {k: sum(v) / frames / 1e6 for k, v in per.items()}
-    fetch_b = pmc.get("FETCH_SIZE", 0.0) * 1024 / steps_prof
-    write_b = pmc.get("WRITE_SIZE", 0.0) * 1024 / steps_prof
+    # split the dispatches into frames at each wave_init (bench.py: warm-up + one counted
+    # frame + timed frames); a family's ms per frame averages the frames it ran in (the
+    # counted frame runs the instrumented kernels instead of the default ones)
+    frame_sums = []
+    for r in sorted(keep, key=lambda r: int(r["Start_Timestamp"])):
+        fam = family(r["Kernel_Name"])
+        if fam == "wave_init_kernel" or not frame_sums:
+            frame_sums.append(defaultdict(int))
+        frame_sums[-1][fam] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    frames = len(frame_sums)
+    fams = {f for fs in frame_sums for f in fs}
+    fam_ms = {f: sum(fs[f] for fs in frame_sums if f in fs) / sum(1 for fs in frame_sums if f in fs) / 1e6
+              for f in fams}
+    timed_ms = sum(v for f, v in fam_ms.items() if not f.startswith("instrumented"))
+    fetch_b = pmc.get("FETCH_SIZE", 0.0) * 1024
+    write_b = pmc.get("WRITE_SIZE", 0.0) * 1024
     traffic = {
         "workload": bench["config"]["workload"],
         "bytes_per_launch": fetch_b * 2 + write_b,
@@ -93,15 +109,15 @@ def main(tag):
         f"{frame_ms} ms (HIP events), algorithmic {bench['roofline']['achieved']} TFLOP/s = "
         f"{bench['roofline']['frac']:.3f} of 157.3 (f32 vector peak).",
         "",
-        "## rocprofv3 --kernel-trace --stats (4 frames: 1 warm-up + 3 timed)",
+        f"## rocprofv3 --kernel-trace --stats ({frames} frames: warm-up + counted + timed; ms per frame)",
         "",
         "| kernel family | ms per frame |",
         "|---|---|",
     ] + [f"| {k} | {v:.3f} |" for k, v in sorted(fam_ms.items(), key=lambda x: -x[1])] + [
         "",
-        f"Sum of render kernels per frame: {sum(fam_ms.values()):.3f} ms (bench HIP events: {frame_ms} ms).",
+        f"Sum of the default kernels per frame: {timed_ms:.3f} ms (bench HIP events: {frame_ms} ms).",
         "",
-        "## PMC (one frame, separate passes, render kernels only)",
+        "## PMC (per frame, separate passes, render kernels only)",
         "",
         "| counter | value |",
         "|---|---|",
