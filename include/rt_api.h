@@ -213,6 +213,41 @@ rt_status rt_scene_set_scan_counting(rt_scene* scene, int32_t enable);
  * environment at rt_scene_create turns it off), 0 if they test every shape. */
 int32_t rt_scene_uses_bvh(const rt_scene* scene);
 
+/* ---- ray forest (src/render_tree.rs) -------------------------------------------------
+ * generate_ray_forest(camera, scene, w, h, depth) -> RayForest (render_tree.rs:147-164):
+ * traces every pixel's ray tree (the same rays, shadow tests and child rules as
+ * render.rs) once and keeps every intersection on the device. */
+typedef struct rt_forest rt_forest;
+rt_status rt_forest_create(rt_scene* scene, const rt_camera* camera, uint32_t depth, rt_forest** out);
+rt_status rt_forest_destroy(rt_forest* forest);
+
+/* render_forest(&forest, &mut buffer, ambient) (render_tree.rs:121-127, render_ray_tree
+ * :214-255): shades every tree with the scene's CURRENT materials into `rgb`
+ * (row-major y_res x x_res x 3 floats).  Note the forest's shading differs from
+ * render.rs: the reflected term uses the hit's eye_dir as light direction, the refracted
+ * term is not scaled by the diffuse colour. */
+rt_status rt_forest_render(rt_forest* forest, float* rgb);
+
+/* render_forest_filter(&forest, &mut buffer, ambient, mutated_shapes)
+ * (render_tree.rs:129-145): re-shades only the pixels whose tree holds one of
+ * `mutated_ids`; the other pixels of `rgb` are left as they are.  Shape ids are the
+ * reference's: the insertion index, except that a cube hit reports the id of the cube's
+ * inner triangle (0..11, cube.rs:93-99). */
+rt_status rt_forest_render_filter(rt_forest* forest, const int32_t* mutated_ids, uint32_t n_ids, float* rgb);
+
+/* RayTree::size per pixel (render_tree.rs:39-48, row-major), for RayForest::stats (:73-93). */
+rt_status rt_forest_tree_sizes(rt_forest* forest, uint32_t* sizes);
+
+/* RayForest::trees_with(shape_id) (render_tree.rs:66-71). */
+rt_status rt_forest_trees_with(rt_forest* forest, int32_t shape_id, uint64_t* count);
+
+/* Ray counts of the build (node rays, shadow rays, pixels). */
+rt_status rt_forest_counters(const rt_forest* forest, rt_counters* out);
+
+/* Replace material `index`'s parameters (same kind) -- the GUI's material edits
+ * (gui.rs:221-236).  Affects later renders and forest shades. */
+rt_status rt_scene_set_material(rt_scene* scene, uint32_t index, const rt_material* material);
+
 const char* rt_status_str(rt_status status);
 int32_t rt_api_version(void);
 

@@ -45,6 +45,14 @@ def lib():
     L.oracle_render_rows_mt.argtypes = [vp, P(abi.rt_camera), C.c_uint32, C.c_uint32, C.c_uint32,
                                         C.c_uint32, fa, P(C.c_uint64), C.c_uint32]
     L.oracle_render_forest.argtypes = [vp, P(abi.rt_camera), C.c_uint32, fa, P(C.c_uint32)]
+    L.oracle_forest_build.argtypes = [vp, P(abi.rt_camera), C.c_uint32, P(vp)]
+    L.oracle_forest_render.argtypes = [vp, fa]
+    L.oracle_forest_render_filter.argtypes = [vp, P(C.c_int32), C.c_uint32, fa]
+    L.oracle_forest_tree_sizes.argtypes = [vp, P(C.c_uint32)]
+    L.oracle_forest_trees_with.argtypes = [vp, C.c_int32]
+    L.oracle_forest_trees_with.restype = C.c_uint64
+    L.oracle_forest_destroy.argtypes = [vp]
+    L.oracle_scene_set_material.argtypes = [vp, C.c_uint32, P(abi.rt_material)]
     L.oracle_as_u8.argtypes = [fa, C.c_uint64, P(C.c_uint8)]
     for n in ("identity",):
         getattr(L, "oracle_matrix_" + n).argtypes = [fa]
@@ -111,6 +119,15 @@ class OracleScene:
             raise RuntimeError(f"oracle_render failed: {st}")
         return rgb, {"node_rays": cnt[0], "shadow_rays": cnt[1], "pixels": cnt[2]}
 
+    def set_material(self, index, material):
+        """In-place material edit (desc-built scenes); mirrors rt_scene_set_material."""
+        st = self.L.oracle_scene_set_material(self.h, index, C.byref(material))
+        if st != 0:
+            raise RuntimeError(f"oracle_scene_set_material failed: {st}")
+
+    def forest(self, x_res, y_res, depth):
+        return OracleForest(self, x_res, y_res, depth)
+
     def render_forest(self, x_res, y_res, depth):
         from rust_tracer_amd import abi
         cam = abi.camera(x_res, y_res)
@@ -122,6 +139,44 @@ class OracleScene:
         if st != 0:
             raise RuntimeError(f"oracle_render_forest failed: {st}")
         return rgb, sizes
+
+
+class OracleForest:
+    """render_tree.rs RayForest on the CPU (test infrastructure)."""
+
+    def __init__(self, scene, x_res, y_res, depth):
+        from rust_tracer_amd import abi
+        self.L, self.scene = scene.L, scene
+        self.w, self.h_res = x_res, y_res
+        self.h = C.c_void_p()
+        cam = abi.camera(x_res, y_res)
+        st = self.L.oracle_forest_build(scene.h, C.byref(cam), depth, C.byref(self.h))
+        if st != 0:
+            raise RuntimeError(f"oracle_forest_build failed: {st}")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.oracle_forest_destroy(self.h)
+            self.h = None
+
+    def render(self):
+        rgb = np.zeros((self.h_res, self.w, 3), np.float32)
+        self.L.oracle_forest_render(self.h, rgb.ctypes.data_as(C.POINTER(C.c_float)))
+        return rgb
+
+    def render_filter(self, mutated_ids, rgb):
+        rgb = np.array(rgb, np.float32, copy=True)
+        ids = (C.c_int32 * max(1, len(mutated_ids)))(*mutated_ids)
+        self.L.oracle_forest_render_filter(self.h, ids, len(mutated_ids), rgb.ctypes.data_as(C.POINTER(C.c_float)))
+        return rgb
+
+    def tree_sizes(self):
+        sizes = np.zeros((self.h_res, self.w), np.uint32)
+        self.L.oracle_forest_tree_sizes(self.h, sizes.ctypes.data_as(C.POINTER(C.c_uint32)))
+        return sizes
+
+    def trees_with(self, shape_id):
+        return int(self.L.oracle_forest_trees_with(self.h, shape_id))
 
 
 def as_u8(rgb):

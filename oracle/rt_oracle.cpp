@@ -773,9 +773,9 @@ static ColorFun texfun(const rt_texture& t) {
     return [c](TexCoords) { return c; };
 }
 
-static rt_status from_desc(const rt_scene_desc* d, Scene& scene) {
+static rt_status from_desc(const rt_scene_desc* d, Scene& scene, std::vector<std::shared_ptr<Material>>& mats) {
     if (!d) return RT_ERR_INVALID_ARG;
-    std::vector<std::shared_ptr<Material>> mats;
+    mats.clear();
     for (uint32_t k = 0; k < d->n_materials; k++) {
         const rt_material& m = d->materials[k];
         if (m.kind == RT_MAT_PHONG) {
@@ -852,6 +852,15 @@ using namespace oracle;
 
 struct oracle_scene {
     Scene scene;
+    std::vector<std::shared_ptr<Material>> mats;  // by description index (shared with the shapes)
+};
+
+// render_tree.rs:51-105: one RayTree per pixel (row-major here), its shape-id set
+struct oracle_forest {
+    const oracle_scene* s = nullptr;
+    uint32_t w = 0, h = 0;
+    std::vector<std::unique_ptr<RayTreeNode>> roots;
+    std::vector<std::set<int32_t>> shapes;
 };
 
 extern "C" {
@@ -859,7 +868,7 @@ extern "C" {
 rt_status oracle_scene_from_desc(const rt_scene_desc* desc, oracle_scene** out) {
     if (!out) return RT_ERR_INVALID_ARG;
     std::unique_ptr<oracle_scene> s(new oracle_scene());
-    rt_status st = from_desc(desc, s->scene);
+    rt_status st = from_desc(desc, s->scene, s->mats);
     if (st != RT_OK) return st;
     *out = s.release();
     return RT_OK;
@@ -934,6 +943,97 @@ rt_status oracle_render_forest(const oracle_scene* s, const rt_camera* cam, uint
         }
     }
     return RT_OK;
+}
+
+// ---- persistent forest: generate_ray_forest (render_tree.rs:147-164) once, then
+// render_forest (:121-127) / render_forest_filter (:129-145) any number of times; the
+// trees hold the scene's materials, so oracle_scene_set_material edits show up on the
+// next shade exactly as the GUI's RefCell mutations do (gui.rs:221-236)
+rt_status oracle_forest_build(const oracle_scene* s, const rt_camera* cam, uint32_t depth, oracle_forest** out) {
+    if (!s || !cam || !out) return RT_ERR_INVALID_ARG;
+    std::unique_ptr<oracle_forest> f(new oracle_forest());
+    Camera c = cam_of(cam);
+    f->s = s;
+    f->w = c.x_res;
+    f->h = c.y_res;
+    f->roots.resize((size_t)c.x_res * c.y_res);
+    f->shapes.resize((size_t)c.x_res * c.y_res);
+    Counters cnt;
+    for (uint32_t v = 0; v < c.y_res; v++)
+        for (uint32_t u = 0; u < c.x_res; u++) {
+            size_t k = (size_t)v * c.x_res + u;
+            f->roots[k] = build_ray_tree(s->scene, c.get_ray(u, v), depth, f->shapes[k], cnt);
+        }
+    *out = f.release();
+    return RT_OK;
+}
+
+rt_status oracle_forest_render(const oracle_forest* f, float* rgb) {
+    if (!f || !rgb) return RT_ERR_INVALID_ARG;
+    for (size_t k = 0; k < f->roots.size(); k++) {
+        Color col = render_ray_tree(f->roots[k].get(), f->s->scene.ambient).first;
+        rgb[3 * k] = col.r; rgb[3 * k + 1] = col.g; rgb[3 * k + 2] = col.b;
+    }
+    return RT_OK;
+}
+
+rt_status oracle_forest_render_filter(const oracle_forest* f, const int32_t* ids, uint32_t n_ids, float* rgb) {
+    if (!f || !rgb || (n_ids && !ids)) return RT_ERR_INVALID_ARG;
+    std::set<int32_t> mutated(ids, ids + n_ids);
+    for (size_t k = 0; k < f->roots.size(); k++) {
+        bool hit = false;
+        for (int32_t id : f->shapes[k])
+            if (mutated.count(id)) { hit = true; break; }
+        if (!hit) continue;  // the pixel keeps its previous value
+        Color col = render_ray_tree(f->roots[k].get(), f->s->scene.ambient).first;
+        rgb[3 * k] = col.r; rgb[3 * k + 1] = col.g; rgb[3 * k + 2] = col.b;
+    }
+    return RT_OK;
+}
+
+rt_status oracle_forest_tree_sizes(const oracle_forest* f, uint32_t* sizes) {
+    if (!f || !sizes) return RT_ERR_INVALID_ARG;
+    for (size_t k = 0; k < f->roots.size(); k++) sizes[k] = tree_size(f->roots[k].get());
+    return RT_OK;
+}
+
+uint64_t oracle_forest_trees_with(const oracle_forest* f, int32_t id) {  // render_tree.rs:66-71
+    uint64_t n = 0;
+    if (f)
+        for (const auto& st : f->shapes) n += st.count(id) ? 1u : 0u;
+    return n;
+}
+
+void oracle_forest_destroy(oracle_forest* f) { delete f; }
+
+// Replaces material `index`'s parameters in place (same kind): every shape and every
+// cached intersection that holds it sees the new values.
+rt_status oracle_scene_set_material(oracle_scene* s, uint32_t index, const rt_material* m) {
+    if (!s || !m || index >= s->mats.size()) return RT_ERR_INVALID_ARG;
+    Material* cur = s->mats[index].get();
+    if (m->kind == RT_MAT_PHONG) {
+        Phong* p = dynamic_cast<Phong*>(cur);
+        if (!p) return RT_ERR_INVALID_ARG;
+        p->ka = cc(m->ambient.color);
+        p->kd = cc(m->diffuse.color);
+        p->ks = cc(m->specular.color);
+        p->power = m->power;
+        p->refl = m->reflectivity;
+        p->ri = m->refraction_index;
+        return RT_OK;
+    }
+    if (m->kind == RT_MAT_TEXTURE_PHONG) {
+        TexturePhong* p = dynamic_cast<TexturePhong*>(cur);
+        if (!p) return RT_ERR_INVALID_ARG;
+        p->fa = texfun(m->ambient);
+        p->fd = texfun(m->diffuse);
+        p->fs = texfun(m->specular);
+        p->power = m->power;
+        p->refl = m->reflectivity;
+        p->ri = m->refraction_index;
+        return RT_OK;
+    }
+    return RT_ERR_INVALID_ARG;
 }
 
 void oracle_as_u8(const float* rgb, uint64_t n, uint8_t* out) {

@@ -91,6 +91,31 @@ def _color(c):
     return abi.rt_color(*[float(F32(v)) for v in c])
 
 
+def phong_material(ambient, diffuse, specular, power, reflectivity, refraction_index):
+    """Phong::new (material.rs:33-52) as an rt_material."""
+    m = abi.rt_material()
+    m.kind = RT_MAT_PHONG
+    m.ambient = abi.rt_texture(RT_TEX_CONST, _color(ambient))
+    m.diffuse = abi.rt_texture(RT_TEX_CONST, _color(diffuse))
+    m.specular = abi.rt_texture(RT_TEX_CONST, _color(specular))
+    m.power, m.reflectivity, m.refraction_index = power, reflectivity, refraction_index
+    return m
+
+
+def texture_phong_material(ambient, diffuse, specular, power, reflectivity, refraction_index):
+    """TexturePhong::new (material.rs:112-131); a texture is an RGB tuple or 'checkerboard'."""
+    def tex(t):
+        if isinstance(t, str):
+            assert t == "checkerboard"
+            return abi.rt_texture(RT_TEX_CHECKERBOARD, abi.rt_color(0, 0, 0))
+        return abi.rt_texture(RT_TEX_CONST, _color(t))
+    m = abi.rt_material()
+    m.kind = RT_MAT_TEXTURE_PHONG
+    m.ambient, m.diffuse, m.specular = tex(ambient), tex(diffuse), tex(specular)
+    m.power, m.reflectivity, m.refraction_index = power, reflectivity, refraction_index
+    return m
+
+
 class SceneDesc:
     """An rt_scene_desc: either produced by the C++ host builders (my_scene, synth,
     bench_128) or assembled here shape by shape (Scene::add_shape order)."""
@@ -134,27 +159,14 @@ class SceneDesc:
 
     # ---- assembled in Python
     def phong(self, ambient, diffuse, specular, power, reflectivity, refraction_index):
-        m = abi.rt_material()
-        m.kind = RT_MAT_PHONG
-        m.ambient = abi.rt_texture(RT_TEX_CONST, _color(ambient))
-        m.diffuse = abi.rt_texture(RT_TEX_CONST, _color(diffuse))
-        m.specular = abi.rt_texture(RT_TEX_CONST, _color(specular))
-        m.power, m.reflectivity, m.refraction_index = power, reflectivity, refraction_index
-        self.materials.append(m)
+        self.materials.append(phong_material(ambient, diffuse, specular, power, reflectivity,
+                                             refraction_index))
         return len(self.materials) - 1
 
     def texture_phong(self, ambient, diffuse, specular, power, reflectivity, refraction_index):
         """Each texture is an RGB tuple (constant) or the string 'checkerboard'."""
-        def tex(t):
-            if isinstance(t, str):
-                assert t == "checkerboard"
-                return abi.rt_texture(RT_TEX_CHECKERBOARD, abi.rt_color(0, 0, 0))
-            return abi.rt_texture(RT_TEX_CONST, _color(t))
-        m = abi.rt_material()
-        m.kind = RT_MAT_TEXTURE_PHONG
-        m.ambient, m.diffuse, m.specular = tex(ambient), tex(diffuse), tex(specular)
-        m.power, m.reflectivity, m.refraction_index = power, reflectivity, refraction_index
-        self.materials.append(m)
+        self.materials.append(texture_phong_material(ambient, diffuse, specular, power, reflectivity,
+                                                     refraction_index))
         return len(self.materials) - 1
 
     def _shape(self, kind, mat, transform=None, data=()):
@@ -280,11 +292,85 @@ class DeviceScene:
         self.last_wave_iterations = cnt.wave_iterations
         return rgb, counters, ms.value, rgb8
 
+    def set_material(self, index, material):
+        """rt_scene_set_material: replace material `index` (same kind), e.g. the GUI's edits."""
+        check(self._L.rt_scene_set_material(self.h, index, C.byref(material)), "rt_scene_set_material")
+
+    def forest(self, x_res, y_res, depth):
+        """generate_ray_forest (render_tree.rs:147-164) on the device."""
+        return DeviceForest(self, x_res, y_res, depth)
+
     def render_bands_async(self, cam, depth, band_rows, rank, world, d_rgb_ptr, d_counters_ptr,
                            stream_ptr):
         check(self._L.rt_render_bands_async(self.h, C.byref(cam), depth, band_rows, rank, world,
                                             C.c_void_p(d_rgb_ptr), C.c_void_p(d_counters_ptr),
                                             C.c_void_p(stream_ptr)), "rt_render_bands_async")
+
+
+class DeviceForest:
+    """A RayForest kept on the device (rt_forest_*): built once, shaded any number of times."""
+
+    def __init__(self, scene, x_res, y_res, depth):
+        self._L = lib()
+        self.scene = scene  # keeps the scene alive
+        self.w, self.h_res = x_res, y_res
+        self.h = C.c_void_p()
+        cam = camera(x_res, y_res)
+        check(self._L.rt_forest_create(scene.h, C.byref(cam), depth, C.byref(self.h)), "rt_forest_create")
+
+    def close(self):
+        if self.h:
+            self._L.rt_forest_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def render(self):
+        """render_forest (render_tree.rs:121-127) -> rgb float32 [y, x, 3]"""
+        rgb = np.zeros((self.h_res, self.w, 3), np.float32)
+        check(self._L.rt_forest_render(self.h, rgb.ctypes.data_as(C.POINTER(C.c_float))), "rt_forest_render")
+        return rgb
+
+    def render_filter(self, mutated_ids, rgb):
+        """render_forest_filter (render_tree.rs:129-145): a copy of `rgb` in which the pixels
+        whose tree holds a mutated shape id are re-shaded (the others keep their values)."""
+        rgb = np.array(rgb, np.float32, order="C", copy=True)
+        ids = (C.c_int32 * max(1, len(mutated_ids)))(*mutated_ids)
+        check(self._L.rt_forest_render_filter(self.h, ids, len(mutated_ids),
+                                              rgb.ctypes.data_as(C.POINTER(C.c_float))),
+              "rt_forest_render_filter")
+        return rgb
+
+    def tree_sizes(self):
+        sizes = np.zeros((self.h_res, self.w), np.uint32)
+        check(self._L.rt_forest_tree_sizes(self.h, sizes.ctypes.data_as(C.POINTER(C.c_uint32))),
+              "rt_forest_tree_sizes")
+        return sizes
+
+    def trees_with(self, shape_id):
+        n = C.c_uint64(0)
+        check(self._L.rt_forest_trees_with(self.h, shape_id, C.byref(n)), "rt_forest_trees_with")
+        return int(n.value)
+
+    def counters(self):
+        c = abi.rt_counters()
+        check(self._L.rt_forest_counters(self.h, C.byref(c)), "rt_forest_counters")
+        return {"node_rays": c.node_rays, "shadow_rays": c.shadow_rays, "pixels": c.pixels}
+
+    def stats(self):
+        """RayForest::stats (render_tree.rs:73-93), including its f32 percentile indexing."""
+        sizes = np.sort(self.tree_sizes().ravel(order="F"))  # the reference iterates forest[u][v]
+        n = len(sizes)
+
+        def at(q):
+            return int(sizes[int(np.float32(q) * np.float32(n))])
+        return {"num_trees": n, "num_intersections": int(sizes.sum()), "smallest_tree": int(sizes.min()),
+                "largest_tree": int(sizes.max()), "median": int(sizes[n // 2]), "p90": at(0.9),
+                "p95": at(0.95), "p99": at(0.99)}
 
 
 def band_rows_per_rank(y_res, band_rows, world):

@@ -131,6 +131,14 @@ def lib():
     L.rt_scene_device_bytes.restype = C.c_uint64
     L.rt_scene_scan_ops.argtypes = [vp, P(C.c_uint64), C.c_uint32, C.c_int32]
     L.rt_scene_set_scan_counting.argtypes = [vp, C.c_int32]
+    L.rt_forest_create.argtypes = [vp, P(rt_camera), C.c_uint32, P(vp)]
+    L.rt_forest_destroy.argtypes = [vp]
+    L.rt_forest_render.argtypes = [vp, P(C.c_float)]
+    L.rt_forest_render_filter.argtypes = [vp, P(C.c_int32), C.c_uint32, P(C.c_float)]
+    L.rt_forest_tree_sizes.argtypes = [vp, P(C.c_uint32)]
+    L.rt_forest_trees_with.argtypes = [vp, C.c_int32, P(C.c_uint64)]
+    L.rt_forest_counters.argtypes = [vp, P(rt_counters)]
+    L.rt_scene_set_material.argtypes = [vp, C.c_uint32, P(rt_material)]
     L.rt_scene_uses_bvh.argtypes = [vp]
     L.rt_scene_uses_bvh.restype = C.c_int32
     L.rt_status_str.argtypes = [C.c_int32]

@@ -36,6 +36,10 @@ hipError_t launch_wave_init(uint32_t* levels, uint32_t n_words, uint32_t total_i
                             hipStream_t stream);
 hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream);
 hipError_t launch_wave_combine(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream);
+hipError_t launch_forest_shade(const WaveParams& p, uint32_t level, int blocks, float* frame, hipStream_t stream);
+hipError_t launch_forest_mark(const uint32_t* node_key, const uint32_t* node_pixel, const NodeRec* nodes,
+                              uint32_t n_nodes, const uint8_t* key_mask, uint32_t n_keys, uint8_t* mark,
+                              uint32_t* sizes, hipStream_t stream);
 hipError_t sort_pairs_u32(void* tmp, size_t& bytes, const uint32_t* keys_in, uint32_t* keys_out,
                           const uint32_t* vals_in, uint32_t* vals_out, uint32_t n, int end_bit,
                           hipStream_t stream);
@@ -134,6 +138,27 @@ void cube_triangles(std::vector<float>& out) {
         put4(out, e2.x, e2.y, e2.z, 0.f);
         put4(out, n.x, n.y, n.z, 0.f);
     }
+}
+
+// rt_material -> device record (material.rs: Phong / TexturePhong with a closed set of
+// texture programs)
+rt_status mat_rec(const rt_material& m, MatRec& M) {
+    if (m.kind != RT_MAT_PHONG && m.kind != RT_MAT_TEXTURE_PHONG) return RT_ERR_INVALID_ARG;
+    const rt_texture* tx[3] = {&m.ambient, &m.diffuse, &m.specular};
+    for (int k = 0; k < 3; k++) {
+        if (tx[k]->kind != RT_TEX_CONST && tx[k]->kind != RT_TEX_CHECKERBOARD) return RT_ERR_INVALID_ARG;
+        // Phong ignores texture programs: its colours are constants (material.rs:55-65)
+        if (m.kind == RT_MAT_PHONG && tx[k]->kind != RT_TEX_CONST) return RT_ERR_INVALID_ARG;
+    }
+    std::memset(&M, 0, sizeof(M));
+    M.kind = m.kind;
+    M.power = m.power;
+    M.reflectivity = m.reflectivity;
+    M.refraction_index = m.refraction_index;
+    M.ambient = TexRec{m.ambient.kind, m.ambient.color.r, m.ambient.color.g, m.ambient.color.b};
+    M.diffuse = TexRec{m.diffuse.kind, m.diffuse.color.r, m.diffuse.color.g, m.diffuse.color.b};
+    M.specular = TexRec{m.specular.kind, m.specular.color.r, m.specular.color.g, m.specular.color.b};
+    return RT_OK;
 }
 
 // ---- culling hierarchy (rt_bvh.hpp) and the run layout --------------------------------
@@ -619,6 +644,11 @@ struct Workspace {
     void* sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
     uint32_t* h_count = nullptr;     // pinned: a level's (offset, count)
+    // ray forest only (rt_forest): per-node shade inputs, grown with the pool
+    bool forest = false;
+    float4* node_aux = nullptr;
+    uint32_t* node_key = nullptr;
+    uint32_t* node_pixel = nullptr;
 };
 
 // RT_SORT=0 keeps the queues in production order, RT_SORT=shadow orders only the
@@ -740,8 +770,31 @@ rt_status grow_node_pool(Workspace& w, uint32_t cap) {
     HIP_TRY(hipMalloc(&w.nodes, (size_t)cap * sizeof(NodeRec)));
     HIP_TRY(hipMalloc(&w.node_ps, (size_t)cap * sizeof(float4)));
     HIP_TRY(hipMalloc(&w.node_lit, (size_t)cap * sizeof(uint32_t)));
+    if (w.forest) {
+        (void)hipFree(w.node_aux);
+        (void)hipFree(w.node_key);
+        (void)hipFree(w.node_pixel);
+        w.node_aux = nullptr;
+        w.node_key = nullptr;
+        w.node_pixel = nullptr;
+        HIP_TRY(hipMalloc(&w.node_aux, (size_t)cap * sizeof(float4)));
+        HIP_TRY(hipMalloc(&w.node_key, (size_t)cap * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&w.node_pixel, (size_t)cap * sizeof(uint32_t)));
+    }
     w.capacity = cap;
     return RT_OK;
+}
+
+// Frees every device / pinned buffer of a workspace.
+void free_workspace(Workspace& w) {
+    for (void* b : {(void*)w.out, (void*)w.out8, (void*)w.counters, (void*)w.work, (void*)w.tasks, (void*)w.shadow,
+                    (void*)w.nodes, (void*)w.levels, (void*)w.overflow, (void*)w.node_ps, (void*)w.node_lit,
+                    (void*)w.task_keys, (void*)w.task_vals, (void*)w.perm, (void*)w.keys_alt,
+                    (void*)w.shadow_keys, (void*)w.shadow_keys_alt, (void*)w.shadow_sorted, w.sort_tmp,
+                    (void*)w.node_aux, (void*)w.node_key, (void*)w.node_pixel})
+        if (b) (void)hipFree(b);
+    if (w.h_count) (void)hipHostFree(w.h_count);
+    w = Workspace();
 }
 
 }  // namespace
@@ -862,23 +915,8 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     if (!rt_cube_table_check(cubetri.data())) return RT_ERR_UNSUPPORTED;
     std::vector<MatRec> mats(d->n_materials);
     for (uint32_t i = 0; i < d->n_materials; i++) {
-        const rt_material& m = d->materials[i];
-        if (m.kind != RT_MAT_PHONG && m.kind != RT_MAT_TEXTURE_PHONG) return RT_ERR_INVALID_ARG;
-        const rt_texture* tx[3] = {&m.ambient, &m.diffuse, &m.specular};
-        for (int k = 0; k < 3; k++) {
-            if (tx[k]->kind != RT_TEX_CONST && tx[k]->kind != RT_TEX_CHECKERBOARD) return RT_ERR_INVALID_ARG;
-            // Phong ignores texture programs: its colours are constants (material.rs:55-65)
-            if (m.kind == RT_MAT_PHONG && tx[k]->kind != RT_TEX_CONST) return RT_ERR_INVALID_ARG;
-        }
-        MatRec& M = mats[i];
-        std::memset(&M, 0, sizeof(M));
-        M.kind = m.kind;
-        M.power = m.power;
-        M.reflectivity = m.reflectivity;
-        M.refraction_index = m.refraction_index;
-        M.ambient = TexRec{m.ambient.kind, m.ambient.color.r, m.ambient.color.g, m.ambient.color.b};
-        M.diffuse = TexRec{m.diffuse.kind, m.diffuse.color.r, m.diffuse.color.g, m.diffuse.color.b};
-        M.specular = TexRec{m.specular.kind, m.specular.color.r, m.specular.color.g, m.specular.color.b};
+        rt_status r = mat_rec(d->materials[i], mats[i]);
+        if (r != RT_OK) return r;
     }
     if (d->n_lights > 32) return RT_ERR_UNSUPPORTED;  // shadow results are a 32-bit mask per node
     uint32_t n_point = 0;
@@ -984,20 +1022,7 @@ rt_status rt_scene_destroy(rt_scene* s) {
     if (!s) return RT_ERR_INVALID_ARG;
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    if (s->ws.out) (void)hipFree(s->ws.out);
-    if (s->ws.out8) (void)hipFree(s->ws.out8);
-    if (s->ws.counters) (void)hipFree(s->ws.counters);
-    if (s->ws.work) (void)hipFree(s->ws.work);
-    if (s->ws.tasks) (void)hipFree(s->ws.tasks);
-    if (s->ws.shadow) (void)hipFree(s->ws.shadow);
-    if (s->ws.nodes) (void)hipFree(s->ws.nodes);
-    if (s->ws.levels) (void)hipFree(s->ws.levels);
-    if (s->ws.overflow) (void)hipFree(s->ws.overflow);
-    for (void* b : {(void*)s->ws.node_ps, (void*)s->ws.node_lit, (void*)s->ws.task_keys, (void*)s->ws.task_vals,
-                    (void*)s->ws.perm, (void*)s->ws.keys_alt, (void*)s->ws.shadow_keys,
-                    (void*)s->ws.shadow_keys_alt, (void*)s->ws.shadow_sorted, s->ws.sort_tmp})
-        if (b) (void)hipFree(b);
-    if (s->ws.h_count) (void)hipHostFree(s->ws.h_count);
+    free_workspace(s->ws);
     if (s->dmem) (void)hipFree(s->dmem);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -1093,9 +1118,22 @@ static rt_status launch_bands(rt_scene* s, const rt_camera* cam, uint32_t depth,
 }
 
 // Level-synchronous pipeline: trace(0..L-1), then combine(L-1..0), all on `stream`.
+// The level-synchronous pipeline into workspace `w`.  Forest builds (w.forest) write the
+// per-node shade inputs, always read the level sizes on the host, skip the combine pass
+// and leave the parameters (with the device level table) in *forest_params.
+static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
+                               uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
+                               hipStream_t stream, WaveParams* forest_params, uint32_t* forest_levels);
+
 static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
                                    uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
                                    hipStream_t stream) {
+    return wave_pipeline(s, s->ws, cam, depth, band_rows, rank, world, d_rgb, d_counters, stream, nullptr, nullptr);
+}
+
+static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
+                               uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
+                               hipStream_t stream, WaveParams* forest_params, uint32_t* forest_levels) {
     WaveParams p;
     std::memset(&p, 0, sizeof(p));
     p.S = s->S;
@@ -1121,7 +1159,6 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
     // (config 3 needs 2.7); an overflow is reported, never silently truncated
     uint64_t want = std::max<uint64_t>(total * 12u, 1u << 20);
     if (want > 0x7FFFFFFFu) want = 0x7FFFFFFFu;
-    Workspace& w = s->ws;
     if (w.capacity < want) {  // grows only (rt_render may have grown it after an overflow)
         rt_status st = grow_node_pool(w, (uint32_t)want);
         if (st != RT_OK) return st;
@@ -1189,8 +1226,8 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
             HIP_TRY(hipMalloc(&w.sort_tmp, need));
             w.sort_tmp_bytes = need;
         }
-        if (!w.h_count) HIP_TRY(hipHostMalloc((void**)&w.h_count, 16, hipHostMallocDefault));
     }
+    if ((sort_on || w.forest) && !w.h_count) HIP_TRY(hipHostMalloc((void**)&w.h_count, 16, hipHostMallocDefault));
     p.task_keys = sort_on ? w.task_keys : nullptr;
     p.task_vals = sort_on ? w.task_vals : nullptr;
     p.shadow_keys = sort_on ? w.shadow_keys : nullptr;
@@ -1207,6 +1244,11 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
     p.overflow = w.overflow;
     p.out = d_rgb;
     p.ray_counters = d_counters;
+    if (w.forest) {
+        p.node_aux = w.node_aux;
+        p.node_key = w.node_key;
+        p.node_pixel = w.node_pixel;
+    }
     if (s->occ_trace == 0) {
         int a = 0, b = 0, c = 0;
         HIP_TRY(wave_occupancy(&a, &b, &c));
@@ -1219,7 +1261,7 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
     int cb = s->num_cus * s->occ_combine;
     uint32_t levels = depth > 0 ? depth : 1;
     HIP_TRY(launch_wave_init(w.levels, 2 * (RT_MAX_DEPTH + 2), p.total_items, w.overflow, stream));
-    if (!sort_on) {
+    if (!sort_on && !w.forest) {
         for (uint32_t k = 0; k < levels; k++) HIP_TRY(launch_wave_trace(p, k, tb, stream));
         HIP_TRY(launch_wave_shadow(p, sb, stream));
         for (uint32_t k = levels; k-- > 0;) HIP_TRY(launch_wave_combine(p, k, cb, stream));
@@ -1239,7 +1281,7 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
         if (off >= w.capacity) break;  // overflowed: the flag is already set
         cnt = std::min(cnt, w.capacity - off);
         if (cnt == 0) break;
-        if (sort_tasks) {
+        if (sort_on && sort_tasks) {
             size_t bytes = w.sort_tmp_bytes;
             HIP_TRY(sort_pairs_u32(w.sort_tmp, bytes, w.task_keys + off, w.keys_alt, w.task_vals + off,
                                    w.perm + off, cnt, task_bits, stream));
@@ -1251,11 +1293,22 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
     HIP_TRY(read2(w.levels + 2 * (RT_MAX_DEPTH + 1)));
     uint32_t n_sh = std::min(w.h_count[0], w.shadow_capacity);
     if (n_sh > 0) {
-        size_t bytes = w.sort_tmp_bytes;
-        HIP_TRY(sort_pairs_u32(w.sort_tmp, bytes, w.shadow_keys, w.shadow_keys_alt, w.shadow, w.shadow_sorted, n_sh,
-                               shadow_bits, stream));
-        p.shadow_in = w.shadow_sorted;
+        if (sort_on) {
+            size_t bytes = w.sort_tmp_bytes;
+            HIP_TRY(sort_pairs_u32(w.sort_tmp, bytes, w.shadow_keys, w.shadow_keys_alt, w.shadow, w.shadow_sorted,
+                                   n_sh, shadow_bits, stream));
+            p.shadow_in = w.shadow_sorted;
+        }
         HIP_TRY(launch_wave_shadow(p, sb, stream));
+    }
+    if (w.forest) {  // no combine: the forest is shaded later, any number of times
+        HIP_TRY(hipMemcpyAsync(forest_levels, w.levels, 2 * (RT_MAX_DEPTH + 1) * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        p.perm = nullptr;
+        *forest_params = p;
+        forest_levels[2 * (RT_MAX_DEPTH + 1)] = used;
+        return RT_OK;
     }
     for (uint32_t k = used; k-- > 0;) HIP_TRY(launch_wave_combine(p, k, cb, stream));
     return RT_OK;
@@ -1331,6 +1384,206 @@ rt_status rt_render(const rt_scene* scene, const rt_camera* cam, uint32_t depth,
         HIP_TRY(hipEventElapsedTime(&ms, s->ev0, s->ev1));
         *opts->kernel_ms = ms;
     }
+    return RT_OK;
+}
+
+
+// ---------------------------------------------------------------- ray forest
+// render_tree.rs: generate_ray_forest (:147-164) keeps every intersection of every
+// pixel's ray tree; render_forest (:121-127) shades the whole forest; render_forest_filter
+// (:129-145) re-shades only trees that hold a mutated shape.  On the device the forest is
+// the level-synchronous pipeline's node pool, kept after the trace + shadow passes, plus
+// per node: material index, texture coordinates, `entering`, the shape id and the pixel.
+
+}  // extern "C"
+
+struct rt_forest {
+    rt_scene* s = nullptr;
+    rt_camera cam{};
+    uint32_t depth = 0;
+    Workspace ws;
+    WaveParams p{};
+    uint32_t levels[2 * (RT_MAX_DEPTH + 1) + 1] = {};  // (offset, count) per level, then levels used
+    uint32_t n_nodes = 0;
+    float* frame = nullptr;     // [y_res * x_res * 3] the last shade
+    uint8_t* mark = nullptr;    // [pixels] dirty / tree-holds-id marks
+    uint8_t* key_mask = nullptr;
+    uint32_t n_keys = 0;
+    uint32_t* sizes = nullptr;  // [pixels]
+    unsigned long long* counters = nullptr;  // node, shadow, pixels of the build
+};
+
+namespace {
+
+size_t forest_pixels(const rt_forest* f) { return (size_t)f->cam.x_res * f->cam.y_res; }
+
+rt_status forest_shade(rt_forest* f, const uint8_t* dirty) {
+    WaveParams p = f->p;
+    p.S = f->s->S;  // current material table
+    p.dirty = dirty;
+    int cb = f->s->num_cus * (f->s->occ_combine > 0 ? f->s->occ_combine : 1);
+    uint32_t used = f->levels[2 * (RT_MAX_DEPTH + 1)];
+    for (uint32_t k = used; k-- > 0;) HIP_TRY(launch_forest_shade(p, k, cb, f->frame, f->s->stream));
+    return RT_OK;
+}
+
+// mark[pixel] = tree holds one of `ids` (or sizes per pixel when ids == nullptr)
+rt_status forest_mark(rt_forest* f, const int32_t* ids, uint32_t n_ids, bool sizes) {
+    hipStream_t st = f->s->stream;
+    size_t px = forest_pixels(f);
+    const uint8_t* mask = nullptr;
+    if (ids) {
+        std::vector<uint8_t> h(f->n_keys, 0);
+        for (uint32_t i = 0; i < n_ids; i++)
+            if (ids[i] >= 0 && (uint32_t)ids[i] < f->n_keys) h[ids[i]] = 1;
+        HIP_TRY(hipMemcpyAsync(f->key_mask, h.data(), f->n_keys, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemsetAsync(f->mark, 0, px, st));
+        HIP_TRY(hipStreamSynchronize(st));  // h goes out of scope
+        mask = f->key_mask;
+    }
+    if (sizes) HIP_TRY(hipMemsetAsync(f->sizes, 0, px * sizeof(uint32_t), st));
+    HIP_TRY(launch_forest_mark(f->ws.node_key, f->ws.node_pixel, f->ws.nodes, f->n_nodes, mask, f->n_keys, f->mark,
+                               sizes ? f->sizes : nullptr, st));
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+rt_status rt_forest_create(rt_scene* s, const rt_camera* cam, uint32_t depth, rt_forest** out) {
+    if (!s || !cam || !out) return RT_ERR_INVALID_ARG;
+    if (cam->x_res == 0 || cam->y_res == 0) return RT_ERR_INVALID_ARG;
+    if (depth > RT_MAX_DEPTH) return RT_ERR_UNSUPPORTED;
+    if ((uint64_t)cam->x_res * cam->y_res * 3 >= (1ull << 32)) return RT_ERR_UNSUPPORTED;
+    HIP_TRY(hipSetDevice(s->device));
+    std::unique_ptr<rt_forest> f(new (std::nothrow) rt_forest());
+    if (!f) return RT_ERR_OUT_OF_MEMORY;
+    f->s = s;
+    f->cam = *cam;
+    f->depth = depth;
+    f->ws.forest = true;
+    size_t px = forest_pixels(f.get());
+    f->n_keys = std::max<uint32_t>((uint32_t)s->S.n_shapes, 12u);  // cube hits report ids 0..11
+    struct Guard {  // frees everything if creation fails half way
+        rt_forest* f;
+        ~Guard() {
+            if (!f) return;
+            free_workspace(f->ws);
+            for (void* b : {(void*)f->frame, (void*)f->mark, (void*)f->key_mask, (void*)f->sizes, (void*)f->counters})
+                if (b) (void)hipFree(b);
+        }
+    } guard{f.get()};
+    HIP_TRY(hipMalloc(&f->frame, px * 3 * sizeof(float)));
+    HIP_TRY(hipMalloc(&f->mark, px));
+    HIP_TRY(hipMalloc(&f->key_mask, f->n_keys));
+    HIP_TRY(hipMalloc(&f->sizes, px * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&f->counters, 4 * sizeof(unsigned long long)));
+    hipStream_t st = s->stream;
+    const uint32_t band_rows = 8;
+    for (int attempt = 0;; attempt++) {
+        HIP_TRY(hipMemsetAsync(f->counters, 0, 4 * sizeof(unsigned long long), st));
+        rt_status r = wave_pipeline(s, f->ws, cam, depth, band_rows, 0, 1, nullptr, f->counters, st, &f->p, f->levels);
+        if (r != RT_OK) return r;
+        uint32_t ovf = 0;
+        HIP_TRY(hipMemcpyAsync(&ovf, f->ws.overflow, sizeof(ovf), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (!ovf) break;
+        if (attempt >= 6 || f->ws.capacity >= 0x40000000u) return RT_ERR_OUT_OF_MEMORY;
+        rt_status g = grow_node_pool(f->ws, f->ws.capacity * 2u);
+        if (g != RT_OK) return g;
+    }
+    uint32_t used = f->levels[2 * (RT_MAX_DEPTH + 1)];
+    f->n_nodes = used ? f->levels[2 * (used - 1)] + f->levels[2 * (used - 1) + 1] : 0;
+    guard.f = nullptr;
+    *out = f.release();
+    return RT_OK;
+}
+
+rt_status rt_forest_destroy(rt_forest* f) {
+    if (!f) return RT_ERR_INVALID_ARG;
+    (void)hipSetDevice(f->s->device);
+    (void)hipStreamSynchronize(f->s->stream);
+    free_workspace(f->ws);
+    for (void* b : {(void*)f->frame, (void*)f->mark, (void*)f->key_mask, (void*)f->sizes, (void*)f->counters})
+        if (b) (void)hipFree(b);
+    delete f;
+    return RT_OK;
+}
+
+rt_status rt_forest_render(rt_forest* f, float* rgb) {
+    if (!f || !rgb) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(f->s->device));
+    rt_status r = forest_shade(f, nullptr);
+    if (r != RT_OK) return r;
+    HIP_TRY(hipMemcpyAsync(rgb, f->frame, forest_pixels(f) * 3 * sizeof(float), hipMemcpyDeviceToHost,
+                           f->s->stream));
+    HIP_TRY(hipStreamSynchronize(f->s->stream));
+    return RT_OK;
+}
+
+rt_status rt_forest_render_filter(rt_forest* f, const int32_t* mutated_ids, uint32_t n_ids, float* rgb) {
+    if (!f || !rgb || (n_ids && !mutated_ids)) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(f->s->device));
+    hipStream_t st = f->s->stream;
+    size_t bytes = forest_pixels(f) * 3 * sizeof(float);
+    HIP_TRY(hipMemcpyAsync(f->frame, rgb, bytes, hipMemcpyHostToDevice, st));  // untouched pixels keep these
+    rt_status r = forest_mark(f, mutated_ids, n_ids, false);
+    if (r != RT_OK) return r;
+    r = forest_shade(f, f->mark);
+    if (r != RT_OK) return r;
+    HIP_TRY(hipMemcpyAsync(rgb, f->frame, bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return RT_OK;
+}
+
+rt_status rt_forest_tree_sizes(rt_forest* f, uint32_t* sizes) {
+    if (!f || !sizes) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(f->s->device));
+    rt_status r = forest_mark(f, nullptr, 0, true);
+    if (r != RT_OK) return r;
+    HIP_TRY(hipMemcpyAsync(sizes, f->sizes, forest_pixels(f) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           f->s->stream));
+    HIP_TRY(hipStreamSynchronize(f->s->stream));
+    return RT_OK;
+}
+
+rt_status rt_forest_trees_with(rt_forest* f, int32_t shape_id, uint64_t* count) {
+    if (!f || !count) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(f->s->device));
+    rt_status r = forest_mark(f, &shape_id, 1, false);
+    if (r != RT_OK) return r;
+    std::vector<uint8_t> m(forest_pixels(f));
+    HIP_TRY(hipMemcpyAsync(m.data(), f->mark, m.size(), hipMemcpyDeviceToHost, f->s->stream));
+    HIP_TRY(hipStreamSynchronize(f->s->stream));
+    uint64_t n = 0;
+    for (uint8_t v : m) n += v;
+    *count = n;
+    return RT_OK;
+}
+
+rt_status rt_forest_counters(const rt_forest* f, rt_counters* out) {
+    if (!f || !out) return RT_ERR_INVALID_ARG;
+    unsigned long long h[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpy(h, f->counters, sizeof(h), hipMemcpyDeviceToHost));
+    out->node_rays = h[0];
+    out->shadow_rays = h[1];
+    out->pixels = h[2];
+    out->wave_iterations = 0;
+    return RT_OK;
+}
+
+rt_status rt_scene_set_material(rt_scene* s, uint32_t index, const rt_material* m) {
+    if (!s || !m || index >= (uint32_t)s->S.n_mats) return RT_ERR_INVALID_ARG;
+    MatRec cur;
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    HIP_TRY(hipMemcpy(&cur, s->S.mats + index, sizeof(cur), hipMemcpyDeviceToHost));
+    if (m->kind != cur.kind) return RT_ERR_INVALID_ARG;  // the same kind, as the GUI's edits
+    MatRec M;
+    rt_status r = mat_rec(*m, M);
+    if (r != RT_OK) return r;
+    HIP_TRY(hipMemcpy(const_cast<MatRec*>(s->S.mats) + index, &M, sizeof(M), hipMemcpyHostToDevice));
     return RT_OK;
 }
 

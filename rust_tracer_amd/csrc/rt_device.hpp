@@ -130,7 +130,7 @@ struct RenderParams {
 struct Task {
     float ox, oy, oz, dx, dy, dz;
     uint32_t parent;   // (node index << 1) | slot  (slot 0 = reflected, 1 = refracted)
-    uint32_t pad;
+    uint32_t pixel;    // y * width + x of the tree's pixel (ray forest)
 };
 
 // One traced tree node: the shading inputs of render.rs:57-68 (lights are summed later,
@@ -183,6 +183,11 @@ struct WaveParams {
     uint32_t key_mode;                 // task key variant (A/B)
     uint32_t light_shift;              // shadow key = (light << light_shift) | (Morton >> (15 - light_shift))
     uint32_t count_mask;               // bit 0: trace kernels add to scan_ops, bit 1: shadow kernel
+    // ray forest (render_tree.rs; set only when building an rt_forest): per node
+    float4* node_aux;                  // {material index bits, tex u, tex v, entering bits}
+    uint32_t* node_key;                // shape id as the reference records it (cube: inner triangle)
+    uint32_t* node_pixel;              // y * width + x of the tree's pixel
+    const uint8_t* dirty;              // forest shade: per-pixel mask (null: every pixel)
 };
 
 // 15-bit Morton code of a point in the 32^3 grid over [c - r, c + r]^3 (clamped)

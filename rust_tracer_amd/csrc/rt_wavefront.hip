@@ -21,6 +21,7 @@
 // critical-path bound.  Here every queue entry costs one scan, lanes stay full, and the
 // post-order combine keeps the reference's exact operation order (pixel values reach
 // |4000| in config 3, so a reassociated "throughput" formulation would break 1e-4).
+#include <algorithm>
 #include <type_traits>
 
 #include "rt_common.hpp"
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         const uint32_t t = base + lane;
         bool active = t < count;
         V3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
-        uint32_t parent = 0;
+        uint32_t parent = 0, pix = 0;
         const uint32_t n = off + t;
         if (active) {
             if (level == 0) {
@@ -191,6 +192,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                     active = false;
                 } else {
                     n_pix++;
+                    pix = px.v * P.width + px.u;
                     if (P.depth == 0) {  // trace_ray(.., 0) == BLACK, no scan
                         P.nodes[n].flags = NODE_MISS;
                         active = false;
@@ -207,6 +209,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 ro = v3(T.ox, T.oy, T.oz);
                 rd = v3(T.dx, T.dy, T.dz);
                 parent = T.parent;
+                pix = T.pixel;
             }
         }
         bool want_refl = false, want_refr = false, hit = false;
@@ -247,6 +250,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 P.node_lit[n] = 0u;
                 rec.parent = parent;
                 rec.pad[0] = rec.pad[1] = rec.pad[2] = 0u;
+                if (P.node_aux) {  // ray forest: what render_ray_tree re-reads at shade time
+                    P.node_aux[n] = make_float4(__uint_as_float((uint32_t)h.mat), h.tu, h.tv,
+                                                __uint_as_float(h.entering ? 1u : 0u));
+                    uint32_t shape = bk >> 4;
+                    P.node_key[n] = (S.shapes[shape].kind == RT_SHAPE_CUBE) ? (bk & 15u) : shape;
+                    P.node_pixel[n] = pix;
+                }
                 bool child_ok = level + 1 < P.depth;
                 if (M.reflectivity > RT_EPS) {  // render.rs:70-84, reflect_ray :105-110
                     rec.flags |= F_REFL;
@@ -278,6 +288,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                         rec.flags |= F_TIR;
                     }
                 }
+                if (P.node_aux) {  // children's directions arrive here (0: no / missed child)
+                    rec.kdx = rec.kdy = rec.kdz = 0.f;
+                    rec.ksx = rec.ksy = rec.ksz = 0.f;
+                }
                 P.nodes[n] = rec;
             }
         }
@@ -287,7 +301,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         if (want_refl) {
             uint32_t slot = next_off + my;
             if (slot < P.capacity) {
-                Task T = {rro.x, rro.y, rro.z, rrd.x, rrd.y, rrd.z, (n << 1) | 0u, 0u};
+                Task T = {rro.x, rro.y, rro.z, rrd.x, rrd.y, rrd.z, (n << 1) | 0u, pix};
                 P.tasks[slot] = T;
                 if (P.task_keys) {
                     P.task_keys[slot] = task_key(P, rro, rrd);
@@ -301,7 +315,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         if (want_refr) {
             uint32_t slot = next_off + my;
             if (slot < P.capacity) {
-                Task T = {tro.x, tro.y, tro.z, trd.x, trd.y, trd.z, (n << 1) | 1u, 0u};
+                Task T = {tro.x, tro.y, tro.z, trd.x, trd.y, trd.z, (n << 1) | 1u, pix};
                 P.tasks[slot] = T;
                 if (P.task_keys) {
                     P.task_keys[slot] = task_key(P, tro, trd);
@@ -464,6 +478,115 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
     }
 }
 
+// ---------------------------------------------------------------- ray forest
+// render_ray_tree (render_tree.rs:214-255) for every node of `level`, bottom-up like the
+// combine pass but with the forest's own shading, from the CURRENT materials (a material
+// edited since the build shows up, as through the reference's RefCell):
+//   n1, n2        from the material's refraction index and the hit's `entering`
+//   lights        sum over lights of fresnel(ldir) * reflected_energy(E, ldir)  (as render.rs)
+//   reflected     fresnel(dir_r) * reflected_energy(E_r, eye_dir)   -- eye_dir as light dir
+//   refracted     (1 - fresnel(dir_t, -n)) * E_t                     -- no diffuse factor
+//   colour        ((ambient + lights) + reflected) + refracted, reported with dir = -eye_dir
+// (E, dir) of a missing or missed child = (BLACK, 0): its slots were zeroed at build time.
+// dirty != null: only nodes of marked pixels are shaded (render_forest_filter).
+__global__ __launch_bounds__(256) void forest_shade_level_kernel(WaveParams P, uint32_t level, float* frame) {
+    const DevScene& S = P.S;
+    const uint32_t off = P.levels[2 * level];
+    const uint32_t count = min(P.levels[2 * level + 1], off < P.capacity ? P.capacity - off : 0u);
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < count; t += stride) {
+        const uint32_t n = off + t;
+        const NodeRec& R = P.nodes[n];
+        const uint32_t flags = R.flags;
+        if (flags & NODE_NONE) continue;
+        if (!(flags & NODE_HIT)) {  // RayTreeNode::None: (BLACK, 0)
+            if (level == 0) {
+                PixelRef px = pixel_of(P, t);
+                uint32_t pix = px.v * P.width + px.u;
+                if (!P.dirty || P.dirty[pix]) {
+                    float* o = frame + (size_t)pix * 3u;
+                    o[0] = 0.f;
+                    o[1] = 0.f;
+                    o[2] = 0.f;
+                }
+            }
+            continue;
+        }
+        const uint32_t pix = P.node_pixel[n];
+        if (P.dirty && !P.dirty[pix]) continue;
+        const float4 aux = P.node_aux[n];
+        const MatRec& M = S.mats[__float_as_uint(aux.x)];
+        Hit h;
+        h.n = v3(R.nx, R.ny, R.nz);
+        h.eye = v3(R.ex, R.ey, R.ez);
+        h.tu = aux.y;
+        h.tv = aux.z;
+        const bool entering = __float_as_uint(aux.w) != 0u;
+        const float ri = M.refraction_index;
+        const float n1 = entering ? 1.f : ri;
+        const float n2 = entering ? ri : 1.f;
+        const V3 kd = tex_eval(M.diffuse, h.tu, h.tv), ks = tex_eval(M.specular, h.tu, h.tv);
+        V3 ps = v3(R.psx, R.psy, R.psz);
+        V3 lsum = v3(0.f, 0.f, 0.f);
+        const uint32_t litmask = P.node_lit[n];
+        for (int li = 0; li < S.n_lights; ++li) {
+            const LightRec& L = S.lights[li];
+            V3 ldir = v3(0.f, 0.f, 0.f);
+            V3 E = v3(L.r, L.g, L.b);
+            if (L.kind == RT_LIGHT_POINT) {
+                ldir = norm(sub(v3(L.px, L.py, L.pz), ps));
+                if (!((litmask >> li) & 1u)) E = v3(0.f, 0.f, 0.f);
+            }
+            float f = fresnel_reflection(ldir, h.n, n1, n2);
+            V3 g = reflected_energy(E, ldir, h, kd, ks, M.power);
+            lsum = add(lsum, v3(f * g.x, f * g.y, f * g.z));
+        }
+        const V3 er = v3(R.erx, R.ery, R.erz), dr = v3(R.kdx, R.kdy, R.kdz);
+        const V3 et = v3(R.etx, R.ety, R.etz), dt = v3(R.ksx, R.ksy, R.ksz);
+        float fr = fresnel_reflection(dr, h.n, n1, n2);
+        V3 gr = reflected_energy(er, h.eye, h, kd, ks, M.power);
+        V3 refl = v3(fr * gr.x, fr * gr.y, fr * gr.z);
+        float ft = 1.f - fresnel_reflection(dt, neg(h.n), n1, n2);
+        V3 refr = v3(ft * et.x, ft * et.y, ft * et.z);
+        V3 ka = tex_eval(M.ambient, h.tu, h.tv);
+        V3 amb = v3(ka.x * S.amb_r, ka.y * S.amb_g, ka.z * S.amb_b);
+        V3 c = add(add(add(amb, lsum), refl), refr);
+        if (level == 0) {
+            float* o = frame + (size_t)pix * 3u;
+            o[0] = c.x;
+            o[1] = c.y;
+            o[2] = c.z;
+        } else {
+            NodeRec& Q = P.nodes[R.parent >> 1];
+            V3 d = neg(h.eye);
+            if (R.parent & 1u) {
+                Q.etx = c.x; Q.ety = c.y; Q.etz = c.z;
+                Q.ksx = d.x; Q.ksy = d.y; Q.ksz = d.z;
+            } else {
+                Q.erx = c.x; Q.ery = c.y; Q.erz = c.z;
+                Q.kdx = d.x; Q.kdy = d.y; Q.kdz = d.z;
+            }
+        }
+    }
+}
+
+// mark[pixel] = 1 for every pixel whose tree holds a node with key_mask[id] set
+// (render_forest_filter's shapes ∩ mutated, render_tree.rs:138-140); also counts the
+// hit nodes per pixel when sizes != null (RayTree::size, :39-48)
+__global__ void forest_mark_kernel(const uint32_t* node_key, const uint32_t* node_pixel, const NodeRec* nodes,
+                                   uint32_t n_nodes, const uint8_t* key_mask, uint32_t n_keys, uint8_t* mark,
+                                   uint32_t* sizes) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_nodes; i += gridDim.x * blockDim.x) {
+        if (!(nodes[i].flags & NODE_HIT)) continue;
+        uint32_t pix = node_pixel[i];
+        if (sizes) atomicAdd(&sizes[pix], 1u);
+        if (key_mask) {
+            uint32_t k = node_key[i];
+            if (k < n_keys && key_mask[k]) mark[pix] = 1;
+        }
+    }
+}
+
 // levels[] = {0, total_items, 0, ...} (incl. the shadow count), overflow 0
 __global__ void wave_init_kernel(uint32_t* levels, uint32_t n_words, uint32_t total_items, uint32_t* overflow) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -507,6 +630,21 @@ hipError_t launch_wave_shadow(const WaveParams& p, int blocks, hipStream_t strea
         hipLaunchKernelGGL((shadow_kernel<false, true>), dim3(blocks), dim3(256), 0, stream, p);
     else
         hipLaunchKernelGGL((shadow_kernel<false, false>), dim3(blocks), dim3(256), 0, stream, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_forest_shade(const WaveParams& p, uint32_t level, int blocks, float* frame, hipStream_t stream) {
+    hipLaunchKernelGGL(forest_shade_level_kernel, dim3(blocks), dim3(256), 0, stream, p, level, frame);
+    return hipGetLastError();
+}
+
+hipError_t launch_forest_mark(const uint32_t* node_key, const uint32_t* node_pixel, const NodeRec* nodes,
+                              uint32_t n_nodes, const uint8_t* key_mask, uint32_t n_keys, uint8_t* mark,
+                              uint32_t* sizes, hipStream_t stream) {
+    if (n_nodes == 0) return hipSuccess;
+    uint32_t blocks = std::min<uint32_t>((n_nodes + 255) / 256, 4096u);
+    hipLaunchKernelGGL(forest_mark_kernel, dim3(blocks), dim3(256), 0, stream, node_key, node_pixel, nodes, n_nodes,
+                       key_mask, n_keys, mark, sizes);
     return hipGetLastError();
 }
 
