@@ -183,6 +183,10 @@ rt_status rt_unpermute_bands_async(const float* d_gathered, uint32_t x_res, uint
                                    uint32_t band_rows, uint32_t world, float* d_frame,
                                    void* stream);
 
+/* Saves a row-major RGB8 frame (Color::as_u8 values) as PNG, BMP or PPM, chosen by the
+ * file extension (.png default) -- bmp.rs:8-19 / main.rs:71-74 (host code). */
+rt_status rt_write_image(const char* path, const uint8_t* rgb8, uint32_t x_res, uint32_t y_res);
+
 /* Color::as_u8 (color.rs:43-46) of a row-major float frame, on the device. */
 rt_status rt_quantize_u8_async(const float* d_rgb, size_t n_values, uint8_t* d_rgb8,
                                void* stream);

@@ -373,6 +373,13 @@ class DeviceForest:
                 "p95": at(0.95), "p99": at(0.99)}
 
 
+def write_image(path, rgb8):
+    """rt_write_image: save an RGB8 frame [y, x, 3] as .png / .bmp / .ppm (host code)."""
+    rgb8 = np.ascontiguousarray(rgb8, np.uint8)
+    check(lib().rt_write_image(str(path).encode(), rgb8.ctypes.data_as(C.POINTER(C.c_uint8)),
+                               rgb8.shape[1], rgb8.shape[0]), "rt_write_image")
+
+
 def band_rows_per_rank(y_res, band_rows, world):
     return int(lib().rt_band_rows_per_rank(y_res, band_rows, world))
 

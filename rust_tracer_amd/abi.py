@@ -139,6 +139,7 @@ def lib():
     L.rt_forest_trees_with.argtypes = [vp, C.c_int32, P(C.c_uint64)]
     L.rt_forest_counters.argtypes = [vp, P(rt_counters)]
     L.rt_scene_set_material.argtypes = [vp, C.c_uint32, P(rt_material)]
+    L.rt_write_image.argtypes = [C.c_char_p, P(C.c_uint8), C.c_uint32, C.c_uint32]
     L.rt_scene_uses_bvh.argtypes = [vp]
     L.rt_scene_uses_bvh.restype = C.c_int32
     L.rt_status_str.argtypes = [C.c_int32]

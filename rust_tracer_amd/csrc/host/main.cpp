@@ -1,19 +1,24 @@
 // main.cpp -- `rust_tracer` command line front-end over the C ABI.
 //
-// The subset of the reference CLI (src/cli.rs:34-118, src/main.rs:27-261) that drives
-// the render path:
-//   rust_tracer [-w W] [-h H] [-d D] [--scene my_scene|bench128|synth2|synth3]
-//               [--device N] [--out FILE.bmp|.ppm]
-//   rust_tracer [...] bench [-n RUNS]
-// Normal mode renders once and writes the image (bmp.rs:8-19 writes RGB8 from
-// Color::as_u8); bench mode repeats render_scene_basic RUNS times and prints the same
-// "Total Time" / "Avg Per Op" lines as main.rs:137-151.  Timing covers the render call
-// (scene upload excluded, as in main.rs:250-253).
+// The reference CLI (src/cli.rs:34-175) and its modes (src/main.rs:27-291), minus the GTK
+// GUI and the terminal preview:
+//   rust_tracer [-w W] [-h H] [-d D] [--method basic|rayforest] [--stats] [-i]
+//               [--scene my_scene|bench128|synth2|synth3] [--device N] [--out FILE]
+//   rust_tracer [...] bench [-n RUNS] [-f]
+// Normal mode renders once and saves ./output/<unix seconds>.png (main.rs:71-74,
+// bmp.rs:8-19: RGB8 from Color::as_u8), or --out FILE (.png, .bmp or .ppm).  With
+// --method rayforest it builds the forest, optionally prints RayForest::stats
+// (main.rs:88-103) and saves render_forest's image.  Bench mode prints the same
+// "Total Time" / "Avg Per Op" lines as main.rs:137-219: RUNS renders, RUNS forest shades,
+// or with -f RUNS render_forest_filter calls for the shape named "blue".
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <string>
+#include <sys/stat.h>
 #include <vector>
 
 #include "scene.hpp"
@@ -22,52 +27,42 @@ using namespace rust_tracer;
 
 namespace {
 
-bool write_bmp(const std::string& path, const std::vector<uint8_t>& rgb, uint32_t w, uint32_t h) {
-    FILE* f = std::fopen(path.c_str(), "wb");
-    if (!f) return false;
-    uint32_t row = (w * 3 + 3) & ~3u;
-    uint32_t size = 54 + row * h;
-    uint8_t hdr[54] = {'B', 'M'};
-    auto put32 = [&](int off, uint32_t v) {
-        for (int i = 0; i < 4; i++) hdr[off + i] = (uint8_t)(v >> (8 * i));
-    };
-    put32(2, size);
-    put32(10, 54);
-    put32(14, 40);
-    put32(18, w);
-    put32(22, h);
-    hdr[26] = 1;
-    hdr[28] = 24;
-    put32(34, row * h);
-    std::fwrite(hdr, 1, 54, f);
-    std::vector<uint8_t> line(row, 0);
-    for (uint32_t y = 0; y < h; y++) {
-        uint32_t v = h - 1 - y;  // bottom-up
-        for (uint32_t u = 0; u < w; u++) {
-            const uint8_t* p = &rgb[((size_t)v * w + u) * 3];
-            line[u * 3 + 0] = p[2];
-            line[u * 3 + 1] = p[1];
-            line[u * 3 + 2] = p[0];
-        }
-        std::fwrite(line.data(), 1, row, f);
-    }
-    std::fclose(f);
-    return true;
+typedef std::chrono::steady_clock Clock;
+
+long long ms_since(Clock::time_point t0) {
+    return (long long)std::chrono::duration_cast<std::chrono::milliseconds>(Clock::now() - t0).count();
 }
 
-bool write_ppm(const std::string& path, const std::vector<uint8_t>& rgb, uint32_t w, uint32_t h) {
-    FILE* f = std::fopen(path.c_str(), "wb");
-    if (!f) return false;
-    std::fprintf(f, "P6\n%u %u\n255\n", w, h);
-    std::fwrite(rgb.data(), 1, rgb.size(), f);
-    std::fclose(f);
-    return true;
+bool save(const std::string& path, const std::vector<uint8_t>& rgb8, uint32_t w, uint32_t h) {
+    return rt_write_image(path.c_str(), rgb8.data(), w, h) == RT_OK;
+}
+
+// Color::as_u8 (color.rs:43-46) on the host for the forest path's float frames
+void as_u8(const std::vector<float>& rgb, std::vector<uint8_t>& out) {
+    out.resize(rgb.size());
+    for (size_t i = 0; i < rgb.size(); i++) {
+        float x = 255.f * rgb[i];
+        out[i] = x >= 255.f ? 255 : (x > 0.f ? (uint8_t)x : 0);  // `as u8` saturates, NaN -> 0
+    }
+}
+
+void enter_to_proceed() {  // main.rs:125-131
+    std::printf("Enter To Proceed: ");
+    std::fflush(stdout);
+    char buf[256];
+    if (!std::fgets(buf, sizeof buf, stdin)) return;
 }
 
 void usage() {
     std::fprintf(stderr,
-                 "usage: rust_tracer [-w W] [-h H] [-d D] [--scene my_scene|bench128|synth2|synth3]\n"
-                 "                   [--device N] [--out FILE] [bench [-n RUNS]]\n");
+                 "usage: rust_tracer [-w W] [-h H] [-d D] [--method basic|rayforest] [--stats] [-i]\n"
+                 "                   [--scene my_scene|bench128|synth2|synth3] [--device N] [--out FILE]\n"
+                 "                   [bench [-n RUNS] [-f]]\n");
+}
+
+int fail(const char* what, rt_status st) {
+    std::fprintf(stderr, "%s: %s\n", what, rt_status_str(st));
+    return 1;
 }
 
 }  // namespace
@@ -75,7 +70,7 @@ void usage() {
 int main(int argc, char** argv) {
     uint32_t w = 512, h = 512, depth = 8;  // cli.rs defaults
     int device = -1, runs = 10;
-    bool bench = false;
+    bool bench = false, forest_method = false, stats = false, interactive = false, filter = false;
     std::string scene_name = "my_scene", out;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
@@ -92,12 +87,18 @@ int main(int argc, char** argv) {
         else if (a == "--scene") scene_name = next();
         else if (a == "--device") device = std::atoi(next());
         else if (a == "--out") out = next();
+        else if (a == "--stats") stats = true;
+        else if (a == "-i" || a == "--interactive") interactive = true;
         else if (a == "bench") bench = true;
         else if (a == "-n" || a == "--runs") runs = std::atoi(next());
+        else if (a == "-f" || a == "--filter") filter = true;
         else if (a == "--method") {
             std::string m = next();
-            if (m != "basic") {
-                std::fprintf(stderr, "--method %s: only the basic renderer is on the device path\n", m.c_str());
+            for (auto& ch : m) ch = (char)std::tolower(ch);
+            if (m == "rayforest") forest_method = true;
+            else if (m == "basic") forest_method = false;
+            else {
+                std::fprintf(stderr, "Unexpected value provided for `--method`: %s\n", m.c_str());  // cli.rs:150
                 return 2;
             }
         } else {
@@ -105,6 +106,11 @@ int main(int argc, char** argv) {
             return 2;
         }
     }
+    std::printf("Rendering configuration: Config { width: %u, height: %u, depth: %u, method: %s, interactive: %s, "
+                "subcommand: %s, print_forest_stats: %s }\n",
+                w, h, depth, forest_method ? "RayForest" : "Basic", interactive ? "true" : "false",
+                bench ? "Benchmark" : "Normal", stats ? "true" : "false");
+    std::printf("Create Scene\n");
     Scene scene;
     if (scene_name == "my_scene") create_scene(scene);
     else if (scene_name == "bench128") create_bench_128_scene(scene);
@@ -116,51 +122,129 @@ int main(int argc, char** argv) {
         usage();
         return 2;
     }
-    std::printf("Rendering configuration: w=%u h=%u depth=%u scene=%s\n", w, h, depth, scene_name.c_str());
+    std::printf("Done Creating Scene\n");
 
     auto flat = scene.flatten();
     rt_scene* s = nullptr;
     rt_status st = rt_scene_create(&flat->desc, device, &s);
-    if (st != RT_OK) {
-        std::fprintf(stderr, "rt_scene_create: %s\n", rt_status_str(st));
-        return 1;
-    }
+    if (st != RT_OK) return fail("rt_scene_create", st);
     Camera cam(w, h);
     rt_camera c = cam.to_c();
     std::vector<float> rgb((size_t)w * h * 3);
     std::vector<uint8_t> rgb8((size_t)w * h * 3);
-    rt_counters cnt;
-    float kms = 0.f;
-    rt_render_opts opts{device, &cnt, &kms};
-    int n = bench ? runs : 1;
-    auto t0 = std::chrono::steady_clock::now();
-    for (int k = 0; k < n; k++) {
-        auto r0 = std::chrono::steady_clock::now();
-        st = rt_render(s, &c, depth, &opts, rgb.data(), rgb8.data());
-        if (st != RT_OK) {
-            std::fprintf(stderr, "rt_render: %s\n", rt_status_str(st));
-            return 1;
+    if (out.empty() && !bench) {  // main.rs:71-74: ./output/<unix seconds>.png
+        ::mkdir("./output", 0755);
+        out = "./output/" + std::to_string((long long)std::time(nullptr)) + ".png";
+    }
+    if (interactive && !bench) enter_to_proceed();
+
+    if (!forest_method) {
+        rt_counters cnt;
+        float kms = 0.f;
+        rt_render_opts opts{device, &cnt, &kms};
+        int n = bench ? runs : 1;
+        auto t0 = Clock::now();
+        for (int k = 0; k < n; k++) {
+            auto r0 = Clock::now();
+            st = rt_render(s, &c, depth, &opts, rgb.data(), rgb8.data());
+            if (st != RT_OK) return fail("rt_render", st);
+            std::printf("render_scene: %lldms\n", ms_since(r0));  // main.rs:250-253
         }
-        auto r1 = std::chrono::steady_clock::now();
-        std::printf("render_scene: %lldms (kernel %.3f ms)\n",
-                    (long long)std::chrono::duration_cast<std::chrono::milliseconds>(r1 - r0).count(), kms);
+        long long ns = (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
+        if (bench) {
+            std::printf("Total Time: %lldms | %lldns\n", ns / 1000000, ns);
+            std::printf("Avg Per Op: %gms | %gns\n", (double)(ns / 1000000) / n, (double)ns / n);
+        }
+        std::printf("rays: node %llu shadow %llu pixels %llu (kernel %.3f ms)\n", (unsigned long long)cnt.node_rays,
+                    (unsigned long long)cnt.shadow_rays, (unsigned long long)cnt.pixels, kms);
+    } else {
+        if (bench) std::printf("This will benchmark evaluating the complete forest\n");
+        std::printf("Rendering in RayForest Mode\nGenerate Forest\n");
+        auto g0 = Clock::now();
+        rt_forest* f = nullptr;
+        st = rt_forest_create(s, &c, depth, &f);
+        if (st != RT_OK) return fail("rt_forest_create", st);
+        std::printf("generate_forest: %lldms\nDone Generating Forest\n", ms_since(g0));
+        if (stats && !bench) {  // main.rs:88-103, render_tree.rs:73-93
+            std::vector<uint32_t> sizes((size_t)w * h);
+            st = rt_forest_tree_sizes(f, sizes.data());
+            if (st != RT_OK) return fail("rt_forest_tree_sizes", st);
+            std::vector<uint32_t> sorted(sizes);
+            std::sort(sorted.begin(), sorted.end());
+            size_t n = sorted.size();
+            unsigned long long total = 0;
+            for (uint32_t v : sorted) total += v;
+            auto at = [&](float q) { return sorted[(size_t)(q * (float)n)]; };
+            std::printf("Number of Trees: %zu\n", n);
+            std::printf("Min Tree Size: %u\n", sorted.front());
+            std::printf("Max Tree Size: %u\n", sorted.back());
+            std::printf("Median Size: %u\n", sorted[n / 2]);
+            std::printf("p90 Size: %u\n", at(0.9f));
+            std::printf("p95 Size: %u\n", at(0.95f));
+            std::printf("p99 Size: %u\n", at(0.99f));
+            std::printf("Number of Intersections: %llu\n", total);
+            std::printf("Number of Shapes: %zu\n", scene.size());
+            std::printf("Number of Intersection Tests: %llu\n", (unsigned long long)scene.size() * total);
+        }
+        if (interactive && !bench) enter_to_proceed();
+        if (!bench) {
+            auto r0 = Clock::now();
+            st = rt_forest_render(f, rgb.data());
+            if (st != RT_OK) return fail("rt_forest_render", st);
+            as_u8(rgb, rgb8);
+            if (!save(out, rgb8, w, h)) {
+                std::fprintf(stderr, "cannot write %s\n", out.c_str());
+                return 1;
+            }
+            std::printf("render_forest_to_file: %lldms\n", ms_since(r0));
+        } else {
+            long long ns = 0;
+            if (!filter) {
+                std::printf("Render full forest\n");
+                auto t0 = Clock::now();
+                for (int k = 0; k < runs; k++) {
+                    auto r0 = Clock::now();
+                    st = rt_forest_render(f, rgb.data());
+                    if (st != RT_OK) return fail("rt_forest_render", st);
+                    std::printf("render_forest: %lldms\n", ms_since(r0));
+                }
+                ns = (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
+            } else {
+                std::printf("Render partial forest\n");
+                const Shape* blue = scene.find_shape("blue");
+                if (!blue) {
+                    std::fprintf(stderr, "no shape named \"blue\" in this scene\n");
+                    return 1;
+                }
+                int32_t id = blue->id;
+                std::vector<float> buffer((size_t)w * h * 3, 0.f);  // RenderBuffer::new
+                auto t0 = Clock::now();
+                for (int k = 0; k < runs; k++) {
+                    st = rt_forest_render_filter(f, &id, 1, buffer.data());
+                    if (st != RT_OK) return fail("rt_forest_render_filter", st);
+                }
+                ns = (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
+                uint64_t with = 0;
+                st = rt_forest_trees_with(f, id, &with);
+                if (st != RT_OK) return fail("rt_forest_trees_with", st);
+                size_t trees = (size_t)w * h;
+                std::printf("Forest Size: %zu\n", trees);
+                std::printf("Trees Evaluated: %llu\n", (unsigned long long)with);
+                std::printf("%% evaluated: %g\n", 100.f * (float)with / (float)trees);
+            }
+            std::printf("Total Time: %lldms | %lldns\n", ns / 1000000, ns);
+            std::printf("Avg Per Op: %gms | %gns\n", (double)(ns / 1000000) / runs, (double)ns / runs);
+        }
+        rt_forest_destroy(f);
+        rt_scene_destroy(s);
+        return 0;
     }
-    auto t1 = std::chrono::steady_clock::now();
-    if (bench) {
-        long long ns = (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
-        std::printf("Total Time: %lldms | %lldns\n", ns / 1000000, ns);
-        std::printf("Avg Per Op: %gms | %gns\n", (double)ns / 1e6 / n, (double)ns / n);
-    }
-    std::printf("rays: node %llu shadow %llu pixels %llu\n", (unsigned long long)cnt.node_rays,
-                (unsigned long long)cnt.shadow_rays, (unsigned long long)cnt.pixels);
-    if (!out.empty()) {
-        bool ok = out.size() > 4 && out.substr(out.size() - 4) == ".ppm" ? write_ppm(out, rgb8, w, h)
-                                                                          : write_bmp(out, rgb8, w, h);
-        if (!ok) {
+    if (!bench || !out.empty()) {
+        if (!out.empty() && !save(out, rgb8, w, h)) {
             std::fprintf(stderr, "cannot write %s\n", out.c_str());
             return 1;
         }
-        std::printf("wrote %s\n", out.c_str());
+        if (!out.empty()) std::printf("wrote %s\n", out.c_str());
     }
     rt_scene_destroy(s);
     return 0;

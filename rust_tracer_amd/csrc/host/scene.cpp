@@ -157,6 +157,12 @@ void Scene::add_shape(Shape s) {
     shapes_.push_back(std::move(s));
 }
 
+size_t Scene::size() const {
+    size_t n = 0;
+    for (const Shape& s : shapes_) n += s.kind == RT_SHAPE_CUBE ? 12u : 1u;
+    return n;
+}
+
 const Shape* Scene::find_shape(const std::string& name) const {
     for (const auto& s : shapes_)
         if (s.name == name) return &s;

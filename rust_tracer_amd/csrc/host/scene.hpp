@@ -119,6 +119,8 @@ public:
     const std::vector<Shape>& shapes() const { return shapes_; }
     const std::vector<Light>& lights() const { return lights_; }
     const Shape* find_shape(const std::string& name) const;
+    // Renderable::size (mod.rs:124-126): a cube counts its 12 triangles (cube.rs:113-115)
+    size_t size() const;
 
     // Flatten into the C-ABI description (materials de-duplicated by identity, shapes and
     // lights in insertion order).  The returned holder owns every array it points at.
