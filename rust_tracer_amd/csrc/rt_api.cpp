@@ -1293,7 +1293,8 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     HIP_TRY(read2(w.levels + 2 * (RT_MAX_DEPTH + 1)));
     uint32_t n_sh = std::min(w.h_count[0], w.shadow_capacity);
     if (n_sh > 0) {
-        if (sort_on) {
+        const char* ss = std::getenv("RT_SORT_SHADOW");  // "0": keep production order (A/B)
+        if (sort_on && !(ss && ss[0] == '0')) {
             size_t bytes = w.sort_tmp_bytes;
             HIP_TRY(sort_pairs_u32(w.sort_tmp, bytes, w.shadow_keys, w.shadow_keys_alt, w.shadow, w.shadow_sorted,
                                    n_sh, shadow_bits, stream));

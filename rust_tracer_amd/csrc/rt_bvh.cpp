@@ -3,14 +3,27 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <limits>
 
 namespace rtbvh {
 namespace {
 
 constexpr int BINS = 16;
-constexpr double C_NODE = 40.0;      // one 2-wide child-box test per visited node
-constexpr size_t MAX_LEAF = 8;
+// SAH cost of one visited node and the largest leaf.  The node cost is not the child-box
+// test's ~30 VALU: a visit is a dependent scalar load, ballots, a branch and an LDS stack
+// operation for the whole wave, while leaf tests are straight-line packed arithmetic.
+// Measured (config 3, 1080p, ms/frame): node cost 40 / leaves <= 8: 7.88; 80: 7.20;
+// 120 / 16: 6.98; 200 / 16: 6.76; 200 / 32: 6.73; 300 / 32: 6.78; 500 / 64: 7.09.
+// RT_BVH_CNODE / RT_BVH_MAXLEAF override them (A/B measurements).
+double c_node() {
+    const char* e = std::getenv("RT_BVH_CNODE");
+    return e ? std::atof(e) : 200.0;
+}
+size_t max_leaf() {
+    const char* e = std::getenv("RT_BVH_MAXLEAF");
+    return e ? (size_t)std::atoi(e) : 32;
+}
 
 struct Box {
     double lo[3], hi[3];
@@ -57,6 +70,8 @@ struct Cost {
 };
 
 struct Builder {
+    const double C_NODE_V = c_node();
+    const size_t MAX_LEAF_V = max_leaf();
     const std::vector<Prim>& P;
     Tree& T;
     std::vector<double> cen;  // 3 per prim
@@ -116,7 +131,7 @@ struct Builder {
                 left.grow(bb[b]);
                 lc.add(bc[b]);
                 if (left.empty() || right[b + 1].empty()) continue;
-                double cost = C_NODE + (left.area() * lc.value() + right[b + 1].area() * rc[b + 1]) / parea;
+                double cost = C_NODE_V + (left.area() * lc.value() + right[b + 1].area() * rc[b + 1]) / parea;
                 if (cost < best) {
                     best = cost;
                     best_axis = ax;
@@ -125,7 +140,7 @@ struct Builder {
             }
         }
         if (depth >= MAX_DEPTH) return make_leaf(std::move(idx));  // depth cap: one big leaf
-        bool force = idx.size() > MAX_LEAF;
+        bool force = idx.size() > MAX_LEAF_V;
         if (!force && !(best < leaf_cost)) return make_leaf(std::move(idx));
         std::vector<uint32_t> L, R;
         int axis = best_axis;
