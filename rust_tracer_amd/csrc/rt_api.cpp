@@ -40,9 +40,10 @@ hipError_t launch_forest_shade(const WaveParams& p, uint32_t level, int blocks, 
 hipError_t launch_forest_mark(const uint32_t* node_key, const uint32_t* node_pixel, const NodeRec* nodes,
                               uint32_t n_nodes, const uint8_t* key_mask, uint32_t n_keys, uint8_t* mark,
                               uint32_t* sizes, hipStream_t stream);
-hipError_t sort_pairs_u32(void* tmp, size_t& bytes, const uint32_t* keys_in, uint32_t* keys_out,
-                          const uint32_t* vals_in, uint32_t* vals_out, uint32_t n, int end_bit,
-                          hipStream_t stream);
+hipError_t launch_sort16(const uint32_t* levels, int32_t level, uint32_t cap, const uint32_t* keys,
+                         const uint32_t* vals, uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t* vals_out,
+                         uint32_t* tile_counts, uint32_t* digit_totals, int blocks, hipStream_t stream);
+uint32_t sort_max_tiles(uint32_t cap);
 }  // namespace rtdev
 
 using namespace rtdev;
@@ -192,14 +193,26 @@ bool bvh_enabled() {
 }
 
 // Safety factors over the largest ratios tools/cull_bounds_check.py measures for each
-// bound (sphere 0.43, cube 1.83, triangle lateral 0.30 / along-ray 0.33 for
-// sin(phi) >= 0.01), and the grazing threshold.
-constexpr double SAFETY_SPHERE = 4.0, SAFETY_CUBE = 32.0, SAFETY_TRI = 16.0, SAFETY_TRI_T = 8.0,
+// bound (sphere 0.43, cube 1.83; triangles: the reported hit point's distance
+// rho eps (|o - v0| + |e|max + |o| + |v0|) / (sin(alpha) sin(phi)) with rho <= 0.6 for
+// sin(phi) < 0.1 and rho / sin(phi) <= 1.3 above).
+constexpr double SAFETY_SPHERE = 4.0, SAFETY_CUBE = 32.0, SAFETY_TRI = 4.0, TRI_STEEP = 10.0,
                  SAFETY_SLAB = 4.0;
-constexpr double GRAZE_SIN = 0.01;          // sin(phi_min): below it, the grazing pass
 constexpr double MAX_COND = 100.0;          // sigma_max(L) sigma_max(A) above it: linear pass
 constexpr double MIN_SIN_ALPHA = 0.02;      // sliver triangles: linear pass
 const double FEPS = (double)std::numeric_limits<float>::epsilon();
+
+// A hierarchy triangle's grazing threshold sin(phi_T) = GRAZE_K / sin(alpha), clamped:
+// rays meeting its plane at sin(phi) < 1.01 sin(phi_T) go to the grazing pass; the
+// rest are covered by its box grown by SAFETY_TRI eps (...) / (sin(alpha) sin(phi_T)).
+// GRAZE_K trades the grazing band's width against that growth (RT_GRAZE_K overrides).
+constexpr double GRAZE_MIN = 2e-4, GRAZE_MAX = 0.05;
+double graze_sin(double sin_a) {
+    const char* e = std::getenv("RT_GRAZE_K");
+    double k = e ? std::atof(e) : 1e-3;
+    if (!(k > 0)) k = 1e-3;
+    return std::min(GRAZE_MAX, std::max(GRAZE_MIN, k / sin_a));
+}
 
 float down_f(double x) {
     float f = (float)x;
@@ -316,14 +329,17 @@ void emit_cube(std::vector<float>& v, const CubeIn& A, float lf, float sn) {
 
 // Grazing pass data (rt_scan.hpp graze_pass): the hierarchy's triangles ordered by
 // normal direction (sign-free) in blocks of 8, each with a cone {axis, s^2}: a ray with
-// (d.axis)^2 > s^2 |d|^2 meets every plane of the block at sin(phi) > 1.01 sin(phi_min).
-// Block: {ax ay az s^2} {nx0-3} {nx4-7} {ny0-3} {ny4-7} {nz0-3} {nz4-7} {-}; its triangles
-// as 4 pairs in graze_tri.
-void build_graze(const std::vector<TriIn>& tris, const std::vector<char>& in_tri, RunLayout& L) {
+// (d.axis)^2 > s^2 |d|^2 meets every plane of the block at sin(phi) > 1.01 sin(phi_T).
+// The normals are stored divided by sin(phi_T), so "(d.n')^2 < 1.0201 |d|^2" is the
+// per-triangle grazing test.  Block: {ax ay az s^2} {n'x0-3} {n'x4-7} {n'y0-3} {n'y4-7}
+// {n'z0-3} {n'z4-7} {-}; its triangles as 4 pairs in graze_tri.
+void build_graze(const std::vector<TriIn>& tris, const std::vector<char>& in_tri, const std::vector<double>& gsin,
+                 RunLayout& L) {
     struct G {
         const TriIn* t;
         double n[3];
         uint32_t code;
+        double s;
     };
     std::vector<G> g;
     for (size_t i = 0; i < tris.size(); i++) {
@@ -347,12 +363,14 @@ void build_graze(const std::vector<TriIn>& tris, const std::vector<char>& in_tri
         uint32_t iy = (uint32_t)std::min(255.0, std::max(0.0, (py * 0.5 + 0.5) * 256.0));
         uint32_t code = 0;
         for (int b = 0; b < 8; b++) code |= (((ix >> b) & 1u) << (2 * b)) | (((iy >> b) & 1u) << (2 * b + 1));
-        g.push_back(G{&tris[i], {n[0], n[1], n[2]}, code});
+        g.push_back(G{&tris[i], {n[0], n[1], n[2]}, code, gsin[i]});
     }
     std::stable_sort(g.begin(), g.end(), [](const G& a, const G& b) { return a.code < b.code; });
-    const double phi = std::asin(1.01 * GRAZE_SIN) + 1e-4;
     for (size_t b0 = 0; b0 < g.size(); b0 += 8) {
         size_t b1 = std::min(g.size(), b0 + 8);
+        double smax = 0;
+        for (size_t i = b0; i < b1; i++) smax = std::max(smax, g[i].s);
+        const double phi = std::asin(std::min(1.0, 1.01 * smax)) + 1e-4;
         double a[3] = {0, 0, 0};
         for (size_t i = b0; i < b1; i++)
             for (int k = 0; k < 3; k++) a[k] += g[i].n[k];
@@ -373,9 +391,10 @@ void build_graze(const std::vector<TriIn>& tris, const std::vector<char>& in_tri
         for (int k = 0; k < 8; k++) {
             if (b0 + k < b1) {
                 F3 u = unit_normal(*g[b0 + k].t);
-                nx[k] = u.x;
-                ny[k] = u.y;
-                nz[k] = u.z;
+                double is = 1.0 / g[b0 + k].s;
+                nx[k] = (float)(u.x * is);
+                ny[k] = (float)(u.y * is);
+                nz[k] = (float)(u.z * is);
             } else {  // padding: never grazes (and its pair slot is a degenerate triangle)
                 nx[k] = ny[k] = nz[k] = 1e18f;
             }
@@ -410,6 +429,7 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
     std::vector<Prim> prims;
     std::vector<Geo> geo;
     std::vector<char> in_sph(sph.size(), 0), in_tri(tris.size(), 0), in_cube(cubes.size(), 0);
+    std::vector<double> tri_gsin(tris.size(), 0.0);
     std::vector<double> cube_lf(cubes.size(), 0), cube_sn(cubes.size(), 0);
     // per-primitive bounds as polynomials in D (see rt_scan.hpp): box inflation
     // h = a2 D^2 + a1 D + a0 + cC |C|, t-margin m = b1 D + b0 + bC |C|
@@ -468,11 +488,16 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
             g.r = rad * (1 + 1e-9);
             // basis eps (|o - v0| + |e|max + |o| + |v0|) / sin(alpha): lateral; the same
             // over sin(phi_min) along the ray (t-margin)
-            double k = SAFETY_TRI * FEPS / sin_a, km = SAFETY_TRI_T * FEPS / (sin_a * GRAZE_SIN);
+            // the reported hit point lies within rho eps (...) / (sin(alpha) sin(phi)) of the
+            // triangle and on the ray, so for sin(phi) >= sin(phi_T) the box grown by that
+            // bound contains it: no t-margin needed
+            double gs = graze_sin(sin_a);
+            double k = SAFETY_TRI * FEPS / sin_a * std::max(1.0 / gs, TRI_STEEP);
             double v0n = std::sqrt(v[0][0] * v[0][0] + v[0][1] * v[0][1] + v[0][2] * v[0][2]);
             double e = std::max(l1, l2) + v0n;
-            coef.push_back(Coef{0.0, 2.0 * k, k * e, k, 2.0 * km, km * e, km});
+            coef.push_back(Coef{0.0, 2.0 * k, k * e, k, 0.0, 0.0, 0.0});
             in_tri[i] = 1;
+            tri_gsin[i] = gs;
             Prim p;
             p.kind = P_TRI;
             p.id = (uint32_t)i;
@@ -591,7 +616,7 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
                          T.nodes.size(), T.leaves.size(), T.depth, max_leaf, L.c[0], L.c[1], L.c[2], L.r, L.g2,
                          L.g1, L.g0, L.m1, L.m0);
         }
-        build_graze(tris, in_tri, L);
+        build_graze(tris, in_tri, tri_gsin, L);
         L.n_dsph_bvh = (int)(L.dsph.size() / 16);
         L.n_gsph_bvh = (int)(L.gsph.size() / 16);
         L.n_tri_bvh = (int)(L.tri.size() / 24);
@@ -631,19 +656,15 @@ struct Workspace {
     uint32_t shadow_capacity = 0;
     uint32_t* levels = nullptr;      // 2 * (RT_MAX_DEPTH + 2) words
     uint32_t* overflow = nullptr;
-    // queue ordering (rt_sort.hip)
-    uint32_t* task_keys = nullptr;   // [capacity] x4 buffers
-    uint32_t* task_vals = nullptr;
+    // queue ordering (rt_order.hip)
+    uint32_t* task_keys = nullptr;   // [capacity] x2 buffers
     uint32_t* perm = nullptr;
-    uint32_t* keys_alt = nullptr;
     uint32_t sort_capacity = 0;
-    uint32_t* shadow_keys = nullptr; // [shadow_capacity] x3 buffers
-    uint32_t* shadow_keys_alt = nullptr;
+    uint32_t* shadow_keys = nullptr; // [shadow_capacity] x2 buffers
     uint32_t* shadow_sorted = nullptr;
     uint32_t sort_shadow_capacity = 0;
-    void* sort_tmp = nullptr;
-    size_t sort_tmp_bytes = 0;
-    uint32_t* h_count = nullptr;     // pinned: a level's (offset, count)
+    uint32_t* sort_tmp = nullptr;    // scratch keys + values, 256 x tiles counts, 256 digit totals
+    size_t sort_tmp_words = 0;
     // ray forest only (rt_forest): per-node shade inputs, grown with the pool
     bool forest = false;
     float4* node_aux = nullptr;
@@ -708,10 +729,14 @@ rt_status hip_status(hipError_t e) {
     if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return RT_ERR_NO_DEVICE;
     return RT_ERR_HIP;
 }
-#define HIP_TRY(x)                                  \
-    do {                                            \
-        hipError_t e_ = (x);                        \
-        if (e_ != hipSuccess) return hip_status(e_); \
+// a failing HIP call is reported on stderr (expression, line, HIP's message)
+#define HIP_TRY(x)                                                                                   \
+    do {                                                                                             \
+        hipError_t e_ = (x);                                                                         \
+        if (e_ != hipSuccess) {                                                                      \
+            std::fprintf(stderr, "rt_api.cpp:%d: %s: %s\n", __LINE__, #x, hipGetErrorString(e_));  \
+            return hip_status(e_);                                                                   \
+        }                                                                                            \
     } while (0)
 
 rt_status select_device(int32_t device, int* resolved) {
@@ -767,7 +792,7 @@ rt_status grow_node_pool(Workspace& w, uint32_t cap) {
     w.node_lit = nullptr;
     w.capacity = 0;
     HIP_TRY(hipMalloc(&w.tasks, (size_t)cap * sizeof(Task)));
-    HIP_TRY(hipMalloc(&w.nodes, (size_t)cap * sizeof(NodeRec)));
+    HIP_TRY(hipMalloc(&w.nodes, node_alloc_count(cap) * sizeof(NodeRec)));
     HIP_TRY(hipMalloc(&w.node_ps, (size_t)cap * sizeof(float4)));
     HIP_TRY(hipMalloc(&w.node_lit, (size_t)cap * sizeof(uint32_t)));
     if (w.forest) {
@@ -789,11 +814,9 @@ rt_status grow_node_pool(Workspace& w, uint32_t cap) {
 void free_workspace(Workspace& w) {
     for (void* b : {(void*)w.out, (void*)w.out8, (void*)w.counters, (void*)w.work, (void*)w.tasks, (void*)w.shadow,
                     (void*)w.nodes, (void*)w.levels, (void*)w.overflow, (void*)w.node_ps, (void*)w.node_lit,
-                    (void*)w.task_keys, (void*)w.task_vals, (void*)w.perm, (void*)w.keys_alt,
-                    (void*)w.shadow_keys, (void*)w.shadow_keys_alt, (void*)w.shadow_sorted, w.sort_tmp,
+                    (void*)w.task_keys, (void*)w.perm, (void*)w.shadow_keys, (void*)w.shadow_sorted, (void*)w.sort_tmp,
                     (void*)w.node_aux, (void*)w.node_key, (void*)w.node_pixel})
         if (b) (void)hipFree(b);
-    if (w.h_count) (void)hipHostFree(w.h_count);
     w = Workspace();
 }
 
@@ -1004,7 +1027,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     S.bvh_g0 = lay.g0;
     S.bvh_m1 = lay.m1;
     S.bvh_m0 = lay.m0;
-    S.graze_s2 = (float)(GRAZE_SIN * GRAZE_SIN * 1.0201);  // checked at 1.01 sin(phi_min)
+    S.graze_s2 = 1.0201f;  // normals pre-divided by sin(phi_T): checked at 1.01 sin(phi_T)
     S.amb_r = d->ambient.r;
     S.amb_g = d->ambient.g;
     S.amb_b = d->ambient.b;
@@ -1177,8 +1200,10 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         HIP_TRY(hipMalloc(&w.shadow, want_sh * sizeof(uint32_t)));
         w.shadow_capacity = (uint32_t)want_sh;
     }
+    const char* ss = std::getenv("RT_SORT_SHADOW");  // "0": keep production order (A/B)
     const bool sort_on = s->S.use_bvh && sort_enabled();
-    const bool sort_tasks = sort_tasks_enabled();
+    const bool sort_tasks = sort_on && sort_tasks_enabled();
+    const bool sort_shadow = sort_on && !(ss && ss[0] == '0');
     p.key_mode = task_key_mode();
     if (s->count_ops) {  // instrumented kernels; RT_COUNT=trace|shadow: only that kernel's tests
         const char* e = std::getenv("RT_COUNT");
@@ -1186,52 +1211,47 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     } else {
         p.count_mask = 0u;
     }
-    // 16-bit keys (two 8-bit radix passes): task = octant | 13 Morton bits; shadow =
+    // 16-bit keys: task = direction cell | coarse origin Morton (task_key); shadow =
     // light index | the Morton bits that fit (all 15 above 16 lights' worth of bits)
     uint32_t lbits = 0;
     while ((1u << lbits) < s->S.n_lights) lbits++;
     p.light_shift = lbits <= 1 ? 15u : (16u - lbits > 15u ? 15u : 16u - lbits);
-    const int task_bits = 16, shadow_bits = (int)(p.light_shift + lbits);
-    if (sort_on) {
-        if (w.sort_capacity < w.capacity) {
-            for (uint32_t** b : {&w.task_keys, &w.task_vals, &w.perm, &w.keys_alt}) {
-                if (*b) (void)hipFree(*b);
-                *b = nullptr;
-            }
-            w.sort_capacity = 0;
-            for (uint32_t** b : {&w.task_keys, &w.task_vals, &w.perm, &w.keys_alt})
-                HIP_TRY(hipMalloc(b, (size_t)w.capacity * sizeof(uint32_t)));
-            w.sort_capacity = w.capacity;
+    if (sort_tasks && w.sort_capacity < w.capacity) {
+        for (uint32_t** b : {&w.task_keys, &w.perm}) {
+            if (*b) (void)hipFree(*b);
+            *b = nullptr;
         }
-        if (w.sort_shadow_capacity < w.shadow_capacity) {
-            for (uint32_t** b : {&w.shadow_keys, &w.shadow_keys_alt, &w.shadow_sorted}) {
-                if (*b) (void)hipFree(*b);
-                *b = nullptr;
-            }
-            w.sort_shadow_capacity = 0;
-            for (uint32_t** b : {&w.shadow_keys, &w.shadow_keys_alt, &w.shadow_sorted})
-                HIP_TRY(hipMalloc(b, (size_t)w.shadow_capacity * sizeof(uint32_t)));
-            w.sort_shadow_capacity = w.shadow_capacity;
-        }
-        size_t b1 = 0, b2 = 0;
-        HIP_TRY(sort_pairs_u32(nullptr, b1, w.task_keys, w.keys_alt, w.task_vals, w.perm, w.capacity, task_bits,
-                               stream));
-        HIP_TRY(sort_pairs_u32(nullptr, b2, w.shadow_keys, w.shadow_keys_alt, w.shadow, w.shadow_sorted,
-                               w.shadow_capacity, shadow_bits, stream));
-        size_t need = std::max(b1, b2);
-        if (w.sort_tmp_bytes < need) {
-            if (w.sort_tmp) (void)hipFree(w.sort_tmp);
-            w.sort_tmp = nullptr;
-            w.sort_tmp_bytes = 0;
-            HIP_TRY(hipMalloc(&w.sort_tmp, need));
-            w.sort_tmp_bytes = need;
-        }
+        w.sort_capacity = 0;
+        for (uint32_t** b : {&w.task_keys, &w.perm}) HIP_TRY(hipMalloc(b, (size_t)w.capacity * sizeof(uint32_t)));
+        w.sort_capacity = w.capacity;
     }
-    if ((sort_on || w.forest) && !w.h_count) HIP_TRY(hipHostMalloc((void**)&w.h_count, 16, hipHostMallocDefault));
-    p.task_keys = sort_on ? w.task_keys : nullptr;
-    p.task_vals = sort_on ? w.task_vals : nullptr;
-    p.shadow_keys = sort_on ? w.shadow_keys : nullptr;
+    if (sort_shadow && w.sort_shadow_capacity < w.shadow_capacity) {
+        for (uint32_t** b : {&w.shadow_keys, &w.shadow_sorted}) {
+            if (*b) (void)hipFree(*b);
+            *b = nullptr;
+        }
+        w.sort_shadow_capacity = 0;
+        for (uint32_t** b : {&w.shadow_keys, &w.shadow_sorted})
+            HIP_TRY(hipMalloc(b, (size_t)w.shadow_capacity * sizeof(uint32_t)));
+        w.sort_shadow_capacity = w.shadow_capacity;
+    }
+    // sort scratch: keys + values for the larger queue, its tile counts, digit totals
+    const uint32_t sort_cap = std::max(w.capacity, w.shadow_capacity);
+    const size_t sort_words = 2 * (size_t)sort_cap + 256 * (size_t)sort_max_tiles(sort_cap) + 256;
+    if ((sort_tasks || sort_shadow) && w.sort_tmp_words < sort_words) {
+        if (w.sort_tmp) (void)hipFree(w.sort_tmp);
+        w.sort_tmp = nullptr;
+        w.sort_tmp_words = 0;
+        HIP_TRY(hipMalloc(&w.sort_tmp, sort_words * sizeof(uint32_t)));
+        w.sort_tmp_words = sort_words;
+    }
+    uint32_t* tmp_keys = w.sort_tmp;
+    uint32_t* tmp_vals = w.sort_tmp ? w.sort_tmp + sort_cap : nullptr;
+    uint32_t* tile_counts = w.sort_tmp ? w.sort_tmp + 2 * (size_t)sort_cap : nullptr;
+    uint32_t* digit_totals = w.sort_tmp ? tile_counts + 256 * (size_t)sort_max_tiles(sort_cap) : nullptr;
+    p.task_keys = sort_tasks ? w.task_keys : nullptr;
     p.perm = nullptr;
+    p.shadow_keys = sort_shadow ? w.shadow_keys : nullptr;
     p.shadow_in = w.shadow;
     p.capacity = w.capacity;
     p.shadow_capacity = w.shadow_capacity;
@@ -1260,58 +1280,40 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     int sb = s->num_cus * s->occ_shadow;
     int cb = s->num_cus * s->occ_combine;
     uint32_t levels = depth > 0 ? depth : 1;
+    // Every launch sizes itself from the device-side level counts: the whole frame is
+    // enqueued without a host round trip (levels past the deepest non-empty one are no-ops).
     HIP_TRY(launch_wave_init(w.levels, 2 * (RT_MAX_DEPTH + 2), p.total_items, w.overflow, stream));
-    if (!sort_on && !w.forest) {
-        for (uint32_t k = 0; k < levels; k++) HIP_TRY(launch_wave_trace(p, k, tb, stream));
-        HIP_TRY(launch_wave_shadow(p, sb, stream));
-        for (uint32_t k = levels; k-- > 0;) HIP_TRY(launch_wave_combine(p, k, cb, stream));
-        return RT_OK;
-    }
-    // ordered queues: the host reads each level's size (one small copy + stream sync),
-    // sorts its (key, slot) pairs into `perm` and stops at the first empty level
-    auto read2 = [&](const uint32_t* src) -> hipError_t {
-        hipError_t e = hipMemcpyAsync(w.h_count, src, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream);
-        return e == hipSuccess ? hipStreamSynchronize(stream) : e;
-    };
     HIP_TRY(launch_wave_trace(p, 0, tb, stream));
-    uint32_t used = 1;  // levels that hold nodes
     for (uint32_t k = 1; k < levels; k++) {
-        HIP_TRY(read2(w.levels + 2 * k));
-        uint32_t off = w.h_count[0], cnt = w.h_count[1];
-        if (off >= w.capacity) break;  // overflowed: the flag is already set
-        cnt = std::min(cnt, w.capacity - off);
-        if (cnt == 0) break;
-        if (sort_on && sort_tasks) {
-            size_t bytes = w.sort_tmp_bytes;
-            HIP_TRY(sort_pairs_u32(w.sort_tmp, bytes, w.task_keys + off, w.keys_alt, w.task_vals + off,
-                                   w.perm + off, cnt, task_bits, stream));
+        if (sort_tasks) {
+            HIP_TRY(launch_sort16(w.levels, (int32_t)k, w.capacity, w.task_keys, nullptr, tmp_keys, tmp_vals, w.perm,
+                                  tile_counts, digit_totals, 4 * s->num_cus, stream));
             p.perm = w.perm;
         }
         HIP_TRY(launch_wave_trace(p, k, tb, stream));
-        used = k + 1;
     }
-    HIP_TRY(read2(w.levels + 2 * (RT_MAX_DEPTH + 1)));
-    uint32_t n_sh = std::min(w.h_count[0], w.shadow_capacity);
-    if (n_sh > 0) {
-        const char* ss = std::getenv("RT_SORT_SHADOW");  // "0": keep production order (A/B)
-        if (sort_on && !(ss && ss[0] == '0')) {
-            size_t bytes = w.sort_tmp_bytes;
-            HIP_TRY(sort_pairs_u32(w.sort_tmp, bytes, w.shadow_keys, w.shadow_keys_alt, w.shadow, w.shadow_sorted,
-                                   n_sh, shadow_bits, stream));
-            p.shadow_in = w.shadow_sorted;
-        }
-        HIP_TRY(launch_wave_shadow(p, sb, stream));
+    if (sort_shadow) {
+        HIP_TRY(launch_sort16(w.levels, -1, w.shadow_capacity, w.shadow_keys, w.shadow, tmp_keys, tmp_vals,
+                              w.shadow_sorted, tile_counts, digit_totals, 4 * s->num_cus, stream));
+        p.shadow_in = w.shadow_sorted;
     }
+    HIP_TRY(launch_wave_shadow(p, sb, stream));
     if (w.forest) {  // no combine: the forest is shaded later, any number of times
         HIP_TRY(hipMemcpyAsync(forest_levels, w.levels, 2 * (RT_MAX_DEPTH + 1) * sizeof(uint32_t),
                                hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
+        uint32_t used = 1;  // levels that hold nodes
+        for (uint32_t k = 1; k < levels; k++) {
+            uint32_t off = forest_levels[2 * k], cnt = forest_levels[2 * k + 1];
+            if (off >= w.capacity || std::min(cnt, w.capacity - off) == 0) break;
+            used = k + 1;
+        }
         p.perm = nullptr;
         *forest_params = p;
         forest_levels[2 * (RT_MAX_DEPTH + 1)] = used;
         return RT_OK;
     }
-    for (uint32_t k = used; k-- > 0;) HIP_TRY(launch_wave_combine(p, k, cb, stream));
+    for (uint32_t k = levels; k-- > 0;) HIP_TRY(launch_wave_combine(p, k, cb, stream));
     return RT_OK;
 }
 

@@ -82,7 +82,7 @@ struct DevScene {
     // per ray, D = |o - c| + r: box inflation h(D) = (g2 D + g1) D + g0 and t-margin
     // m(D) = m1 D + m0 (distance units), see rt_scan.hpp
     float bvh_cx, bvh_cy, bvh_cz, bvh_r, bvh_g2, bvh_g1, bvh_g0, bvh_m1, bvh_m0;
-    float graze_s2;            // (sin phi_min)^2: below it a ray grazes a triangle plane
+    float graze_s2;            // 1.0201: (d.n')^2 < graze_s2 |d|^2 with n' = n / sin(phi_T): the ray grazes
     unsigned long long* scan_ops;  // RT_OPS_* lane-weighted test counts
 };
 
@@ -135,24 +135,23 @@ struct Task {
 
 // One traced tree node: the shading inputs of render.rs:57-68 (lights are summed later,
 // once the shadow scans have run), the child weights of render.rs:70-98, the colours its
-// children report, and where to report its own colour.  144 B.  The shadow pass reads a
-// node's shadow-ray origin from the compact `node_ps` array and reports into `node_lit`
-// (bit l: point light l is NOT shadowed), so its randomly ordered accesses touch 16 + 4
-// bytes per entry instead of the record's cache lines.
+// children report, and where to report its own colour: 8 float4 chunks (128 B),
+//   NC_AMB {ambient (tex) * scene ambient, flags}   NC_N   {hit normal, parent}
+//   NC_EYE {eye_dir, power}                         NC_KD  {kd, n1}     NC_KS {ks, n2}
+//   NC_W   {fresnel_r, rdir.n, (m.h)^power, 1 - fresnel_t}
+//   NC_ER  {colour of the reflected child, -}       NC_ET  {... of the refracted child, -}
+// stored AoSoA: blocks of 64 nodes, chunk-major inside a block (rt_wavefront.hip
+// node_c), so a wave's load or store of one chunk is one contiguous 1 KB access.  The
+// shadow-ray origin lives in the compact `node_ps` array and the shadow results in
+// `node_lit` (bit l: point light l is NOT shadowed): the shadow pass's randomly ordered
+// accesses touch 16 + 4 bytes per entry.  (Ray forest: NC_KD / NC_KS hold the children's
+// directions instead, render_tree.rs:214-255.)
+enum : int { NC_AMB = 0, NC_N = 1, NC_EYE = 2, NC_KD = 3, NC_KS = 4, NC_W = 5, NC_ER = 6, NC_ET = 7, NC_CHUNKS = 8 };
 struct NodeRec {
-    float ambx, amby, ambz;    // material ambient (tex) * scene ambient (render.rs:57)
-    float psx, psy, psz;       // shadow-ray origin: point + 0.0002 * normal (render.rs:147)
-    float nx, ny, nz;          // hit normal
-    float ex, ey, ez;          // eye_dir
-    float kdx, kdy, kdz, ksx, ksy, ksz;
-    float power, n1, n2;
-    float fr, dr, pw, ft;      // reflected: fresnel, rdir.n, (m.h)^power; refracted: 1 - fresnel
-    float erx, ery, erz;       // colour of the reflected child (0 until it reports)
-    float etx, ety, etz;       // colour of the refracted child
-    uint32_t flags;
-    uint32_t parent;           // as Task::parent; level 0: unused
-    uint32_t pad[3];
+    float4 c[NC_CHUNKS];  // allocation unit only; element n lives at node_c(base, n, chunk)
 };
+// nodes to allocate for `cap` slots (whole 64-node blocks)
+inline size_t node_alloc_count(uint32_t cap) { return ((size_t)cap + 63u) & ~(size_t)63u; }
 
 struct WaveParams {
     DevScene S;
@@ -173,10 +172,10 @@ struct WaveParams {
     uint32_t* overflow;                // set when an append would exceed a capacity
     float* out;
     unsigned long long* ray_counters;  // [node, shadow, pixels], added to
-    // ray-queue ordering (rt_sort.hip): the producer writes a key and its slot per task /
-    // shadow entry; the host sorts a level's pairs; the consumer reads through `perm`
+    // ray-queue ordering (rt_order.hip): the producer writes a 16-bit key per task /
+    // shadow entry; the sort writes the order; the consumer reads through `perm` (tasks)
+    // or `shadow_in` (shadow entries).  Null keys: no ordering.
     uint32_t* task_keys;               // [capacity]
-    uint32_t* task_vals;               // [capacity]: the slot itself
     const uint32_t* perm;              // [capacity] or null: level-k slot -> task slot
     uint32_t* shadow_keys;             // [shadow_capacity]
     const uint32_t* shadow_in;         // the shadow entries the shadow kernel reads

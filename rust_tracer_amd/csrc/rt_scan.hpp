@@ -376,9 +376,9 @@ __device__ __forceinline__ void run_cube(const DevScene& S, int b, int e, V3 o, 
 // DESIGN.md "Exact culling".  For a ray (o, d) and D = |o - c| + r (the ball (c, r)
 // holds every hierarchy primitive), every hit the reference's f32 tests can report at t'
 // satisfies: the point o + t*d lies within h(D) = (g2 D + g1) D + g0 of the primitive for
-// some t* with |t' - t*| <= m(D)/|d|.  Spheres and cubes: t* = t' (their reported points
-// themselves are that close); triangles: h bounds how far the LINE passes and m how far
-// the f32 t' slides along it, for rays meeting the plane at sin(phi) >= sin(phi_min).
+// some t* with |t' - t*| <= m(D)/|d|.  Every primitive's bound is on the reported point
+// itself (t* = t', m = 0 today); triangles for rays meeting their plane at
+// sin(phi) >= sin(phi_T), the triangle's own grazing threshold (rt_api.cpp graze_sin).
 // h also covers the rounding of this slab test.  A child box is skipped for a lane only
 // when its box grown by h misses the ray on [-m, t_max + m] (t_max = the lane's best t,
 // or the shadow limit); the wave skips it only when every lane does.  Spheres,

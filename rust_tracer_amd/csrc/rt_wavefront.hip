@@ -32,6 +32,17 @@ enum : uint32_t { NODE_HIT = 1u << 8, NODE_MISS = 1u << 9, NODE_NONE = 1u << 10 
 
 #define RT_SHADOW_COUNT(P) ((P).levels[2 * (RT_MAX_DEPTH + 1)])
 
+// chunk `c` of node n (NodeRec layout, rt_device.hpp)
+__device__ __forceinline__ float4* node_c(NodeRec* nodes, uint32_t n, int c) {
+    return reinterpret_cast<float4*>(nodes) + ((((size_t)(n >> 6) * NC_CHUNKS + (size_t)c) << 6) + (n & 63u));
+}
+__device__ __forceinline__ const float4* node_c(const NodeRec* nodes, uint32_t n, int c) {
+    return reinterpret_cast<const float4*>(nodes) + ((((size_t)(n >> 6) * NC_CHUNKS + (size_t)c) << 6) + (n & 63u));
+}
+__device__ __forceinline__ void node_flags(NodeRec* nodes, uint32_t n, uint32_t f) {
+    node_c(nodes, n, NC_AMB)->w = __uint_as_float(f);
+}
+
 struct PixelRef {
     bool valid;
     uint32_t u, v, lr;
@@ -188,13 +199,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
             if (level == 0) {
                 PixelRef px = pixel_of(P, t);
                 if (!px.valid) {
-                    P.nodes[n].flags = NODE_NONE;
+                    node_flags(P.nodes, n, NODE_NONE);
                     active = false;
                 } else {
                     n_pix++;
                     pix = px.v * P.width + px.u;
                     if (P.depth == 0) {  // trace_ray(.., 0) == BLACK, no scan
-                        P.nodes[n].flags = NODE_MISS;
+                        node_flags(P.nodes, n, NODE_MISS);
                         active = false;
                     } else {
                         float x = P.x_min + (float)px.u * P.x_delta;
@@ -221,7 +232,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
             uint32_t bk;
             scan(S, ro, rd, bt, bk, cnt);
             if (bk == 0xFFFFFFFFu) {
-                P.nodes[n].flags = NODE_MISS;  // trace_ray -> BLACK; the parent slot stays 0
+                node_flags(P.nodes, n, NODE_MISS);  // trace_ray -> BLACK; the parent slot stays 0
             } else {
                 hit = true;
                 const MatRec& M = S.mats[S.shapes[bk >> 4].mat];
@@ -234,22 +245,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 V3 ks = tex_eval(M.specular, h.tu, h.tv);
                 V3 ps = add(h.p, mul(h.n, 0.0002f));  // render.rs:147
                 if (P.shadow_keys) mort = morton15(S, ps);
-                NodeRec rec;
-                rec.ambx = ka.x * S.amb_r; rec.amby = ka.y * S.amb_g; rec.ambz = ka.z * S.amb_b;
-                rec.psx = ps.x; rec.psy = ps.y; rec.psz = ps.z;
-                rec.nx = h.n.x; rec.ny = h.n.y; rec.nz = h.n.z;
-                rec.ex = h.eye.x; rec.ey = h.eye.y; rec.ez = h.eye.z;
-                rec.kdx = kd.x; rec.kdy = kd.y; rec.kdz = kd.z;
-                rec.ksx = ks.x; rec.ksy = ks.y; rec.ksz = ks.z;
-                rec.power = M.power; rec.n1 = n1; rec.n2 = n2;
-                rec.fr = 0.f; rec.dr = 0.f; rec.pw = 0.f; rec.ft = 0.f;
-                rec.erx = 0.f; rec.ery = 0.f; rec.erz = 0.f;
-                rec.etx = 0.f; rec.ety = 0.f; rec.etz = 0.f;
-                rec.flags = NODE_HIT;
+                uint32_t flags = NODE_HIT;
+                float fr = 0.f, dr = 0.f, pw = 0.f, ft = 0.f;
                 P.node_ps[n] = make_float4(ps.x, ps.y, ps.z, 0.f);
                 P.node_lit[n] = 0u;
-                rec.parent = parent;
-                rec.pad[0] = rec.pad[1] = rec.pad[2] = 0u;
                 if (P.node_aux) {  // ray forest: what render_ray_tree re-reads at shade time
                     P.node_aux[n] = make_float4(__uint_as_float((uint32_t)h.mat), h.tu, h.tv,
                                                 __uint_as_float(h.entering ? 1u : 0u));
@@ -259,22 +258,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 }
                 bool child_ok = level + 1 < P.depth;
                 if (M.reflectivity > RT_EPS) {  // render.rs:70-84, reflect_ray :105-110
-                    rec.flags |= F_REFL;
+                    flags |= F_REFL;
                     V3 rv = sub(mul(h.n, 2.f * dot(rd, h.n)), rd);
                     rrd = neg(norm(rv));
                     rro = add(h.p, mul(rrd, 0.0002f));
-                    rec.fr = fresnel_reflection(rrd, h.n, n1, n2);
-                    rec.dr = dot(rrd, h.n);
+                    fr = fresnel_reflection(rrd, h.n, n1, n2);
+                    dr = dot(rrd, h.n);
                     V3 hv = norm(add(norm(h.eye), norm(rrd)));
                     float mh = dot(h.n, hv);
                     if (!(mh < 0.f)) {
-                        rec.flags |= F_SPEC;
-                        rec.pw = powf(mh, M.power);
+                        flags |= F_SPEC;
+                        pw = powf(mh, M.power);
                     }
                     want_refl = child_ok;
                 }
                 if (ri > RT_EPS) {  // render.rs:86-98, refract_ray :112-125
-                    rec.flags |= F_REFR;
+                    flags |= F_REFR;
                     float ratio = n1 / n2;
                     float m_dot_r = -dot(rd, h.n);
                     float cos2 = 1.f - ratio * ratio * (1.f - m_dot_r * m_dot_r);
@@ -282,17 +281,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                         float ct = sqrtf(cos2);
                         trd = add(mul(rd, ratio), mul(h.n, ratio * m_dot_r - ct));
                         tro = add(h.p, mul(trd, 0.0002f));
-                        rec.ft = 1.f - fresnel_reflection(trd, neg(h.n), n1, n2);
+                        ft = 1.f - fresnel_reflection(trd, neg(h.n), n1, n2);
                         want_refr = child_ok;
                     } else {
-                        rec.flags |= F_TIR;
+                        flags |= F_TIR;
                     }
                 }
                 if (P.node_aux) {  // children's directions arrive here (0: no / missed child)
-                    rec.kdx = rec.kdy = rec.kdz = 0.f;
-                    rec.ksx = rec.ksy = rec.ksz = 0.f;
+                    kd = v3(0.f, 0.f, 0.f);
+                    ks = v3(0.f, 0.f, 0.f);
                 }
-                P.nodes[n] = rec;
+                *node_c(P.nodes, n, NC_AMB) = make_float4(ka.x * S.amb_r, ka.y * S.amb_g, ka.z * S.amb_b,
+                                                          __uint_as_float(flags));
+                *node_c(P.nodes, n, NC_N) = make_float4(h.n.x, h.n.y, h.n.z, __uint_as_float(parent));
+                *node_c(P.nodes, n, NC_EYE) = make_float4(h.eye.x, h.eye.y, h.eye.z, M.power);
+                *node_c(P.nodes, n, NC_KD) = make_float4(kd.x, kd.y, kd.z, n1);
+                *node_c(P.nodes, n, NC_KS) = make_float4(ks.x, ks.y, ks.z, n2);
+                *node_c(P.nodes, n, NC_W) = make_float4(fr, dr, pw, ft);
+                *node_c(P.nodes, n, NC_ER) = make_float4(0.f, 0.f, 0.f, 0.f);
+                *node_c(P.nodes, n, NC_ET) = make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
         // ---- children -> level k+1 queue
@@ -303,10 +310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
             if (slot < P.capacity) {
                 Task T = {rro.x, rro.y, rro.z, rrd.x, rrd.y, rrd.z, (n << 1) | 0u, pix};
                 P.tasks[slot] = T;
-                if (P.task_keys) {
-                    P.task_keys[slot] = task_key(P, rro, rrd);
-                    P.task_vals[slot] = slot;
-                }
+                if (P.task_keys) P.task_keys[slot] = task_key(P, rro, rrd);
             } else {
                 atomicOr(P.overflow, 1u);
             }
@@ -317,10 +321,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
             if (slot < P.capacity) {
                 Task T = {tro.x, tro.y, tro.z, trd.x, trd.y, trd.z, (n << 1) | 1u, pix};
                 P.tasks[slot] = T;
-                if (P.task_keys) {
-                    P.task_keys[slot] = task_key(P, tro, trd);
-                    P.task_vals[slot] = slot;
-                }
+                if (P.task_keys) P.task_keys[slot] = task_key(P, tro, trd);
             } else {
                 atomicOr(P.overflow, 1u);
             }
@@ -417,8 +418,8 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < count; t += stride) {
         const uint32_t n = off + t;
-        const NodeRec& R = P.nodes[n];
-        uint32_t flags = R.flags;
+        const float4 c0 = *node_c(P.nodes, n, NC_AMB);
+        const uint32_t flags = __float_as_uint(c0.w);
         if (flags & NODE_NONE) {  // padding of the band buffer: defined as 0
             PixelRef px = pixel_of(P, t);
             if (level == 0 && px.u < P.width && px.lr < P.rows_local) {
@@ -430,12 +431,20 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
             continue;
         }
         V3 c = v3(0.f, 0.f, 0.f);
+        uint32_t parent = 0;
         if (flags & NODE_HIT) {
+            const float4 cn = *node_c(P.nodes, n, NC_N), ce = *node_c(P.nodes, n, NC_EYE);
+            const float4 ckd = *node_c(P.nodes, n, NC_KD), cks = *node_c(P.nodes, n, NC_KS);
+            const float4 cw = *node_c(P.nodes, n, NC_W);
+            const float4 cer = *node_c(P.nodes, n, NC_ER), cet = *node_c(P.nodes, n, NC_ET);
+            const float4 q = P.node_ps[n];
+            parent = __float_as_uint(cn.w);
             Hit h;
-            h.n = v3(R.nx, R.ny, R.nz);
-            h.eye = v3(R.ex, R.ey, R.ez);
-            V3 ps = v3(R.psx, R.psy, R.psz);
-            V3 kd = v3(R.kdx, R.kdy, R.kdz), ks = v3(R.ksx, R.ksy, R.ksz);
+            h.n = v3(cn.x, cn.y, cn.z);
+            h.eye = v3(ce.x, ce.y, ce.z);
+            const float power = ce.w, n1 = ckd.w, n2 = cks.w;
+            V3 ps = v3(q.x, q.y, q.z);
+            V3 kd = v3(ckd.x, ckd.y, ckd.z), ks = v3(cks.x, cks.y, cks.z);
             V3 lsum = v3(0.f, 0.f, 0.f);  // Sum starts at BLACK (color.rs:164-167)
             const uint32_t litmask = P.node_lit[n];
             for (int li = 0; li < S.n_lights; ++li) {
@@ -446,18 +455,18 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
                     ldir = norm(sub(v3(L.px, L.py, L.pz), ps));
                     if (!((litmask >> li) & 1u)) E = v3(0.f, 0.f, 0.f);
                 }
-                float f = fresnel_reflection(ldir, h.n, R.n1, R.n2);
-                V3 g = reflected_energy(E, ldir, h, kd, ks, R.power);
+                float f = fresnel_reflection(ldir, h.n, n1, n2);
+                V3 g = reflected_energy(E, ldir, h, kd, ks, power);
                 lsum = add(lsum, v3(f * g.x, f * g.y, f * g.z));
             }
-            V3 loc = add(v3(R.ambx, R.amby, R.ambz), lsum);
+            V3 loc = add(v3(c0.x, c0.y, c0.z), lsum);
             Frame f;
             f.ax = loc.x; f.ay = loc.y; f.az = loc.z;
-            f.fr = R.fr; f.dr = R.dr; f.pw = R.pw; f.ft = R.ft;
-            f.kdx = R.kdx; f.kdy = R.kdy; f.kdz = R.kdz;
-            f.ksx = R.ksx; f.ksy = R.ksy; f.ksz = R.ksz;
+            f.fr = cw.x; f.dr = cw.y; f.pw = cw.z; f.ft = cw.w;
+            f.kdx = kd.x; f.kdy = kd.y; f.kdz = kd.z;
+            f.ksx = ks.x; f.ksy = ks.y; f.ksz = ks.z;
             f.flags = flags;
-            c = combine(f, v3(R.erx, R.ery, R.erz), v3(R.etx, R.ety, R.etz));
+            c = combine(f, v3(cer.x, cer.y, cer.z), v3(cet.x, cet.y, cet.z));
         } else if (level > 0) {
             continue;  // a missed child reports BLACK: the parent's slot already holds 0
         }
@@ -468,12 +477,7 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
             o[1] = c.y;
             o[2] = c.z;
         } else {
-            NodeRec& Q = P.nodes[R.parent >> 1];
-            if (R.parent & 1u) {
-                Q.etx = c.x; Q.ety = c.y; Q.etz = c.z;
-            } else {
-                Q.erx = c.x; Q.ery = c.y; Q.erz = c.z;
-            }
+            *node_c(P.nodes, parent >> 1, (parent & 1u) ? NC_ET : NC_ER) = make_float4(c.x, c.y, c.z, 0.f);
         }
     }
 }
@@ -496,8 +500,7 @@ __global__ __launch_bounds__(256) void forest_shade_level_kernel(WaveParams P, u
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < count; t += stride) {
         const uint32_t n = off + t;
-        const NodeRec& R = P.nodes[n];
-        const uint32_t flags = R.flags;
+        const uint32_t flags = __float_as_uint(node_c(P.nodes, n, NC_AMB)->w);
         if (flags & NODE_NONE) continue;
         if (!(flags & NODE_HIT)) {  // RayTreeNode::None: (BLACK, 0)
             if (level == 0) {
@@ -516,9 +519,14 @@ __global__ __launch_bounds__(256) void forest_shade_level_kernel(WaveParams P, u
         if (P.dirty && !P.dirty[pix]) continue;
         const float4 aux = P.node_aux[n];
         const MatRec& M = S.mats[__float_as_uint(aux.x)];
+        const float4 cn = *node_c(P.nodes, n, NC_N), ce = *node_c(P.nodes, n, NC_EYE);
+        const float4 ckd = *node_c(P.nodes, n, NC_KD), cks = *node_c(P.nodes, n, NC_KS);
+        const float4 cer = *node_c(P.nodes, n, NC_ER), cet = *node_c(P.nodes, n, NC_ET);
+        const float4 q = P.node_ps[n];
+        const uint32_t parent = __float_as_uint(cn.w);
         Hit h;
-        h.n = v3(R.nx, R.ny, R.nz);
-        h.eye = v3(R.ex, R.ey, R.ez);
+        h.n = v3(cn.x, cn.y, cn.z);
+        h.eye = v3(ce.x, ce.y, ce.z);
         h.tu = aux.y;
         h.tv = aux.z;
         const bool entering = __float_as_uint(aux.w) != 0u;
@@ -526,7 +534,7 @@ __global__ __launch_bounds__(256) void forest_shade_level_kernel(WaveParams P, u
         const float n1 = entering ? 1.f : ri;
         const float n2 = entering ? ri : 1.f;
         const V3 kd = tex_eval(M.diffuse, h.tu, h.tv), ks = tex_eval(M.specular, h.tu, h.tv);
-        V3 ps = v3(R.psx, R.psy, R.psz);
+        V3 ps = v3(q.x, q.y, q.z);
         V3 lsum = v3(0.f, 0.f, 0.f);
         const uint32_t litmask = P.node_lit[n];
         for (int li = 0; li < S.n_lights; ++li) {
@@ -541,8 +549,8 @@ __global__ __launch_bounds__(256) void forest_shade_level_kernel(WaveParams P, u
             V3 g = reflected_energy(E, ldir, h, kd, ks, M.power);
             lsum = add(lsum, v3(f * g.x, f * g.y, f * g.z));
         }
-        const V3 er = v3(R.erx, R.ery, R.erz), dr = v3(R.kdx, R.kdy, R.kdz);
-        const V3 et = v3(R.etx, R.ety, R.etz), dt = v3(R.ksx, R.ksy, R.ksz);
+        const V3 er = v3(cer.x, cer.y, cer.z), dr = v3(ckd.x, ckd.y, ckd.z);
+        const V3 et = v3(cet.x, cet.y, cet.z), dt = v3(cks.x, cks.y, cks.z);
         float fr = fresnel_reflection(dr, h.n, n1, n2);
         V3 gr = reflected_energy(er, h.eye, h, kd, ks, M.power);
         V3 refl = v3(fr * gr.x, fr * gr.y, fr * gr.z);
@@ -556,16 +564,11 @@ __global__ __launch_bounds__(256) void forest_shade_level_kernel(WaveParams P, u
             o[0] = c.x;
             o[1] = c.y;
             o[2] = c.z;
-        } else {
-            NodeRec& Q = P.nodes[R.parent >> 1];
-            V3 d = neg(h.eye);
-            if (R.parent & 1u) {
-                Q.etx = c.x; Q.ety = c.y; Q.etz = c.z;
-                Q.ksx = d.x; Q.ksy = d.y; Q.ksz = d.z;
-            } else {
-                Q.erx = c.x; Q.ery = c.y; Q.erz = c.z;
-                Q.kdx = d.x; Q.kdy = d.y; Q.kdz = d.z;
-            }
+        } else {  // the parent's slot: colour, and the direction in its kd / ks chunk (n1 / n2 unused here)
+            const V3 d = neg(h.eye);
+            const bool refr = (parent & 1u) != 0;
+            *node_c(P.nodes, parent >> 1, refr ? NC_ET : NC_ER) = make_float4(c.x, c.y, c.z, 0.f);
+            *node_c(P.nodes, parent >> 1, refr ? NC_KS : NC_KD) = make_float4(d.x, d.y, d.z, 0.f);
         }
     }
 }
@@ -577,7 +580,7 @@ __global__ void forest_mark_kernel(const uint32_t* node_key, const uint32_t* nod
                                    uint32_t n_nodes, const uint8_t* key_mask, uint32_t n_keys, uint8_t* mark,
                                    uint32_t* sizes) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_nodes; i += gridDim.x * blockDim.x) {
-        if (!(nodes[i].flags & NODE_HIT)) continue;
+        if (!(__float_as_uint(node_c(nodes, i, NC_AMB)->w) & NODE_HIT)) continue;
         uint32_t pix = node_pixel[i];
         if (sizes) atomicAdd(&sizes[pix], 1u);
         if (key_mask) {

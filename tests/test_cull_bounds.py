@@ -1,14 +1,14 @@
 """The culling hierarchy's error bounds (DESIGN.md "Exact culling") against the
 reference arithmetic, replayed in numpy float32 on adversarial rays
 (tools/cull_bounds_check.py).  rt_api.cpp multiplies each basis by a safety factor
-(sphere 4, cube 32; triangles: 16 on the lateral bound for sin(phi) >= 1e-3, 8 on the
-along-ray slide for sin(phi) >= 0.01); the largest ratio measured here must stay well
-below it, or the product would cull hits the reference reports."""
+(sphere 4, cube 32; triangles 4 on rho for sin(phi) < 0.1 and 4 x 10 on rho / sin(phi)
+above, rt_api.cpp SAFETY_TRI / TRI_STEEP); the largest ratio measured here must stay a
+factor 4 below it, or the product would cull hits the reference reports."""
 import pytest
 
 from tools.cull_bounds_check import run
 
-SAFETY = {"sphere": 4.0, "cube": 32.0, "triangle": 8.0, "triangle_lateral": 16.0}
+SAFETY = {"sphere": 4.0, "cube": 32.0, "triangle": 4.0, "triangle_steep": 40.0}
 
 
 @pytest.mark.parametrize("seed", [101, 202])

@@ -17,8 +17,12 @@ primitive, and prints the largest ratio  distance / bound-basis  per primitive t
 with l = o' (the object-space origin), lam = |L|_F |o| + |s| (the magnitudes the
 rounding of L o + s scales with), phi the angle between the ray and the triangle plane.
 
-rt_api.cpp multiplies each basis by a safety factor (RT_CULL_SAFETY) that must exceed
-the ratios printed here by a wide margin.
+rt_api.cpp multiplies each basis by a safety factor that must exceed the ratios printed
+here by a wide margin.  Triangles report two numbers: rho = distance / basis over rays
+with sin(phi) < 0.1 (the grazing range, where 1/sin(phi) is large), and for steeper rays
+distance * sin(alpha) / (eps (...)), i.e. rho / sin(phi) (the box growth rt_api.cpp
+caps at TRI_STEEP).  The line distance of the ray from the triangle is printed for
+reference only: the hierarchy bounds the reported POINT, which lies on the ray.
 
 usage: python tools/cull_bounds_check.py [n_per_type=2000000] [seed=1]
 """
@@ -260,7 +264,7 @@ def check_cubes(rng, n):
     return report("cube", need / basis)
 
 
-def check_triangles(rng, n):
+def check_triangles(rng, n, phi_lo=1e-7, phi_hi=np.pi / 2, detail=False):
     v0 = rng.uniform(-4, 4, (n, 3))
     size = np.exp(rng.uniform(np.log(0.05), np.log(3.0), n))
     e1 = unit(rng.normal(size=(n, 3))) * size[:, None] * rng.uniform(0.3, 1, (n, 1))
@@ -278,7 +282,7 @@ def check_triangles(rng, n):
     T = a + u[:, None] * (b - a) + v[:, None] * (cc - a)
     T += Nn * (np.sign(rng.normal(size=n)) * np.exp(rng.uniform(np.log(1e-9), np.log(1e-1), n)))[:, None]
     # direction at angle phi to the plane
-    phi = np.exp(rng.uniform(np.log(1e-7), np.log(np.pi / 2), n))
+    phi = np.exp(rng.uniform(np.log(phi_lo), np.log(phi_hi), n))
     inpl = unit(np.cross(Nn, rng.normal(size=(n, 3))))
     d = unit(np.cos(phi)[:, None] * inpl + (np.sin(phi) * np.sign(rng.normal(size=n)))[:, None] * Nn)
     dist = np.exp(rng.uniform(np.log(1e-3), np.log(60.0), n))
@@ -298,27 +302,33 @@ def check_triangles(rng, n):
     lbasis = EPS * (tv + emax + np.linalg.norm(o64, axis=1) + np.linalg.norm(a[hit], axis=1)) / sin_a[hit]
     lratio = lat / lbasis
     buckets = {"LATERAL (line distance, no 1/sin(phi))": f"max ratio {lratio.max():.3g}"}
-    for lo_, hi_ in ((1e-8, 1e-5), (1e-5, 1e-3), (1e-3, 1e-2), (1e-2, 1e-1), (1e-1, 1.01)):
+    for lo_, hi_ in ((1e-8, 1e-5), (1e-5, 1e-4), (1e-4, 3e-4), (3e-4, 1e-3), (1e-3, 2e-3), (2e-3, 1e-2),
+                     (1e-2, 1e-1), (1e-1, 1.01)):
         m = (sphi >= lo_) & (sphi < hi_)
         if m.any():
             buckets[f"sin(phi) in [{lo_:g},{hi_:g})"] = (f"n={m.sum()} max ratio {ratio[m].max():.3g}, "
                                                          f"lateral {lratio[m].max():.3g}")
-    lat_ok = sphi >= 1e-3  # the lateral (line-distance) bound is claimed for sin(phi) >= 1e-3
-    lat_max = float(lratio[lat_ok].max()) if lat_ok.any() else 0.0
-    return report("triangle", ratio, buckets), lat_max
+    if detail:
+        return dict(lratio=lratio, ratio=ratio, sphi=sphi, sin_a=sin_a[hit], o=o64, d=d64, v=(a[hit], b[hit], cc[hit]),
+                    t=t[hit], lat=lat, lbasis=lbasis, dist=dist[hit], V=(V0[hit], V1[hit], V2[hit]), o32=o32[hit], d32=d32[hit])
+    small = sphi < 0.1
+    rho_small = float(ratio[small].max()) if small.any() else 0.0
+    steep = float((ratio / np.maximum(sphi, 1e-30))[~small].max()) if (~small).any() else 0.0
+    report("triangle", ratio, buckets)
+    return rho_small, steep
 
 
 def run(n, seed, chunk=500000):
     """largest measured ratio per primitive type over n adversarial rays each"""
     rng = np.random.default_rng(seed)
-    worst = {"sphere": 0.0, "cube": 0.0, "triangle": 0.0, "triangle_lateral": 0.0}
+    worst = {"sphere": 0.0, "cube": 0.0, "triangle": 0.0, "triangle_steep": 0.0}
     for k in range(0, n, chunk):
         m = min(chunk, n - k)
         worst["sphere"] = max(worst["sphere"], check_spheres(rng, m))
         worst["cube"] = max(worst["cube"], check_cubes(rng, m))
-        tri, lat = check_triangles(rng, m)
+        tri, steep = check_triangles(rng, m)
         worst["triangle"] = max(worst["triangle"], tri)
-        worst["triangle_lateral"] = max(worst["triangle_lateral"], lat)
+        worst["triangle_steep"] = max(worst["triangle_steep"], steep)
     return worst
 
 
