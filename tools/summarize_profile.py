@@ -17,7 +17,7 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 RENDER = ("trace_level_kernel", "shadow_kernel", "combine_level_kernel", "wave_init_kernel", "render_kernel",
-          "rocprim", "fillBufferAligned")
+          "rocprim", "fillBufferAligned", "sort_count_kernel", "sort_scan_kernel", "sort_scatter_kernel")
 
 
 def family(kernel_name):
@@ -29,6 +29,8 @@ def family(kernel_name):
         if k in kernel_name:
             if k == "rocprim":
                 return "queue sort (rocPRIM onesweep)"
+            if k.startswith("sort_"):
+                return "queue sort (device radix: " + k + ")"
             if k == "fillBufferAligned":
                 return "sort lookback reset (fill)"
             return k
