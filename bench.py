@@ -48,12 +48,14 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", type=int, default=3, help="BASELINE config (2..5 synth scenes)")
-    p.add_argument("--width", type=int, default=1920)
-    p.add_argument("--height", type=int, default=1080)
-    p.add_argument("--depth", type=int, default=8)
+    p.add_argument("--width", type=int, default=None, help="default: the config's (1920 / 3840)")
+    p.add_argument("--height", type=int, default=None, help="default: the config's (1080 / 2160)")
+    p.add_argument("--depth", type=int, default=None, help="default: the config's (4 / 8)")
+    p.add_argument("--spp", type=int, default=None, help="samples per pixel (default: 64 for config 5, else 1)")
+    p.add_argument("--seed", type=int, default=None, help="jitter seed (default: 3 for config 5)")
     p.add_argument("--band-rows", type=int, default=8)
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU oracle timing")
-    p.add_argument("--cpu-rows-step", type=int, default=24,
+    p.add_argument("--cpu-rows-step", type=int, default=None,
                    help="CPU baseline renders every k-th row of the frame")
     p.add_argument("--backend", default="nccl", help="nccl (RCCL) or gloo (CPU rehearsal)")
     p.add_argument("--check", type=int, default=0,
@@ -63,7 +65,24 @@ def parse():
                         "(used by the rocprofv3 counter passes so they see only the default kernels)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="rocprofv3 FETCH_SIZE/WRITE_SIZE summary for the render kernel")
-    return p.parse_args()
+    a = p.parse_args()
+    # BASELINE.json configs: 2 = 1080p depth 4 (100 spheres); 3 = 1080p
+    # depth 8 (1k primitives); 4 = 4K depth 8; 5 = 4K depth 8, 64 jittered spp, seed 3
+    big = a.config in (4, 5)
+    a.width = a.width or (3840 if big else 1920)
+    a.height = a.height or (2160 if big else 1080)
+    a.depth = a.depth if a.depth is not None else (4 if a.config == 2 else 8)
+    a.spp = a.spp or (64 if a.config == 5 else 1)
+    a.seed = a.seed if a.seed is not None else (3 if a.config == 5 else 0)
+    if a.cpu_rows_step is None:  # ~86k pixel samples of CPU work (~6 s on config 3)
+        a.cpu_rows_step = max(1, -(-a.width * a.height * a.spp // 86400))
+    return a
+
+
+def scene_label(config):
+    if config == 2:
+        return "synth seed 1 (100 spheres, 2 planes, 3 point lights)"
+    return "synth seed 2 (600 spheres, 25 cubes, 100 triangles, 2 planes, 3 point lights)"
 
 
 def cpu_baseline(args, desc):
@@ -74,15 +93,15 @@ def cpu_baseline(args, desc):
     rows = range(0, args.height, args.cpu_rows_step)
     t0 = time.perf_counter()
     _, cnt = o.render(args.width, args.height, args.depth, rows=(0, args.height, args.cpu_rows_step),
-                      threads=1)
+                      threads=1, spp=args.spp, seed=args.seed)
     dt = time.perf_counter() - t0
     return {
-        "value": round(cnt["pixels"] / dt / 1e6, 6),
+        "value": round(cnt["pixels"] / args.spp / dt / 1e6, 6),
         "unit": "Mpixels/s",
         "cores": 1,
         "kind": "port",
         "sample": f"{len(rows)} of {args.height} rows (every {args.cpu_rows_step}th) of the "
-                  f"benchmark frame, {cnt['pixels']} pixels, {dt:.1f} s, single thread "
+                  f"benchmark frame, {cnt['pixels'] // args.spp} pixels x {args.spp} spp, {dt:.1f} s, single thread "
                   f"(C++ restatement of src/render.rs, g++ -O2 -ffp-contract=off); "
                   f"host: {os.cpu_count()} logical CPUs",
         "seconds": round(dt, 2),
@@ -121,7 +140,8 @@ def main():
 
     desc = SceneDesc.synth_config(args.config)
     scene = DeviceScene(desc, device=dev.index)
-    tiler = FrameTiler(scene, args.width, args.height, args.depth, args.band_rows, rank, world, dev)
+    tiler = FrameTiler(scene, args.width, args.height, args.depth, args.band_rows, rank, world, dev,
+                       spp=args.spp, seed=args.seed)
 
     def barrier():
         if world > 1:
@@ -175,7 +195,8 @@ def main():
         torch.cuda.synchronize()
         if rank == 0:
             import numpy as np
-            ref, _, _, _ = scene.render(args.width, args.height, args.depth, device=dev.index)
+            ref, _, _, _ = scene.render(args.width, args.height, args.depth, device=dev.index, spp=args.spp,
+                                        seed=args.seed)
             got = frame.cpu().numpy()
             frame_check = bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32)))
     elapsed, kernel_ms_max = stats.tolist()
@@ -189,8 +210,8 @@ def main():
         achieved = per_launch_flops / (kernel_ms / 1e3) / 1e12 if ops else None
         # what the reference's linear scan would need for the same rays (F_alg per scan)
         brute_flops = local_scans * scene.flops_per_scan
-        workload = (f"config{args.config}: synth seed 2 (600 spheres, 25 cubes, 100 triangles, "
-                    f"2 planes, 3 point lights), {args.width}x{args.height}, depth {args.depth}")
+        workload = (f"config{args.config}: {scene_label(args.config)}, {args.width}x{args.height}, "
+                    f"depth {args.depth}" + (f", {args.spp} spp (jitter seed {args.seed})" if args.spp > 1 else ""))
         traffic = load_traffic(args.traffic_json, workload)
         roofline = {
             "bound": "valu",
@@ -210,7 +231,7 @@ def main():
                         "linear_scan_equivalent_TFLOPs": round(brute_flops / (kernel_ms / 1e3) / 1e12, 3)},
             "ceilings": {"no_fma_contraction": 0.5},
             "hbm": {
-                "algorithmic_bytes_per_launch": scene.device_bytes + args.width * args.height * 12 / world,
+                "algorithmic_bytes_per_launch": args.spp * (scene.device_bytes + args.width * args.height * 12 / world),
                 "achieved_GBps": round((traffic["bytes_per_launch"] / (kernel_ms / 1e3) / 1e9), 3)
                 if traffic else None,
                 "peak_GBps": PEAK_HBM_GBPS,
@@ -234,7 +255,9 @@ def main():
             "config": {
                 "workload": workload,
                 "width": args.width, "height": args.height, "depth": args.depth,
-                "leaf_primitives": 1000, "band_rows": args.band_rows,
+                "leaf_primitives": 100 if args.config == 2 else 1000,
+                "spp": args.spp, "seed": args.seed, "band_rows": args.band_rows,
+                "msamples_per_s": round(args.width * args.height * args.spp * steps / elapsed / 1e6, 3),
                 "parallelism": f"row-bands x{world}" + ((" + RCCL gather" if args.backend == "nccl"
                                                           else f" + {args.backend} gather (rehearsal)")
                                                          if world > 1 else ""),

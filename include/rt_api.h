@@ -174,6 +174,25 @@ rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* camera,
                                 uint32_t world, float* d_rgb, uint64_t* d_counters,
                                 void* stream);
 
+/* Stochastic supersampling (BASELINE config 5; the reference has no equivalent, SURVEY.md
+ * §7 step 6).  Sample k (0 <= k < spp) of pixel (u, v) is Camera::get_ray's ray through
+ * (u + jx, v + jy) -- x = x_min + ((float)u + jx) * x_delta, y = y_max - ((float)v + jy) *
+ * y_delta (render.rs:178-185 with the jitter added) -- where, with pixel = v * x_res + u
+ * and mix32 the 32-bit finaliser x ^= x>>16; x *= 0x7feb352d; x ^= x>>15;
+ * x *= 0x846ca68b; x ^= x>>16:
+ *     h  = mix32(mix32(seed ^ 0x9e3779b9) ^ pixel)
+ *     j_dim = (mix32(h ^ mix32(2k + dim + 1)) >> 8) * 2^-24     (dim 0: jx, 1: jy)
+ * The pixel is the f32 sum of its sample colours in sample order (sample 0 first),
+ * divided by (float)spp.  spp == 1 is rt_render exactly (no jitter).  The counters count
+ * pixel samples. */
+rt_status rt_render_spp(const rt_scene* scene, const rt_camera* camera, uint32_t depth,
+                        uint32_t spp, uint32_t seed, const rt_render_opts* opts,
+                        float* rgb, uint8_t* rgb8);
+rt_status rt_render_bands_spp_async(const rt_scene* scene, const rt_camera* camera,
+                                    uint32_t depth, uint32_t spp, uint32_t seed,
+                                    uint32_t band_rows, uint32_t rank, uint32_t world,
+                                    float* d_rgb, uint64_t* d_counters, void* stream);
+
 /* Number of rows (including padding) a rank's band buffer holds. */
 uint32_t rt_band_rows_per_rank(uint32_t y_res, uint32_t band_rows, uint32_t world);
 

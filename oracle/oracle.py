@@ -44,6 +44,8 @@ def lib():
                                      C.c_uint32, fa, P(C.c_uint64)]
     L.oracle_render_rows_mt.argtypes = [vp, P(abi.rt_camera), C.c_uint32, C.c_uint32, C.c_uint32,
                                         C.c_uint32, fa, P(C.c_uint64), C.c_uint32]
+    L.oracle_render_rows_spp_mt.argtypes = [vp, P(abi.rt_camera), C.c_uint32, C.c_uint32, C.c_uint32,
+                                            C.c_uint32, C.c_uint32, C.c_uint32, fa, P(C.c_uint64), C.c_uint32]
     L.oracle_render_forest.argtypes = [vp, P(abi.rt_camera), C.c_uint32, fa, P(C.c_uint32)]
     L.oracle_forest_build.argtypes = [vp, P(abi.rt_camera), C.c_uint32, P(vp)]
     L.oracle_forest_render.argtypes = [vp, fa]
@@ -105,16 +107,17 @@ class OracleScene:
         if self.h:
             self.L.oracle_scene_destroy(self.h)
 
-    def render(self, x_res, y_res, depth, rows=None, threads=1):
+    def render(self, x_res, y_res, depth, rows=None, threads=1, spp=1, seed=0):
         """render.rs:31-38 -> (rgb float32 [y_res, x_res, 3], counters dict).
-        rows = (begin, end, step) renders a subset (other rows stay 0)."""
+        rows = (begin, end, step) renders a subset (other rows stay 0).
+        spp > 1: jittered supersampling with rt_render_spp's hash (config 5)."""
         from rust_tracer_amd import abi
         cam = abi.camera(x_res, y_res)
         rgb = np.zeros((y_res, x_res, 3), np.float32)
         cnt = (C.c_uint64 * 3)()
         b, e, s = rows if rows is not None else (0, y_res, 1)
-        st = self.L.oracle_render_rows_mt(self.h, C.byref(cam), depth, b, e, s,
-                                          rgb.ctypes.data_as(C.POINTER(C.c_float)), cnt, threads)
+        st = self.L.oracle_render_rows_spp_mt(self.h, C.byref(cam), depth, b, e, s, spp, seed,
+                                              rgb.ctypes.data_as(C.POINTER(C.c_float)), cnt, threads)
         if st != 0:
             raise RuntimeError(f"oracle_render failed: {st}")
         return rgb, {"node_rays": cnt[0], "shadow_rays": cnt[1], "pixels": cnt[2]}

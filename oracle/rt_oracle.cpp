@@ -907,17 +907,83 @@ rt_status oracle_render_rows(const oracle_scene* s, const rt_camera* cam, uint32
     return RT_OK;
 }
 
+// Stochastic supersampling (no reference equivalent): sample k of
+// pixel (u, v) is Camera::get_ray's ray through (u + jx, v + jy), with the counter hash
+// of include/rt_api.h (rt_render_spp) restated here; the pixel is the f32 sum of its
+// samples in sample order, divided by spp.  spp == 1 is render.rs exactly (no jitter).
+static uint32_t spp_mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+static float spp_jitter(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t dim) {
+    uint32_t h = spp_mix32(spp_mix32(seed ^ 0x9e3779b9u) ^ pixel);
+    h = spp_mix32(h ^ spp_mix32(2u * sample + dim + 1u));
+    return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+
+rt_status oracle_render_rows_spp(const oracle_scene* s, const rt_camera* cam, uint32_t depth,
+                                 uint32_t row_begin, uint32_t row_end, uint32_t row_step,
+                                 uint32_t spp, uint32_t seed, float* rgb, uint64_t* counters) {
+    if (!s || !cam || !rgb || row_step == 0 || spp == 0) return RT_ERR_INVALID_ARG;
+    if (spp == 1) return oracle_render_rows(s, cam, depth, row_begin, row_end, row_step, rgb, counters);
+    Camera c = cam_of(cam);
+    Counters cnt;
+    if (row_end > c.y_res) row_end = c.y_res;
+    const float x_delta = (c.x_max - c.x_min) / (float)c.x_res;
+    const float y_delta = (c.y_max - c.y_min) / (float)c.y_res;
+    for (uint32_t v = row_begin; v < row_end; v += row_step) {
+        for (uint32_t u = 0; u < c.x_res; u++) {
+            const uint32_t pixel = v * c.x_res + u;
+            Color sum(0.f, 0.f, 0.f);
+            for (uint32_t k = 0; k < spp; k++) {
+                float x = c.x_min + ((float)u + spp_jitter(seed, pixel, k, 0)) * x_delta;
+                float y = c.y_max - ((float)v + spp_jitter(seed, pixel, k, 1)) * y_delta;
+                Point3 vp(x, y, 0.f);
+                Color col = trace_ray(s->scene, Ray(c.origin, vp.sub(c.origin).norm()), depth, cnt);
+                if (k == 0) {
+                    sum = col;
+                } else {
+                    sum.r = sum.r + col.r;
+                    sum.g = sum.g + col.g;
+                    sum.b = sum.b + col.b;
+                }
+                cnt.pixels++;
+            }
+            float* px = rgb + ((size_t)v * c.x_res + u) * 3;
+            px[0] = sum.r / (float)spp;
+            px[1] = sum.g / (float)spp;
+            px[2] = sum.b / (float)spp;
+        }
+    }
+    if (counters) {
+        counters[0] += cnt.node_rays;
+        counters[1] += cnt.shadow_rays;
+        counters[2] += cnt.pixels;
+    }
+    return RT_OK;
+}
+
 rt_status oracle_render_rows_mt(const oracle_scene* s, const rt_camera* cam, uint32_t depth,
                                 uint32_t row_begin, uint32_t row_end, uint32_t row_step,
                                 float* rgb, uint64_t* counters, uint32_t threads) {
+    return oracle_render_rows_spp_mt(s, cam, depth, row_begin, row_end, row_step, 1, 0, rgb, counters, threads);
+}
+
+rt_status oracle_render_rows_spp_mt(const oracle_scene* s, const rt_camera* cam, uint32_t depth,
+                                    uint32_t row_begin, uint32_t row_end, uint32_t row_step, uint32_t spp,
+                                    uint32_t seed, float* rgb, uint64_t* counters, uint32_t threads) {
     if (threads <= 1)
-        return oracle_render_rows(s, cam, depth, row_begin, row_end, row_step, rgb, counters);
+        return oracle_render_rows_spp(s, cam, depth, row_begin, row_end, row_step, spp, seed, rgb, counters);
     std::vector<std::thread> pool;
     std::vector<uint64_t> part(3 * threads, 0);
     for (uint32_t k = 0; k < threads; k++) {
         pool.emplace_back([=, &part]() {
-            oracle_render_rows(s, cam, depth, row_begin + k * row_step, row_end, row_step * threads,
-                               rgb, &part[3 * k]);
+            oracle_render_rows_spp(s, cam, depth, row_begin + k * row_step, row_end, row_step * threads,
+                                   spp, seed, rgb, &part[3 * k]);
         });
     }
     for (auto& t : pool) t.join();

@@ -275,18 +275,19 @@ class DeviceScene:
               "rt_scene_scan_ops")
         return dict(zip(self.SCAN_OPS, (int(v) for v in out)))
 
-    def render(self, x_res, y_res, depth, want_u8=False, device=-1):
-        """render.rs:31-38 -> (rgb float32 [y_res, x_res, 3], counters dict, kernel_ms, rgb8)"""
+    def render(self, x_res, y_res, depth, want_u8=False, device=-1, spp=1, seed=0):
+        """render.rs:31-38 -> (rgb float32 [y_res, x_res, 3], counters dict, kernel_ms, rgb8).
+        spp > 1: jittered supersampling (rt_render_spp, BASELINE config 5)."""
         cam = camera(x_res, y_res)
         rgb = np.zeros((y_res, x_res, 3), np.float32)
         rgb8 = np.zeros((y_res, x_res, 3), np.uint8) if want_u8 else None
         cnt = abi.rt_counters()
         ms = C.c_float(0)
         opts = abi.rt_render_opts(device, C.pointer(cnt), C.pointer(ms))
-        check(self._L.rt_render(self.h, C.byref(cam), depth, C.byref(opts),
-                                rgb.ctypes.data_as(C.POINTER(C.c_float)),
-                                rgb8.ctypes.data_as(C.POINTER(C.c_uint8)) if want_u8 else None),
-              "rt_render")
+        check(self._L.rt_render_spp(self.h, C.byref(cam), depth, spp, seed, C.byref(opts),
+                                    rgb.ctypes.data_as(C.POINTER(C.c_float)),
+                                    rgb8.ctypes.data_as(C.POINTER(C.c_uint8)) if want_u8 else None),
+              "rt_render_spp")
         counters = {"node_rays": cnt.node_rays, "shadow_rays": cnt.shadow_rays,
                     "pixels": cnt.pixels}
         self.last_wave_iterations = cnt.wave_iterations
@@ -301,10 +302,10 @@ class DeviceScene:
         return DeviceForest(self, x_res, y_res, depth)
 
     def render_bands_async(self, cam, depth, band_rows, rank, world, d_rgb_ptr, d_counters_ptr,
-                           stream_ptr):
-        check(self._L.rt_render_bands_async(self.h, C.byref(cam), depth, band_rows, rank, world,
-                                            C.c_void_p(d_rgb_ptr), C.c_void_p(d_counters_ptr),
-                                            C.c_void_p(stream_ptr)), "rt_render_bands_async")
+                           stream_ptr, spp=1, seed=0):
+        check(self._L.rt_render_bands_spp_async(self.h, C.byref(cam), depth, spp, seed, band_rows, rank, world,
+                                                C.c_void_p(d_rgb_ptr), C.c_void_p(d_counters_ptr),
+                                                C.c_void_p(stream_ptr)), "rt_render_bands_spp_async")
 
 
 class DeviceForest:

@@ -56,7 +56,8 @@ void enter_to_proceed() {  // main.rs:125-131
 void usage() {
     std::fprintf(stderr,
                  "usage: rust_tracer [-w W] [-h H] [-d D] [--method basic|rayforest] [--stats] [-i]\n"
-                 "                   [--scene my_scene|bench128|synth2|synth3] [--device N] [--out FILE]\n"
+                 "                   [--scene my_scene|bench128|synth2|synth3|synth5] [--device N] [--out FILE]\n"
+                 "                   [--spp N] [--seed S]\n"
                  "                   [bench [-n RUNS] [-f]]\n");
 }
 
@@ -70,6 +71,7 @@ int fail(const char* what, rt_status st) {
 int main(int argc, char** argv) {
     uint32_t w = 512, h = 512, depth = 8;  // cli.rs defaults
     int device = -1, runs = 10;
+    uint32_t spp = 1, seed = 0;  // supersampling (config 5; not in the reference CLI)
     bool bench = false, forest_method = false, stats = false, interactive = false, filter = false;
     std::string scene_name = "my_scene", out;
     for (int i = 1; i < argc; i++) {
@@ -86,6 +88,8 @@ int main(int argc, char** argv) {
         else if (a == "-d" || a == "--depth") depth = (uint32_t)std::atoi(next());
         else if (a == "--scene") scene_name = next();
         else if (a == "--device") device = std::atoi(next());
+        else if (a == "--spp") spp = (uint32_t)std::atoi(next());
+        else if (a == "--seed") seed = (uint32_t)std::atoi(next());
         else if (a == "--out") out = next();
         else if (a == "--stats") stats = true;
         else if (a == "-i" || a == "--interactive") interactive = true;
@@ -114,9 +118,9 @@ int main(int argc, char** argv) {
     Scene scene;
     if (scene_name == "my_scene") create_scene(scene);
     else if (scene_name == "bench128") create_bench_128_scene(scene);
-    else if (scene_name == "synth2" || scene_name == "synth3") {
+    else if (scene_name == "synth2" || scene_name == "synth3" || scene_name == "synth5") {
         rt_synth_params p;
-        rt_synth_config(scene_name == "synth2" ? 2 : 3, &p);
+        rt_synth_config(scene_name[5] - '0', &p);
         create_synth_scene(scene, p);
     } else {
         usage();
@@ -146,8 +150,8 @@ int main(int argc, char** argv) {
         auto t0 = Clock::now();
         for (int k = 0; k < n; k++) {
             auto r0 = Clock::now();
-            st = rt_render(s, &c, depth, &opts, rgb.data(), rgb8.data());
-            if (st != RT_OK) return fail("rt_render", st);
+            st = rt_render_spp(s, &c, depth, spp, seed, &opts, rgb.data(), rgb8.data());
+            if (st != RT_OK) return fail("rt_render_spp", st);
             std::printf("render_scene: %lldms\n", ms_since(r0));  // main.rs:250-253
         }
         long long ns = (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();

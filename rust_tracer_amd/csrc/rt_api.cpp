@@ -1084,21 +1084,23 @@ rt_status rt_scene_set_scan_counting(rt_scene* s, int32_t enable) {
     return RT_OK;
 }
 
-static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
-                                   uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
-                                   hipStream_t stream);
+static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
+                                   uint32_t band_rows, uint32_t rank, uint32_t world, float* d_rgb,
+                                   unsigned long long* d_counters, hipStream_t stream);
 
-static rt_status launch_bands(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
-                              uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
-                              hipStream_t stream) {
+static rt_status launch_bands(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
+                              uint32_t band_rows, uint32_t rank, uint32_t world, float* d_rgb,
+                              unsigned long long* d_counters, hipStream_t stream) {
     if (!s || !cam || !d_rgb || band_rows == 0 || world == 0 || rank >= world) return RT_ERR_INVALID_ARG;
+    if (spp == 0) return RT_ERR_INVALID_ARG;
     if (cam->x_res == 0 || cam->y_res == 0) return RT_ERR_INVALID_ARG;
     if (depth > RT_MAX_DEPTH) return RT_ERR_UNSUPPORTED;
     if ((uint64_t)cam->x_res * cam->y_res * 3 >= (1ull << 32)) return RT_ERR_UNSUPPORTED;
     rt_status st = ensure_ws(s, 0, 0);
     if (st != RT_OK) return st;
     if (!use_megakernel())
-        return launch_bands_wave(s, cam, depth, band_rows, rank, world, d_rgb, d_counters, stream);
+        return launch_bands_wave(s, cam, depth, spp, seed, band_rows, rank, world, d_rgb, d_counters, stream);
+    if (spp != 1) return RT_ERR_UNSUPPORTED;  // the per-pixel megakernel traces one sample
     RenderParams p;
     std::memset(&p, 0, sizeof(p));
     p.S = s->S;
@@ -1146,19 +1148,31 @@ static rt_status launch_bands(rt_scene* s, const rt_camera* cam, uint32_t depth,
 // and leave the parameters (with the device level table) in *forest_params.
 static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
                                uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
-                               hipStream_t stream, WaveParams* forest_params, uint32_t* forest_levels);
+                               hipStream_t stream, WaveParams* forest_params, uint32_t* forest_levels,
+                               uint32_t spp = 1, uint32_t sample = 0, uint32_t seed = 0);
 
-static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
-                                   uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
-                                   hipStream_t stream) {
-    return wave_pipeline(s, s->ws, cam, depth, band_rows, rank, world, d_rgb, d_counters, stream, nullptr, nullptr);
+// spp samples: one pipeline run per sample, in sample order (the level-0 combine adds
+// sample k's colour to the running sum of samples 0..k-1 and the last one divides)
+static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
+                                   uint32_t band_rows, uint32_t rank, uint32_t world, float* d_rgb,
+                                   unsigned long long* d_counters, hipStream_t stream) {
+    for (uint32_t k = 0; k < spp; k++) {
+        rt_status st = wave_pipeline(s, s->ws, cam, depth, band_rows, rank, world, d_rgb, d_counters, stream, nullptr,
+                                     nullptr, spp, k, seed);
+        if (st != RT_OK) return st;
+    }
+    return RT_OK;
 }
 
 static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
                                uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
-                               hipStream_t stream, WaveParams* forest_params, uint32_t* forest_levels) {
+                               hipStream_t stream, WaveParams* forest_params, uint32_t* forest_levels,
+                               uint32_t spp, uint32_t sample, uint32_t seed) {
     WaveParams p;
     std::memset(&p, 0, sizeof(p));
+    p.spp = spp;
+    p.sample = sample;
+    p.seed = seed;
     p.S = s->S;
     p.cam_ox = cam->origin[0];
     p.cam_oy = cam->origin[1];
@@ -1282,7 +1296,8 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     uint32_t levels = depth > 0 ? depth : 1;
     // Every launch sizes itself from the device-side level counts: the whole frame is
     // enqueued without a host round trip (levels past the deepest non-empty one are no-ops).
-    HIP_TRY(launch_wave_init(w.levels, 2 * (RT_MAX_DEPTH + 2), p.total_items, w.overflow, stream));
+    HIP_TRY(launch_wave_init(w.levels, 2 * (RT_MAX_DEPTH + 2), p.total_items, sample == 0 ? w.overflow : nullptr,
+                             stream));
     HIP_TRY(launch_wave_trace(p, 0, tb, stream));
     for (uint32_t k = 1; k < levels; k++) {
         if (sort_tasks) {
@@ -1317,14 +1332,20 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     return RT_OK;
 }
 
-rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* cam, uint32_t depth,
-                                uint32_t band_rows, uint32_t rank, uint32_t world, float* d_rgb,
-                                uint64_t* d_counters, void* stream) {
+rt_status rt_render_bands_spp_async(const rt_scene* scene, const rt_camera* cam, uint32_t depth, uint32_t spp,
+                                    uint32_t seed, uint32_t band_rows, uint32_t rank, uint32_t world, float* d_rgb,
+                                    uint64_t* d_counters, void* stream) {
     rt_scene* s = const_cast<rt_scene*>(scene);
     if (!s) return RT_ERR_INVALID_ARG;
     HIP_TRY(hipSetDevice(s->device));
-    return launch_bands(s, cam, depth, band_rows, rank, world, d_rgb,
+    return launch_bands(s, cam, depth, spp, seed, band_rows, rank, world, d_rgb,
                         reinterpret_cast<unsigned long long*>(d_counters), (hipStream_t)stream);
+}
+
+rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* cam, uint32_t depth,
+                                uint32_t band_rows, uint32_t rank, uint32_t world, float* d_rgb,
+                                uint64_t* d_counters, void* stream) {
+    return rt_render_bands_spp_async(scene, cam, depth, 1, 0, band_rows, rank, world, d_rgb, d_counters, stream);
 }
 
 rt_status rt_unpermute_bands_async(const float* d_gathered, uint32_t x_res, uint32_t y_res,
@@ -1345,8 +1366,13 @@ rt_status rt_quantize_u8_async(const float* d_rgb, size_t n, uint8_t* d_rgb8, vo
 
 rt_status rt_render(const rt_scene* scene, const rt_camera* cam, uint32_t depth, const rt_render_opts* opts,
                     float* rgb, uint8_t* rgb8) {
+    return rt_render_spp(scene, cam, depth, 1, 0, opts, rgb, rgb8);
+}
+
+rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
+                        const rt_render_opts* opts, float* rgb, uint8_t* rgb8) {
     rt_scene* s = const_cast<rt_scene*>(scene);
-    if (!s || !cam || !rgb) return RT_ERR_INVALID_ARG;
+    if (!s || !cam || !rgb || spp == 0) return RT_ERR_INVALID_ARG;
     if (opts && opts->device >= 0 && opts->device != s->device) return RT_ERR_INVALID_ARG;
     HIP_TRY(hipSetDevice(s->device));
     size_t n = (size_t)cam->x_res * cam->y_res * 3;
@@ -1357,7 +1383,7 @@ rt_status rt_render(const rt_scene* scene, const rt_camera* cam, uint32_t depth,
         HIP_TRY(hipMemsetAsync(s->ws.counters, 0, 4 * sizeof(unsigned long long), stream));
         HIP_TRY(hipEventRecord(s->ev0, stream));
         // single device: one "band" holding every row
-        st = launch_bands(s, cam, depth, 8, 0, 1, s->ws.out, s->ws.counters, stream);
+        st = launch_bands(s, cam, depth, spp, seed, 8, 0, 1, s->ws.out, s->ws.counters, stream);
         if (st != RT_OK) return st;
         HIP_TRY(hipEventRecord(s->ev1, stream));
         if (use_megakernel() || !s->ws.overflow) break;

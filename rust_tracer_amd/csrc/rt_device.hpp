@@ -187,6 +187,9 @@ struct WaveParams {
     uint32_t* node_key;                // shape id as the reference records it (cube: inner triangle)
     uint32_t* node_pixel;              // y * width + x of the tree's pixel
     const uint8_t* dirty;              // forest shade: per-pixel mask (null: every pixel)
+    // supersampling (rt_render_spp): this pipeline run traces sample `sample` of `spp`;
+    // level 0 jitters the primary ray (spp > 1) and the level-0 combine accumulates
+    uint32_t spp, sample, seed;
 };
 
 // 15-bit Morton code of a point in the 32^3 grid over [c - r, c + r]^3 (clamped)

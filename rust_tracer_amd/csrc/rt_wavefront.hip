@@ -60,6 +60,22 @@ __device__ __forceinline__ PixelRef pixel_of(const WaveParams& P, uint32_t item)
     return r;
 }
 
+// rt_render_spp's counter hash (include/rt_api.h): jitter in [0, 1) of sample k of a
+// pixel along dimension dim (0: x, 1: y); 24-bit fractions, exact in f32
+__device__ __forceinline__ uint32_t spp_mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ float spp_jitter(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t dim) {
+    uint32_t h = spp_mix32(spp_mix32(seed ^ 0x9e3779b9u) ^ pixel);
+    h = spp_mix32(h ^ spp_mix32(2u * sample + dim + 1u));
+    return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+
 __device__ __forceinline__ uint32_t spread5(uint32_t v) {  // abcde -> a..b..c..d..e
     v = (v | (v << 8)) & 0x0300F00Fu;
     v = (v | (v << 4)) & 0x030C30C3u;
@@ -208,8 +224,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                         node_flags(P.nodes, n, NODE_MISS);
                         active = false;
                     } else {
-                        float x = P.x_min + (float)px.u * P.x_delta;
-                        float y = P.y_max - (float)px.v * P.y_delta;
+                        float fu = (float)px.u, fv = (float)px.v;
+                        if (P.spp > 1) {  // sample `P.sample` of the pixel: (u + jx, v + jy)
+                            fu = fu + spp_jitter(P.seed, pix, P.sample, 0u);
+                            fv = fv + spp_jitter(P.seed, pix, P.sample, 1u);
+                        }
+                        float x = P.x_min + fu * P.x_delta;
+                        float y = P.y_max - fv * P.y_delta;
                         V3 cam = v3(P.cam_ox, P.cam_oy, P.cam_oz);
                         ro = cam;
                         rd = norm(sub(v3(x, y, 0.f), cam));
@@ -473,6 +494,13 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
         if (level == 0) {
             PixelRef px = pixel_of(P, t);
             float* o = P.out + ((size_t)px.lr * P.width + px.u) * 3u;
+            if (P.spp > 1) {  // the f32 sum of the samples in sample order, then / spp
+                if (P.sample > 0) c = v3(o[0] + c.x, o[1] + c.y, o[2] + c.z);
+                if (P.sample + 1 == P.spp) {
+                    const float fs = (float)P.spp;
+                    c = v3(c.x / fs, c.y / fs, c.z / fs);
+                }
+            }
             o[0] = c.x;
             o[1] = c.y;
             o[2] = c.z;
@@ -590,11 +618,11 @@ __global__ void forest_mark_kernel(const uint32_t* node_key, const uint32_t* nod
     }
 }
 
-// levels[] = {0, total_items, 0, ...} (incl. the shadow count), overflow 0
+// levels[] = {0, total_items, 0, ...} (incl. the shadow count), overflow 0 (if given)
 __global__ void wave_init_kernel(uint32_t* levels, uint32_t n_words, uint32_t total_items, uint32_t* overflow) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n_words) levels[i] = (i == 1) ? total_items : 0u;
-    if (i == 0) *overflow = 0u;
+    if (i == 0 && overflow) *overflow = 0u;  // null: keep an earlier sample's overflow
 }
 
 hipError_t launch_wave_init(uint32_t* levels, uint32_t n_words, uint32_t total_items, uint32_t* overflow,

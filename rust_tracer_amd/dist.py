@@ -38,8 +38,9 @@ class FrameTiler:
     """Renders this rank's share of a frame and gathers the frame on rank 0."""
 
     def __init__(self, scene: DeviceScene, width, height, depth, band_rows=8, rank=0, world=1,
-                 device=None):
+                 device=None, spp=1, seed=0):
         self.scene = scene
+        self.spp, self.seed = spp, seed
         self.w, self.h, self.depth = width, height, depth
         self.band_rows, self.rank, self.world = band_rows, rank, world
         self.device = device or torch.device("cuda", torch.cuda.current_device())
@@ -60,7 +61,8 @@ class FrameTiler:
     def render_local(self):
         stream = torch.cuda.current_stream(self.device).cuda_stream
         self.scene.render_bands_async(self.cam, self.depth, self.band_rows, self.rank, self.world,
-                                      self.local.data_ptr(), self.counters.data_ptr(), stream)
+                                      self.local.data_ptr(), self.counters.data_ptr(), stream,
+                                      spp=self.spp, seed=self.seed)
 
     def assemble(self):
         """Gather every rank's bands on rank 0 and restore row order (no-op at world 1)."""

@@ -10,7 +10,8 @@ from tools import make_golden
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.mark.parametrize("name", ["my_scene_64.npz", "bench_128.npz", "forest_64.npz", "synth_small.npz"])
+@pytest.mark.parametrize("name", ["my_scene_64.npz", "bench_128.npz", "forest_64.npz", "synth_small.npz",
+                                  "spp_small.npz"])
 def test_fixture_regenerates_bit_for_bit(name):
     committed = np.load(os.path.join(GOLDEN, name))
     fresh = make_golden.FIXTURES[name]()

@@ -65,12 +65,26 @@ def forest_64():
     return {"rgb_d8": rgb, "tree_sizes_d8": sizes}
 
 
+def spp_small():
+    """Config 5's supersampling (rt_render_spp: counter-hash jitter, seed 3) on small frames."""
+    out = {}
+    rgb, c = OracleScene().render(32, 32, 4, spp=4, seed=3)
+    out["rgb_my_scene"] = rgb
+    out["counters_my_scene"] = np.array([c["node_rays"], c["shadow_rays"], c["pixels"]], np.uint64)
+    d = SceneDesc.synth_config(5)
+    rgb, c = OracleScene(d).render(48, 27, 8, threads=8, spp=4, seed=3)
+    out["rgb_c5"] = rgb
+    out["counters_c5"] = np.array([c["node_rays"], c["shadow_rays"], c["pixels"]], np.uint64)
+    return out
+
+
 FIXTURES = {
     "my_scene_64.npz": my_scene_64,
     "my_scene_256.npz": my_scene_256,
     "bench_128.npz": bench_128,
     "synth_small.npz": synth_small,
     "forest_64.npz": forest_64,
+    "spp_small.npz": spp_small,
 }
 
 
