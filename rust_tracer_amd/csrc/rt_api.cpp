@@ -40,8 +40,8 @@ hipError_t launch_forest_shade(const WaveParams& p, uint32_t level, int blocks, 
 hipError_t launch_forest_mark(const uint32_t* node_key, const uint32_t* node_pixel, const NodeRec* nodes,
                               uint32_t n_nodes, const uint8_t* key_mask, uint32_t n_keys, uint8_t* mark,
                               uint32_t* sizes, hipStream_t stream);
-hipError_t launch_sort16(const uint32_t* levels, int32_t level, uint32_t cap, const uint32_t* keys,
-                         const uint32_t* vals, uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t* vals_out,
+hipError_t launch_sort(const uint32_t* levels, int32_t level, uint32_t cap, uint32_t bits, const uint32_t* keys,
+                       const uint32_t* vals, uint32_t* tmp, uint32_t* vals_out,
                          uint32_t* tile_counts, uint32_t* digit_totals, int blocks, hipStream_t stream);
 uint32_t sort_max_tiles(uint32_t cap);
 }  // namespace rtdev
@@ -689,6 +689,14 @@ uint32_t task_key_mode() {
     const char* e = std::getenv("RT_TASK_KEY");
     return e ? (uint32_t)std::atoi(e) : 1u;
 }
+// 3 / 4: 24-bit keys -- task = face x 8x8 direction cells | 15-bit Morton origin (4:
+// origin-major), shadow = light | 18-bit Morton origin (3 sort passes).  Measured
+// (config 3, 1080p): 1 -> 5.78 ms, 3 -> 6.13, 4 -> 6.42: finer keys scatter the waves.
+// Own-shape shadow pre-test in the trace kernel (default on; RT_SELF_SHADOW=0: off, A/B)
+bool self_shadow_enabled() {
+    const char* e = std::getenv("RT_SELF_SHADOW");
+    return !(e && e[0] == '0');
+}
 
 // Device path: "wave" (level-synchronous, default) or "mega" (per-pixel megakernel),
 // chosen with RT_PIPELINE for A/B measurement.
@@ -1219,6 +1227,7 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     const bool sort_tasks = sort_on && sort_tasks_enabled();
     const bool sort_shadow = sort_on && !(ss && ss[0] == '0');
     p.key_mode = task_key_mode();
+    p.self_shadow = self_shadow_enabled() ? 1u : 0u;
     if (s->count_ops) {  // instrumented kernels; RT_COUNT=trace|shadow: only that kernel's tests
         const char* e = std::getenv("RT_COUNT");
         p.count_mask = !e ? 3u : (std::strcmp(e, "trace") == 0 ? 1u : (std::strcmp(e, "shadow") == 0 ? 2u : 3u));
@@ -1230,6 +1239,12 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     uint32_t lbits = 0;
     while ((1u << lbits) < s->S.n_lights) lbits++;
     p.light_shift = lbits <= 1 ? 15u : (16u - lbits > 15u ? 15u : 16u - lbits);
+    uint32_t task_bits = 16u, shadow_bits = 16u;
+    if (p.key_mode >= 3) {  // light | 18-bit Morton
+        p.light_shift = 18u;
+        task_bits = 24u;
+        shadow_bits = 18u + lbits;
+    }
     if (sort_tasks && w.sort_capacity < w.capacity) {
         for (uint32_t** b : {&w.task_keys, &w.perm}) {
             if (*b) (void)hipFree(*b);
@@ -1251,7 +1266,7 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     }
     // sort scratch: keys + values for the larger queue, its tile counts, digit totals
     const uint32_t sort_cap = std::max(w.capacity, w.shadow_capacity);
-    const size_t sort_words = 2 * (size_t)sort_cap + 256 * (size_t)sort_max_tiles(sort_cap) + 256;
+    const size_t sort_words = 4 * (size_t)sort_cap + 256 * (size_t)sort_max_tiles(sort_cap) + 256;
     if ((sort_tasks || sort_shadow) && w.sort_tmp_words < sort_words) {
         if (w.sort_tmp) (void)hipFree(w.sort_tmp);
         w.sort_tmp = nullptr;
@@ -1259,9 +1274,8 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         HIP_TRY(hipMalloc(&w.sort_tmp, sort_words * sizeof(uint32_t)));
         w.sort_tmp_words = sort_words;
     }
-    uint32_t* tmp_keys = w.sort_tmp;
-    uint32_t* tmp_vals = w.sort_tmp ? w.sort_tmp + sort_cap : nullptr;
-    uint32_t* tile_counts = w.sort_tmp ? w.sort_tmp + 2 * (size_t)sort_cap : nullptr;
+    uint32_t* sort_scratch = w.sort_tmp;
+    uint32_t* tile_counts = w.sort_tmp ? w.sort_tmp + 4 * (size_t)sort_cap : nullptr;
     uint32_t* digit_totals = w.sort_tmp ? tile_counts + 256 * (size_t)sort_max_tiles(sort_cap) : nullptr;
     p.task_keys = sort_tasks ? w.task_keys : nullptr;
     p.perm = nullptr;
@@ -1301,15 +1315,15 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     HIP_TRY(launch_wave_trace(p, 0, tb, stream));
     for (uint32_t k = 1; k < levels; k++) {
         if (sort_tasks) {
-            HIP_TRY(launch_sort16(w.levels, (int32_t)k, w.capacity, w.task_keys, nullptr, tmp_keys, tmp_vals, w.perm,
-                                  tile_counts, digit_totals, 4 * s->num_cus, stream));
+            HIP_TRY(launch_sort(w.levels, (int32_t)k, w.capacity, task_bits, w.task_keys, nullptr, sort_scratch, w.perm,
+                                tile_counts, digit_totals, 4 * s->num_cus, stream));
             p.perm = w.perm;
         }
         HIP_TRY(launch_wave_trace(p, k, tb, stream));
     }
     if (sort_shadow) {
-        HIP_TRY(launch_sort16(w.levels, -1, w.shadow_capacity, w.shadow_keys, w.shadow, tmp_keys, tmp_vals,
-                              w.shadow_sorted, tile_counts, digit_totals, 4 * s->num_cus, stream));
+        HIP_TRY(launch_sort(w.levels, -1, w.shadow_capacity, shadow_bits, w.shadow_keys, w.shadow, sort_scratch,
+                            w.shadow_sorted, tile_counts, digit_totals, 4 * s->num_cus, stream));
         p.shadow_in = w.shadow_sorted;
     }
     HIP_TRY(launch_wave_shadow(p, sb, stream));

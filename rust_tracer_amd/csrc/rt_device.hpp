@@ -190,6 +190,7 @@ struct WaveParams {
     // supersampling (rt_render_spp): this pipeline run traces sample `sample` of `spp`;
     // level 0 jitters the primary ray (spp > 1) and the level-0 combine accumulates
     uint32_t spp, sample, seed;
+    uint32_t self_shadow;              // trace decides shadow rays its own shape settles (A/B: RT_SELF_SHADOW=0)
 };
 
 // 15-bit Morton code of a point in the 32^3 grid over [c - r, c + r]^3 (clamped)

@@ -1,4 +1,4 @@
-// rt_order.hip -- ordering of the ray queues: a 16-bit LSD radix sort sized on the device.
+// rt_order.hip -- ordering of the ray queues: an LSD radix sort sized on the device.
 //
 // The level-synchronous pipeline (rt_wavefront.hip) reorders each level's ray tasks and
 // the frame's shadow rays by a spatial key (direction cell or light, then the Morton code
@@ -11,14 +11,14 @@
 // atomics-based counting sorts are slow here (same-bin atomics from many waves serialise
 // beyond the L2).  This sort reads its extent (offset, count) from the pipeline's level
 // counters, so a whole frame is enqueued without a host round trip, and uses no global
-// atomics.  Two 8-bit passes, each reduce-then-scan:
+// atomics.  One 8-bit pass per key byte (2 for 16-bit keys, 3 for 24), each reduce-then-scan:
 //   count    per 4096-key tile, a digit histogram in LDS -> tile_counts[digit][tile]
 //   scan     per digit, exclusive scan over its tiles (one block per digit) + digit total
 //   scatter  per tile, stable block rank (rocprim::block_radix_rank, wave "match"
 //            algorithm: keys warp-striped, ranks ordered by (wave, item, lane) = index
 //            order) -> position = digit base + the tile's offset within the digit + rank
-// Pass 1 (bits 0-7) writes (key, value) to scratch, pass 2 (bits 8-15) writes only the
-// values to their final place; stability of pass 2 keeps pass 1's order within a digit.
+// Every pass but the last writes (key, value) to scratch; the last writes only the values
+// to their final place; stability keeps the previous passes' order within a digit.
 #include <hip/hip_runtime.h>
 
 #include <rocprim/block/block_radix_rank.hpp>
@@ -167,27 +167,37 @@ __global__ __launch_bounds__(SORT_THREADS) void sort_scatter_kernel(SortRef r, c
 
 uint32_t sort_max_tiles(uint32_t cap) { return (cap + SORT_TILE - 1) / SORT_TILE; }
 
-// Sorts the queue `r` (keys at absolute slots) by 16-bit keys; its values (vals, or the
-// slots themselves when vals == null) land in vals_out at the same offset.  tmp_keys /
-// tmp_vals: r.cap slots each; tile_counts: 256 x sort_max_tiles(r.cap); digit_totals: 256.
-hipError_t launch_sort16(const uint32_t* levels, int32_t level, uint32_t cap, const uint32_t* keys,
-                         const uint32_t* vals, uint32_t* tmp_keys, uint32_t* tmp_vals, uint32_t* vals_out,
-                         uint32_t* tile_counts, uint32_t* digit_totals, int blocks, hipStream_t stream) {
+// Sorts the queue `r` (keys at absolute slots) by `bits`-bit keys (8-bit digits, LSD);
+// its values (vals, or the slots themselves when vals == null) land in vals_out at the
+// same offset.  tmp: 2 x r.cap slots (keys, values) per intermediate buffer -- one for
+// two passes, two (ping-pong) for three or four; tile_counts: 256 x sort_max_tiles(r.cap);
+// digit_totals: 256.
+hipError_t launch_sort(const uint32_t* levels, int32_t level, uint32_t cap, uint32_t bits, const uint32_t* keys,
+                       const uint32_t* vals, uint32_t* tmp, uint32_t* vals_out, uint32_t* tile_counts,
+                       uint32_t* digit_totals, int blocks, hipStream_t stream) {
     const SortRef r{levels, level, cap};
     const uint32_t mt = sort_max_tiles(cap);
     const int nb = (int)std::min<uint32_t>((uint32_t)blocks, mt > 0 ? mt : 1u);
-    // pass 1: bits 0-7, absolute input -> scratch
-    hipLaunchKernelGGL(sort_count_kernel, dim3(nb), dim3(SORT_THREADS), 0, stream, r, keys, 1, 0u, tile_counts, mt);
-    hipLaunchKernelGGL(sort_scan_kernel, dim3(256), dim3(SORT_THREADS), 0, stream, r, tile_counts, mt, digit_totals);
-    hipLaunchKernelGGL(sort_scatter_kernel, dim3(nb), dim3(SORT_THREADS), 0, stream, r, keys, vals, 1, 0u,
-                       (const uint32_t*)tile_counts, mt, (const uint32_t*)digit_totals, tmp_keys, tmp_vals, 0);
-    // pass 2: bits 8-15, scratch -> vals_out (absolute)
-    hipLaunchKernelGGL(sort_count_kernel, dim3(nb), dim3(SORT_THREADS), 0, stream, r, (const uint32_t*)tmp_keys, 0,
-                       8u, tile_counts, mt);
-    hipLaunchKernelGGL(sort_scan_kernel, dim3(256), dim3(SORT_THREADS), 0, stream, r, tile_counts, mt, digit_totals);
-    hipLaunchKernelGGL(sort_scatter_kernel, dim3(nb), dim3(SORT_THREADS), 0, stream, r, (const uint32_t*)tmp_keys,
-                       (const uint32_t*)tmp_vals, 0, 8u, (const uint32_t*)tile_counts, mt,
-                       (const uint32_t*)digit_totals, (uint32_t*)nullptr, vals_out, 1);
+    const uint32_t passes = std::max(1u, std::min(4u, (bits + 7u) / 8u));
+    const uint32_t* kin = keys;
+    const uint32_t* vin = vals;
+    int in_abs = 1;
+    for (uint32_t p = 0; p < passes; p++) {
+        const uint32_t shift = 8u * p;
+        const bool last = p + 1 == passes;
+        uint32_t* kout = last ? nullptr : tmp + (size_t)(p & 1u) * 2u * cap;
+        uint32_t* vout = last ? vals_out : kout + cap;
+        hipLaunchKernelGGL(sort_count_kernel, dim3(nb), dim3(SORT_THREADS), 0, stream, r, kin, in_abs, shift,
+                           tile_counts, mt);
+        hipLaunchKernelGGL(sort_scan_kernel, dim3(256), dim3(SORT_THREADS), 0, stream, r, tile_counts, mt,
+                           digit_totals);
+        hipLaunchKernelGGL(sort_scatter_kernel, dim3(nb), dim3(SORT_THREADS), 0, stream, r, kin, vin, in_abs, shift,
+                           (const uint32_t*)tile_counts, mt, (const uint32_t*)digit_totals, kout, vout,
+                           last ? 1 : 0);
+        kin = kout;
+        vin = vout;
+        in_abs = 0;  // scratch buffers are relative to the queue's offset
+    }
     return hipGetLastError();
 }
 

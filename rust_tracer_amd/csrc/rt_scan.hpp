@@ -25,7 +25,7 @@
 #define RT_STATS 0
 #endif
 #if RT_STATS
-__device__ unsigned long long rt_scan_stats[8];
+__device__ unsigned long long rt_scan_stats[16];
 #define RT_STAT(i) do { if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == \
     (uint32_t)__builtin_ctzll(__ballot(1))) atomicAdd(&rt_scan_stats[i], 1ull); } while (0)
 #else
@@ -516,6 +516,15 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
     uint32_t sp = 0;
     uint32_t cur = S.bvh_root;
     bool done = SHADOW ? shadow_decided(o, d, bt, l2) : false;
+#if RT_STATS
+    // lanes whose own box test admitted the current node (stats build only)
+    __shared__ uint64_t rt_need_stack[4 * 32];
+    uint64_t* nstk = rt_need_stack + ((threadIdx.x >> 6) << 5);
+    uint64_t need = __ballot(1);
+#define RT_NEED(x) x
+#else
+#define RT_NEED(x)
+#endif
     for (;;) {
         // the lane's limit: its best t (a plane's t < 0 beats everything: no votes), the
         // light for shadow rays, nothing once decided
@@ -523,6 +532,17 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
         float tnode = (tmax < 0.f) ? -__builtin_huge_valf() : tmax + R.m;
         RT_T0(C, t_it);
         if (cur & BVH_LEAF) {
+#if RT_STATS
+            {
+                uint64_t act = __ballot(SHADOW ? !done : true);
+                if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == (uint32_t)__builtin_ctzll(__ballot(1))) {
+                    const int sb = SHADOW ? 8 : 5;  // trace walks: slots 5-7, shadow walks: 8-10
+                    atomicAdd(&rt_scan_stats[sb], (unsigned long long)__builtin_popcountll(act));
+                    atomicAdd(&rt_scan_stats[sb + 1], (unsigned long long)__builtin_popcountll(act & need));
+                    atomicAdd(&rt_scan_stats[sb + 2], 1ull);
+                }
+            }
+#endif
             bvh_leaf(S, cur & ~BVH_LEAF, o, d, R.on, tmax, bt, bk, c);
             RT_T1(C, c, cyc_leaf, t_it);
             if (SHADOW) {
@@ -554,20 +574,24 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
                 uint32_t axis = __float_as_uint(q3.z);
                 float da = rfl(axis == 0 ? d.x : (axis == 1 ? d.y : d.z));
                 bool b_first = da < 0.f;  // child A holds the lower centroids
+                RT_NEED(nstk[sp] = __ballot(b_first ? hA : hB); need = __ballot(b_first ? hB : hA);)
                 stk[sp++] = b_first ? cA : cB;
                 cur = b_first ? cB : cA;
                 continue;
             }
             if (anyA) {
+                RT_NEED(need = __ballot(hA);)
                 cur = cA;
                 continue;
             }
             if (anyB) {
+                RT_NEED(need = __ballot(hB);)
                 cur = cB;
                 continue;
             }
         }
         if (sp == 0) break;
+        RT_NEED(need = nstk[sp - 1];)
         cur = rfl(stk[--sp]);
     }
 }

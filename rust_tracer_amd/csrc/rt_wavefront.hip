@@ -92,7 +92,22 @@ __device__ __forceinline__ uint32_t morton15(const DevScene& S, V3 p) {
 __device__ __forceinline__ uint32_t octant(V3 d) {
     return (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u);
 }
-// task ordering key: 16 bits
+__device__ __forceinline__ uint32_t spread6(uint32_t v) {  // abcdef -> a..b..c..d..e..f
+    v = (v | (v << 8)) & 0x0000F00Fu;
+    v = (v | (v << 4)) & 0x000C30C3u;
+    v = (v | (v << 2)) & 0x00249249u;
+    return v;
+}
+// 18-bit Morton code over the 64^3 grid of the same cube
+__device__ __forceinline__ uint32_t morton18(const DevScene& S, V3 p) {
+    float sc = 32.f / S.bvh_r;
+    int x = (int)fminf(fmaxf((p.x - S.bvh_cx) * sc + 32.f, 0.f), 63.f);
+    int y = (int)fminf(fmaxf((p.y - S.bvh_cy) * sc + 32.f, 0.f), 63.f);
+    int z = (int)fminf(fmaxf((p.z - S.bvh_cz) * sc + 32.f, 0.f), 63.f);
+    return (spread6((uint32_t)x) << 2) | (spread6((uint32_t)y) << 1) | spread6((uint32_t)z);
+}
+
+// task ordering key: 16 bits (modes 0-2) or 24 bits (mode 3)
 __device__ __forceinline__ uint32_t task_key(const WaveParams& P, V3 o, V3 d) {
     if (P.key_mode == 0) return (octant(d) << 13) | (morton15(P.S, o) >> 2);  // 16 bits: 2 radix passes
     // cube-map face of d (3 bits) x 2x2 cells of the face (2 bits) | 13-bit coarse origin
@@ -102,6 +117,14 @@ __device__ __forceinline__ uint32_t task_key(const WaveParams& P, V3 o, V3 d) {
     if (ax >= ay && ax >= az) { face = d.x < 0.f; u = d.y; v = d.z; m = ax; }
     else if (ay >= az) { face = 2u + (d.y < 0.f); u = d.x; v = d.z; m = ay; }
     else { face = 4u + (d.z < 0.f); u = d.x; v = d.y; m = az; }
+    if (P.key_mode >= 3) {  // face x 8x8 cells (< 384) and the 15-bit Morton origin
+        float iu = u / m, iv = v / m;  // in [-1, 1]
+        uint32_t qu = (uint32_t)fminf(fmaxf((iu + 1.f) * 4.f, 0.f), 7.f);
+        uint32_t qv = (uint32_t)fminf(fmaxf((iv + 1.f) * 4.f, 0.f), 7.f);
+        uint32_t dir = (face << 6) | (qu << 3) | qv;
+        if (P.key_mode == 4) return (morton15(P.S, o) << 9) | dir;  // origin-major
+        return (dir << 15) | morton15(P.S, o);
+    }
     if (P.key_mode == 2) {  // face x 4x4 cells (< 96) | 9-bit coarse origin
         float iu = u / m, iv = v / m;  // in [-1, 1]
         uint32_t qu = (uint32_t)fminf(fmaxf((iu + 1.f) * 2.f, 0.f), 3.f);
@@ -182,6 +205,31 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, uint32_t n, u
     return base + mine;
 }
 
+// The shading point's own shape, tested first for its shadow rays (trace kernel): the
+// same arithmetic the scan runs for it (sph_general / the triangle test; bit-identical
+// results up to the sign of a zero t, which no distance test can see).  Cubes are left
+// to the shadow pass.
+template <class C>
+__device__ __forceinline__ void own_shape_test(const DevScene& S, uint32_t key, V3 o, V3 d, float& bt, uint32_t& bk,
+                                               C& c) {
+    const ShapeRec& R = S.shapes[key >> 4];
+    if (R.kind == RT_SHAPE_SPHERE) {
+        RT_OPS(c, gsph);
+        Rec16 q;
+        q.r0 = ld4(R.inv);
+        q.r1 = ld4(R.inv + 4);
+        q.r2 = ld4(R.inv + 8);
+        q.rk = make_float4(__uint_as_float(key & ~15u), 0.f, 0.f, 0.f);
+        sph_general(q, o, d, bt, bk);
+    } else if (R.kind == RT_SHAPE_TRIANGLE) {
+        RT_OPS(c, tri);
+        float t, u, v, det;
+        if (tri_hit(o, d, v3(R.a[0], R.a[1], R.a[2]), v3(R.a[3], R.a[4], R.a[5]), v3(R.a[6], R.a[7], R.a[8]), t, u,
+                    v, det))
+            take(t, key & ~15u, bt, bk);
+    }
+}
+
 #ifndef RT_TRACE_WAVES
 #define RT_TRACE_WAVES 5  // 96 VGPRs, 20 B scratch (measured: 4 -> 8.02 ms, 5 -> 7.89, 6 -> 7.85 with 84 B)
 #endif
@@ -194,13 +242,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
     const uint32_t next_off = off + count;
     if (blockIdx.x == 0 && threadIdx.x == 0) P.levels[2 * (level + 1)] = next_off;
     const uint32_t lane = lane_id();
-    uint32_t n_node = 0, n_pix = 0;
+    uint32_t n_node = 0, n_pix = 0, n_pre = 0;
     typename std::conditional<COUNT, ScanCnt, NoCnt>::type cnt;
     if constexpr (COUNT) cnt_init(cnt);
     bc_init();
     // point lights: one shadow ray each per hit (mod.rs:189-206); ambient lights: none
-    uint32_t n_point = 0;
-    for (int li = 0; li < S.n_lights; ++li) n_point += S.lights[li].kind == RT_LIGHT_POINT ? 1u : 0u;
 
     const uint32_t stride = gridDim.x * blockDim.x;
     // whole waves iterate together so the wave-aggregated appends see every lane
@@ -245,6 +291,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
             }
         }
         bool want_refl = false, want_refr = false, hit = false;
+        uint32_t decided = 0;  // point lights whose shadow ray the own-shape test settled
         uint32_t mort = 0;  // Morton code of the shadow-ray origin (queue ordering key)
         V3 rro = v3(0, 0, 0), rrd = v3(0, 0, 0), tro = v3(0, 0, 0), trd = v3(0, 0, 0);
         if (active) {
@@ -265,11 +312,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 V3 kd = tex_eval(M.diffuse, h.tu, h.tv);
                 V3 ks = tex_eval(M.specular, h.tu, h.tv);
                 V3 ps = add(h.p, mul(h.n, 0.0002f));  // render.rs:147
-                if (P.shadow_keys) mort = morton15(S, ps);
+                if (P.shadow_keys) mort = P.key_mode >= 3 ? morton18(S, ps) : morton15(S, ps);
                 uint32_t flags = NODE_HIT;
                 float fr = 0.f, dr = 0.f, pw = 0.f, ft = 0.f;
                 P.node_ps[n] = make_float4(ps.x, ps.y, ps.z, 0.f);
-                P.node_lit[n] = 0u;
+                // PointLight::get_energy (mod.rs:189-206) decided here when the planes and
+                // the shape just hit settle it: a plane's t < 0 is the nearest hit; else any
+                // hit nearer than the light means the nearest one is too (shadow_scan)
+                uint32_t lit_pre = 0u;
+                if (P.self_shadow) {
+                    for (int li = 0; li < S.n_lights; ++li) {
+                        const LightRec& L = S.lights[li];
+                        if (L.kind != RT_LIGHT_POINT) continue;
+                        const V3 lpos = v3(L.px, L.py, L.pz);
+                        const V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
+                        const float l2 = len2(sub(lpos, ps));
+                        float st = __builtin_huge_valf();
+                        uint32_t sk = 0xFFFFFFFFu;
+                        planes(S, ps, ldir, st, sk, cnt);
+                        if (!(st < 0.f)) own_shape_test(S, bk, ps, ldir, st, sk, cnt);
+                        if (shadow_decided(ps, ldir, st, l2)) {
+                            decided |= 1u << li;
+                            if (!shadow_hit(ps, ldir, st, l2)) lit_pre |= 1u << li;
+                        }
+                    }
+                    n_pre += (uint32_t)__builtin_popcount(decided);
+                }
+                P.node_lit[n] = lit_pre;
                 if (P.node_aux) {  // ray forest: what render_ray_tree re-reads at shade time
                     P.node_aux[n] = make_float4(__uint_as_float((uint32_t)h.mat), h.tu, h.tv,
                                                 __uint_as_float(h.entering ? 1u : 0u));
@@ -352,22 +421,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         // holds rays from neighbouring points towards ONE light
         uint64_t hits = __ballot(hit);
         if (hits) {
-            uint32_t nh = (uint32_t)__builtin_popcountll(hits);
-            uint32_t rank_h = (uint32_t)__builtin_popcountll(hits & lanemask_lt());
+            // entries still to trace: per point light, the hit lanes it was not decided for
+            uint32_t total = 0;
+            for (int li = 0; li < S.n_lights; ++li)
+                if (S.lights[li].kind == RT_LIGHT_POINT)
+                    total += (uint32_t)__builtin_popcountll(__ballot(hit && !((decided >> li) & 1u)));
             uint32_t first = (uint32_t)__builtin_ctzll(hits);
             uint32_t sbase = 0;
-            if (lane == first) sbase = atomicAdd(&RT_SHADOW_COUNT(P), nh * n_point);
+            if (lane == first && total) sbase = atomicAdd(&RT_SHADOW_COUNT(P), total);
             sbase = (uint32_t)__builtin_amdgcn_readlane((int)sbase, (int)first);
-            if (hit) {
-                uint32_t k = 0;
-                for (int li = 0; li < S.n_lights; ++li) {
-                    if (S.lights[li].kind != RT_LIGHT_POINT) continue;
-                    uint32_t slot = sbase + k * nh + rank_h;
-                    k++;
+            uint32_t group = 0;  // entries of the earlier lights
+            for (int li = 0; li < S.n_lights; ++li) {
+                if (S.lights[li].kind != RT_LIGHT_POINT) continue;
+                const bool want = hit && !((decided >> li) & 1u);
+                const uint64_t m = __ballot(want);
+                const uint32_t slot = sbase + group + (uint32_t)__builtin_popcountll(m & lanemask_lt());
+                group += (uint32_t)__builtin_popcountll(m);
+                if (want) {
                     if (slot < P.shadow_capacity) {
                         P.shadow[slot] = (n << 5) | (uint32_t)li;
                         if (P.shadow_keys)
-                            P.shadow_keys[slot] = ((uint32_t)li << P.light_shift) | (mort >> (15u - P.light_shift));
+                            P.shadow_keys[slot] = P.key_mode >= 3 ? (((uint32_t)li << 18) | mort)
+                                                                  : ((uint32_t)li << P.light_shift) | (mort >> (15u - P.light_shift));
                     } else
                         atomicOr(P.overflow, 2u);
                 }
@@ -377,10 +452,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
     for (int o = 32; o > 0; o >>= 1) {
         n_node += __shfl_xor(n_node, o);
         n_pix += __shfl_xor(n_pix, o);
+        n_pre += __shfl_xor(n_pre, o);
     }
     if (lane == 0) {
         if constexpr (COUNT) bc_scan(cnt);
         bc_add(RT_OPS_N + 0, n_node);
+        bc_add(RT_OPS_N + 1, n_pre);  // shadow rays decided here count as shadow scans
         bc_add(RT_OPS_N + 2, n_pix);
     }
     bc_flush(ops_slot(S), P.ray_counters);
@@ -688,11 +765,11 @@ hipError_t launch_wave_combine(const WaveParams& p, uint32_t level, int blocks, 
 
 #if RT_STATS
 // tools/scan_stats.py: read (and optionally reset) the wavefront pipeline's scan counters
-extern "C" int rt_debug_scan_stats(unsigned long long* out8, int reset) {
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(rtdev::rt_scan_stats), 8 * sizeof(unsigned long long)) != hipSuccess)
+extern "C" int rt_debug_scan_stats(unsigned long long* out16, int reset) {
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(rtdev::rt_scan_stats), 16 * sizeof(unsigned long long)) != hipSuccess)
         return 1;
     if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[16] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(rtdev::rt_scan_stats), z, sizeof(z)) != hipSuccess) return 1;
     }
     return 0;

@@ -14,9 +14,9 @@ L = abi.lib()
 L.rt_debug_scan_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 s = DeviceScene(SceneDesc.synth_config(cfg))
 s.render(1920, 1080, 1)
-st = (C.c_ulonglong * 8)()
+st = (C.c_ulonglong * 16)()
 L.rt_debug_scan_stats(st, 1)
-prev = [0] * 8
+prev = [0] * 16
 prev_scans = 0
 names = ["wave-scans", "dsph-pair solve", "gsph solve", "tri-pair finish", "cube-tri pass"]
 print(f"config {cfg}: per level, hit-path entries per wave-scan")
