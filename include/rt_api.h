@@ -221,10 +221,11 @@ uint64_t rt_scene_device_bytes(const rt_scene* scene);
  * since the last reset, in this order: child-box pairs, diagonal-sphere pairs, general
  * spheres, triangle pairs, cube boxes, full cubes (12 triangles), grazing cone tests
  * (blocks of 8 triangles), planes, grazing normal tests (blocks of 8); then shader-clock
- * cycles per wave in child-box tests, leaf tests, the grazing pass and whole scans.
+ * cycles per wave in child-box tests, leaf tests, the grazing pass and whole scans, and
+ * in the trace kernel's ray fetch, post-scan work and own-shape shadow tests.
  * Synchronises the device; reset != 0 zeroes the counts after reading.  `out` may be
  * NULL. */
-#define RT_SCAN_OPS_N 13
+#define RT_SCAN_OPS_N 16
 rt_status rt_scene_scan_ops(rt_scene* scene, uint64_t* out, uint32_t n, int32_t reset);
 
 /* Counting is instrumentation: renders after rt_scene_set_scan_counting(scene, 1) run

@@ -157,6 +157,16 @@ class SceneDesc:
         check(lib().rt_synth_config(config, C.byref(p)), "rt_synth_config")
         return cls._from_builder(lib().rt_desc_synth, C.byref(p))
 
+    def editable(self):
+        """A Python-assembled copy (shapes / lights / materials can be appended)."""
+        d = SceneDesc()
+        src = self.ptr().contents
+        d.materials = [abi.rt_material.from_buffer_copy(src.materials[i]) for i in range(src.n_materials)]
+        d.shapes = [abi.rt_shape.from_buffer_copy(src.shapes[i]) for i in range(src.n_shapes)]
+        d.lights = [abi.rt_light.from_buffer_copy(src.lights[i]) for i in range(src.n_lights)]
+        d.ambient = (src.ambient.r, src.ambient.g, src.ambient.b)
+        return d
+
     # ---- assembled in Python
     def phong(self, ambient, diffuse, specular, power, reflectivity, refraction_index):
         self.materials.append(phong_material(ambient, diffuse, specular, power, reflectivity,
@@ -262,7 +272,8 @@ class DeviceScene:
         return bool(self._L.rt_scene_uses_bvh(self.h))
 
     SCAN_OPS = ("node_pairs", "dsph_pairs", "gsph", "tri_pairs", "cube_boxes", "cubes", "graze_cones",
-                "planes", "graze_normals", "cycles_nodes", "cycles_leaves", "cycles_graze", "cycles_scans")
+                "planes", "graze_normals", "cycles_nodes", "cycles_leaves", "cycles_graze", "cycles_scans",
+                "cycles_load", "cycles_post", "cycles_self")
 
     def set_scan_counting(self, enable=True):
         """Run the instrumented (counting) kernels from now on (rt_scene_set_scan_counting)."""

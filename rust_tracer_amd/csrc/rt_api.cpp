@@ -177,9 +177,18 @@ struct CubeIn {
     float key;
 };
 
+// A hierarchy primitive as the light buffers see it: bounding ball and the run record
+// that tests it (LB_* type << 30 | record index).
+enum : uint32_t { LB_DSPH = 0, LB_GSPH = 1, LB_TRI = 2, LB_CUBE = 3 };
+struct LbPrim {
+    double c[3], r;
+    uint32_t code;
+};
+
 struct RunLayout {
     std::vector<float> dsph, gsph, tri, cube, nodes, graze_blk, graze_tri;
     std::vector<uint32_t> leaves;
+    std::vector<LbPrim> lb_prims;  // every hierarchy primitive (light buffers)
     uint32_t root = BVH_LEAF;
     bool use = false;
     int n_dsph_bvh = 0, n_gsph_bvh = 0, n_tri_bvh = 0, n_cube_bvh = 0;
@@ -423,6 +432,163 @@ void build_graze(const std::vector<TriIn>& tris, const std::vector<char>& in_tri
 
 // Lays out the runs: hierarchy primitives leaf by leaf, then the linear rest.  Within
 // a leaf diag spheres pair up (an odd one joins the general run), triangles pair up.
+// Light buffers (shadow rays; DESIGN.md "Light buffers").  Per point light, a cube map
+// of R x R cells per face over the directions from the light; cell c lists every
+// hierarchy record with a primitive whose ball, grown by the hierarchy's bound h(D_max),
+// subtends (from the light, plus LB_MU) a direction inside the cell -- sorted by the
+// ball's nearest distance to the light.  A shadow ray toward the light whose origin has
+// D <= D_max and distance to the light <= LB_LMAX can only get a hit that shadows from a
+// primitive listed in the cell of its direction: such a hit point X lies on the ray
+// within h(D) of the primitive, between the origin and the light, and the direction
+// lpos -> X is within |delta d| (1 + Lambda / rho) <= LB_MU / 2 of -d (|delta d| <= 1e-6,
+// the rounding of d = norm(lpos - o); |X - lpos| >= rho = LB_RHO since no grown ball
+// comes nearer the light: else the light gets no buffer).
+constexpr double LB_MU = 2e-3, LB_RHO = 0.05;  // LB_LMAX: RT_LB_LMAX (rt_device.hpp)
+
+// Each cell becomes a leaf record of the hierarchy's leaf table whose runs are copies
+// of the listed records (appended to the run arrays after the linear rest), so a cell is
+// tested exactly like a leaf (prefetching run loops).
+struct LightBuffers {
+    uint32_t res = 0;
+    std::vector<uint32_t> base;     // per light: leaf index of its first cell, or ~0 (no buffer)
+    float dmax = 0.f;
+};
+
+// the cube-map cell of direction v (same face / axis conventions as rt_scan.hpp lb_cell)
+static void lb_face_dir(int f, double a, double b, double out[3]) {
+    const int k = f >> 1;
+    const double s = (f & 1) ? -1.0 : 1.0;
+    const int u = k == 0 ? 1 : 0, v = k == 2 ? 1 : 2;
+    out[k] = s;
+    out[u] = a;
+    out[v] = b;
+    const double l = std::sqrt(out[0] * out[0] + out[1] * out[1] + out[2] * out[2]);
+    for (int i = 0; i < 3; i++) out[i] /= l;
+}
+
+void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, LightBuffers& B) {
+    const char* e = std::getenv("RT_LB_RES");  // cells per face side; 0: no light buffers (A/B)
+    const int R = e ? std::atoi(e) : 32;
+    B.base.assign(lights.size(), 0xFFFFFFFFu);
+    if (!L.use || R <= 0 || R > 1024 || L.lb_prims.empty()) return;
+    B.res = (uint32_t)R;
+    // origins farther than D_max from the scene ball's centre (+ R) use the hierarchy walk
+    const double dmax = 3.0 * (double)L.r;
+    B.dmax = down_f(dmax);
+    const double hmax = ((double)L.g2 * dmax + (double)L.g1) * dmax + (double)L.g0;
+    // cell centres and angular radii (max angle to a corner, +1%)
+    const int nc = 6 * R * R;
+    std::vector<double> cdir(3 * (size_t)nc), ccos(nc), csin(nc), crad(nc);
+    for (int f = 0; f < 6; f++)
+        for (int j = 0; j < R; j++)
+            for (int i = 0; i < R; i++) {
+                const size_t c = ((size_t)f * R + j) * R + i;
+                const double a0 = -1.0 + 2.0 * i / R, a1 = -1.0 + 2.0 * (i + 1) / R;
+                const double b0 = -1.0 + 2.0 * j / R, b1 = -1.0 + 2.0 * (j + 1) / R;
+                double m[3], q[3];
+                lb_face_dir(f, 0.5 * (a0 + a1), 0.5 * (b0 + b1), m);
+                double rad = 0;
+                for (double a : {a0, a1})
+                    for (double b : {b0, b1}) {
+                        lb_face_dir(f, a, b, q);
+                        rad = std::max(rad, std::acos(std::min(1.0, m[0] * q[0] + m[1] * q[1] + m[2] * q[2])));
+                    }
+                rad = rad * 1.01 + 1e-6;
+                for (int k = 0; k < 3; k++) cdir[3 * c + k] = m[k];
+                ccos[c] = std::cos(rad);
+                csin[c] = std::sin(rad);
+                crad[c] = rad;
+            }
+    const double PI = 3.14159265358979323846;
+    const double FACE_HALF = 0.9556;  // a face's directions lie within 54.75 deg of its axis
+    for (size_t li = 0; li < lights.size(); li++) {
+        if (lights[li].kind != RT_LIGHT_POINT) continue;
+        const double lp[3] = {lights[li].px, lights[li].py, lights[li].pz};
+        struct Cone {
+            double u[3], alpha, ca, sa, near;
+            uint32_t code;
+        };
+        std::vector<Cone> cones;
+        bool ok = true;
+        for (const LbPrim& p : L.lb_prims) {
+            double w[3] = {p.c[0] - lp[0], p.c[1] - lp[1], p.c[2] - lp[2]};
+            const double dist = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+            const double rr = (p.r + hmax) * (1 + 1e-6);
+            if (!(dist - rr >= LB_RHO)) {  // a primitive (nearly) at the light: no buffer
+                ok = false;
+                break;
+            }
+            Cone c;
+            for (int k = 0; k < 3; k++) c.u[k] = w[k] / dist;
+            c.alpha = std::asin(rr / dist) + LB_MU;
+            c.ca = std::cos(c.alpha);
+            c.sa = std::sin(c.alpha);
+            c.near = dist - rr;
+            c.code = p.code;
+            cones.push_back(c);
+        }
+        if (!ok) continue;
+        // nearest first: every cell's list comes out sorted by distance from the light
+        std::stable_sort(cones.begin(), cones.end(), [](const Cone& a, const Cone& b) { return a.near < b.near; });
+        std::vector<std::vector<std::pair<uint32_t, double>>> lists(nc);
+        for (const Cone& c : cones) {
+            for (int f = 0; f < 6; f++) {
+                const int k = f >> 1;
+                const double s = (f & 1) ? -1.0 : 1.0;
+                const double ax_ang = std::acos(std::max(-1.0, std::min(1.0, s * c.u[k])));
+                if (ax_ang > c.alpha + FACE_HALF + 1e-3) continue;
+                for (int cc = f * R * R; cc < (f + 1) * R * R; cc++) {
+                    bool in = c.alpha + crad[cc] >= PI;
+                    if (!in) {
+                        // angle(u, cell centre) <= alpha + cell radius  <=>  dot >= cos(alpha + rad)
+                        const double dt =
+                            c.u[0] * cdir[3 * cc] + c.u[1] * cdir[3 * cc + 1] + c.u[2] * cdir[3 * cc + 2];
+                        in = dt >= c.ca * ccos[cc] - c.sa * csin[cc] - 1e-12;
+                    }
+                    if (in) {
+                        auto& l = lists[cc];
+                        bool dup = false;  // a sphere / triangle pair's partner: keep the first entry
+                        for (const auto& q : l) dup = dup || q.first == c.code;
+                        if (!dup) l.push_back(std::make_pair(c.code, c.near));
+                    }
+                }
+            }
+        }
+        const uint32_t base = (uint32_t)(L.leaves.size() / 8);
+        for (int cc = 0; cc < nc; cc++) {
+            std::vector<uint32_t> by[4];
+            for (const auto& q : lists[cc]) by[q.first >> 30].push_back(q.first & 0x3FFFFFFFu);
+            uint32_t rec[8];
+            rec[0] = (uint32_t)(L.dsph.size() / 16);
+            for (uint32_t r : by[LB_DSPH]) {
+                std::vector<float> t(L.dsph.begin() + 16 * (size_t)r, L.dsph.begin() + 16 * (size_t)r + 16);
+                L.dsph.insert(L.dsph.end(), t.begin(), t.end());
+            }
+            rec[1] = (uint32_t)(L.dsph.size() / 16);
+            rec[2] = (uint32_t)(L.gsph.size() / 16);
+            for (uint32_t r : by[LB_GSPH]) {
+                std::vector<float> t(L.gsph.begin() + 16 * (size_t)r, L.gsph.begin() + 16 * (size_t)r + 16);
+                L.gsph.insert(L.gsph.end(), t.begin(), t.end());
+            }
+            rec[3] = (uint32_t)(L.gsph.size() / 16);
+            rec[4] = (uint32_t)(L.tri.size() / 24);
+            for (uint32_t r : by[LB_TRI]) {
+                std::vector<float> t(L.tri.begin() + 24 * (size_t)r, L.tri.begin() + 24 * (size_t)r + 24);
+                L.tri.insert(L.tri.end(), t.begin(), t.end());
+            }
+            rec[5] = (uint32_t)(L.tri.size() / 24);
+            rec[6] = (uint32_t)(L.cube.size() / 16);
+            for (uint32_t r : by[LB_CUBE]) {
+                std::vector<float> t(L.cube.begin() + 16 * (size_t)r, L.cube.begin() + 16 * (size_t)r + 16);
+                L.cube.insert(L.cube.end(), t.begin(), t.end());
+            }
+            rec[7] = (uint32_t)(L.cube.size() / 16);
+            L.leaves.insert(L.leaves.end(), rec, rec + 8);
+        }
+        B.base[li] = base;
+    }
+}
+
 void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, const std::vector<CubeIn>& cubes,
                 bool enable, RunLayout& L) {
     using namespace rtbvh;
@@ -574,17 +740,35 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
             put4(L.nodes, up_f(n.hi[0][1]), up_f(n.hi[1][1]), up_f(n.hi[0][2]), up_f(n.hi[1][2]));
             put4(L.nodes, keyf(n.child[0]), keyf(n.child[1]), keyf(n.axis), 0.f);
         }
+        auto lb_add = [&](uint32_t pi, uint32_t type, size_t rec) {
+            const Geo& g = geo[pi];
+            L.lb_prims.push_back(LbPrim{{g.c[0], g.c[1], g.c[2]}, g.r, (type << 30) | (uint32_t)rec});
+        };
         for (const auto& leaf : T.leaves) {
             std::vector<const SphIn*> ds, gs;
             std::vector<const TriIn*> ts;
             std::vector<uint32_t> cs;
+            std::vector<uint32_t> dsi, gsi, tsi, csi;  // their prim indices
             for (uint32_t pi : leaf) {
                 const Prim& p = prims[pi];
-                if (p.kind == P_DSPH) ds.push_back(&sph[p.id]);
-                else if (p.kind == P_GSPH) gs.push_back(&sph[p.id]);
-                else if (p.kind == P_TRI) ts.push_back(&tris[p.id]);
-                else cs.push_back(p.id);
+                if (p.kind == P_DSPH) {
+                    ds.push_back(&sph[p.id]);
+                    dsi.push_back(pi);
+                } else if (p.kind == P_GSPH) {
+                    gs.push_back(&sph[p.id]);
+                    gsi.push_back(pi);
+                } else if (p.kind == P_TRI) {
+                    ts.push_back(&tris[p.id]);
+                    tsi.push_back(pi);
+                } else {
+                    cs.push_back(p.id);
+                    csi.push_back(pi);
+                }
             }
+            for (size_t k = 0; k < dsi.size(); k++) lb_add(dsi[k], LB_DSPH, L.dsph.size() / 16 + k / 2);
+            for (size_t k = 0; k < gsi.size(); k++) lb_add(gsi[k], LB_GSPH, L.gsph.size() / 16 + k);
+            for (size_t k = 0; k < tsi.size(); k++) lb_add(tsi[k], LB_TRI, L.tri.size() / 24 + k / 2);
+            for (size_t k = 0; k < csi.size(); k++) lb_add(csi[k], LB_CUBE, L.cube.size() / 16 + k);
             if (ds.size() & 1) ds.push_back(ds.back());  // testing a sphere twice changes nothing
             uint32_t rec[8];
             rec[0] = (uint32_t)(L.dsph.size() / 16);
@@ -935,9 +1119,25 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
                 return RT_ERR_INVALID_ARG;
         }
     }
+    if (d->n_lights > 32) return RT_ERR_UNSUPPORTED;  // shadow results are a 32-bit mask per node
+    uint32_t n_point = 0;
+    std::vector<LightRec> lights(d->n_lights);
+    for (uint32_t i = 0; i < d->n_lights; i++) {
+        const rt_light& l = d->lights[i];
+        if (l.kind != RT_LIGHT_POINT && l.kind != RT_LIGHT_AMBIENT) return RT_ERR_INVALID_ARG;
+        lights[i] = LightRec{l.kind, l.pos[0], l.pos[1], l.pos[2], l.color.r, l.color.g, l.color.b, 0xFFFFFFFFu};
+        if (l.kind == RT_LIGHT_POINT) n_point++;
+    }
     // ---- culling hierarchy and the run layout (leaf order first, then the linear rest)
     RunLayout lay;
     build_runs(sph_in, tri_in, cube_in, bvh_enabled(), lay);
+    // light buffers append cell leaves and record copies to the layout (after the linear
+    // rest: the scan's run counts below exclude them)
+    const int n_dsph_all = (int)(lay.dsph.size() / 16), n_gsph_all = (int)(lay.gsph.size() / 16);
+    const int n_tri_all = (int)(lay.tri.size() / 24), n_cube_all = (int)(lay.cube.size() / 16);
+    LightBuffers lbuf;
+    build_light_buffers(lay, lights, lbuf);
+    for (size_t i = 0; i < lights.size(); i++) lights[i].lb_base = lbuf.base[i];
     dsph.swap(lay.dsph);
     gsph.swap(lay.gsph);
     tri.swap(lay.tri);
@@ -949,16 +1149,6 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
         rt_status r = mat_rec(d->materials[i], mats[i]);
         if (r != RT_OK) return r;
     }
-    if (d->n_lights > 32) return RT_ERR_UNSUPPORTED;  // shadow results are a 32-bit mask per node
-    uint32_t n_point = 0;
-    std::vector<LightRec> lights(d->n_lights);
-    for (uint32_t i = 0; i < d->n_lights; i++) {
-        const rt_light& l = d->lights[i];
-        if (l.kind != RT_LIGHT_POINT && l.kind != RT_LIGHT_AMBIENT) return RT_ERR_INVALID_ARG;
-        lights[i] = LightRec{l.kind, l.pos[0], l.pos[1], l.pos[2], l.color.r, l.color.g, l.color.b, 0.f};
-        if (l.kind == RT_LIGHT_POINT) n_point++;
-    }
-
     // ---- one allocation, 256-B aligned sections
     struct Sec {
         const void* src;
@@ -1005,10 +1195,10 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     S.shapes = (const ShapeRec*)at(6);
     S.mats = (const MatRec*)at(7);
     S.lights = (const LightRec*)at(8);
-    S.n_dsph = (int32_t)(dsph.size() / 16);  // pairs
-    S.n_gsph = (int32_t)(gsph.size() / 16);
-    S.n_tri = (int32_t)(tri.size() / 24);    // pairs
-    S.n_cube = (int32_t)(cube.size() / 16);
+    S.n_dsph = n_dsph_all;  // pairs (light-buffer copies follow)
+    S.n_gsph = n_gsph_all;
+    S.n_tri = n_tri_all;    // pairs
+    S.n_cube = n_cube_all;
     S.n_plane = (int32_t)(plane.size() / 20);
     S.n_shapes = (int32_t)d->n_shapes;
     S.n_lights = (int32_t)d->n_lights;
@@ -1018,6 +1208,8 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     S.graze_blk = (const float4*)at(11);
     S.scan_ops = (unsigned long long*)at(12);
     S.graze_tri = (const float4*)at(13);
+    S.lb_res = lbuf.res;
+    S.lb_dmax = lbuf.dmax;
     S.n_graze_blk = (int32_t)(lay.graze_blk.size() / 32);
     S.bvh_root = lay.root;
     S.n_bvh_nodes = (int32_t)(lay.nodes.size() / 16);

@@ -50,7 +50,8 @@ struct MatRec {
 struct LightRec {
     int32_t kind;
     float px, py, pz;
-    float r, g, b, pad;
+    float r, g, b;
+    uint32_t lb_base;  // first cell of the light's light buffer (DevScene::lb_cells), ~0: none
 };
 
 // Kernel-argument view of an uploaded scene (pointers into the one allocation).
@@ -84,7 +85,12 @@ struct DevScene {
     float bvh_cx, bvh_cy, bvh_cz, bvh_r, bvh_g2, bvh_g1, bvh_g0, bvh_m1, bvh_m0;
     float graze_s2;            // 1.0201: (d.n')^2 < graze_s2 |d|^2 with n' = n / sin(phi_T): the ray grazes
     unsigned long long* scan_ops;  // RT_OPS_* lane-weighted test counts
+    // light buffers (shadow rays; rt_api.cpp build_light_buffers): per point light
+    // 6 x lb_res x lb_res cells, each a leaf of bvh_leaves (LightRec::lb_base + cell)
+    uint32_t lb_res;           // 0: no light buffers
+    float lb_dmax;             // origins with D above it walk the hierarchy
 };
+#define RT_LB_LMAX 45.f        // ... and so do origins farther than this from the light
 
 #define BVH_LEAF 0x80000000u
 // lane-weighted counters of the scan's tests (each += active lanes)
@@ -103,7 +109,11 @@ enum : int {
     RT_OPS_CYC_LEAF = 10,  // ... leaf primitive tests
     RT_OPS_CYC_GRAZE = 11, // ... the grazing pass
     RT_OPS_CYC_SCAN = 12,  // ... whole scans (planes, walk, grazing pass, linear rest)
-    RT_OPS_N = 13,
+    RT_OPS_CYC_LOAD = 13,  // trace kernel: fetching / generating the ray (task gather)
+    RT_OPS_CYC_POST = 14,  // trace kernel: after the scan (attributes, node record, children,
+                           // shadow entries), the own-shape shadow tests excluded
+    RT_OPS_CYC_SELF = 15,  // trace kernel: the own-shape shadow tests
+    RT_OPS_N = 16,
     // scan_ops is RT_OPS_SLOTS x RT_OPS_STRIDE u64: block b adds to slot b % RT_OPS_SLOTS
     // (same-address global atomics from every block would serialise in L2)
     RT_OPS_SLOTS = 64,

@@ -266,7 +266,7 @@ __device__ __forceinline__ void plane_one(cfloat4* r, V3 o, V3 d, float& bt, uin
 struct ScanCnt {
     static constexpr bool kCount = true;
     uint32_t node, dsph, gsph, tri, cube_box, cube, graze, plane, graze_n;
-    uint32_t cyc_node, cyc_leaf, cyc_graze, cyc_scan;
+    uint32_t cyc_node, cyc_leaf, cyc_graze, cyc_scan, cyc_load, cyc_post, cyc_self;
 };
 __device__ __forceinline__ uint32_t rt_clock() { return (uint32_t)__builtin_amdgcn_s_memtime(); }
 // The uncounted variant: the same expressions, every `+=` a no-op (compiled away).
@@ -276,14 +276,14 @@ struct NoCntField {
 struct NoCnt {
     static constexpr bool kCount = false;
     NoCntField node, dsph, gsph, tri, cube_box, cube, graze, plane, graze_n;
-    NoCntField cyc_node, cyc_leaf, cyc_graze, cyc_scan;
+    NoCntField cyc_node, cyc_leaf, cyc_graze, cyc_scan, cyc_load, cyc_post, cyc_self;
 };
 // cycle accounting of the instrumented variant (compiled away otherwise)
 #define RT_T0(C, v) uint32_t v = 0; if constexpr (C::kCount) v = rt_clock()
 #define RT_T1(C, c, f, v) do { if constexpr (C::kCount) (c).f += rt_clock() - (v); } while (0)
 __device__ __forceinline__ void cnt_init(ScanCnt& c) {
     c.node = c.dsph = c.gsph = c.tri = c.cube_box = c.cube = c.graze = c.plane = c.graze_n = 0;
-    c.cyc_node = c.cyc_leaf = c.cyc_graze = c.cyc_scan = 0;
+    c.cyc_node = c.cyc_leaf = c.cyc_graze = c.cyc_scan = c.cyc_load = c.cyc_post = c.cyc_self = 0;
 }
 __device__ __forceinline__ uint32_t active_lanes() { return (uint32_t)__builtin_popcountll(__ballot(1)); }
 #define RT_OPS(c, f) ((c).f += active_lanes())
@@ -508,14 +508,15 @@ typedef const float4 lfloat4;
 #endif
 
 // LDS: node records staged in LDS by the kernel (lnodes != null), else read via SMEM
+// novote (shadow): the lane's hierarchy primitives are settled already (light buffer).
 template <bool SHADOW, bool LDS, class C>
 __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, float tlim,
-                                         float l2, C& c, lfloat4* lnodes) {
+                                         float l2, C& c, lfloat4* lnodes, bool novote = false) {
     const BvhRay R = bvh_ray(S, o, d);
     uint32_t* stk = rt_bvh_stack + ((threadIdx.x >> 6) << 5);
     uint32_t sp = 0;
     uint32_t cur = S.bvh_root;
-    bool done = SHADOW ? shadow_decided(o, d, bt, l2) : false;
+    bool done = SHADOW ? (novote || shadow_decided(o, d, bt, l2)) : false;
 #if RT_STATS
     // lanes whose own box test admitted the current node (stats build only)
     __shared__ uint64_t rt_need_stack[4 * 32];
@@ -546,7 +547,7 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
             bvh_leaf(S, cur & ~BVH_LEAF, o, d, R.on, tmax, bt, bk, c);
             RT_T1(C, c, cyc_leaf, t_it);
             if (SHADOW) {
-                done = shadow_decided(o, d, bt, l2);
+                done = novote || shadow_decided(o, d, bt, l2);
                 if (__ballot(!done) == 0) break;
             }
         } else {
@@ -661,19 +662,73 @@ __device__ __forceinline__ void linear_rest(const DevScene& S, V3 o, V3 d, float
 }
 
 // Scene::intersect (scene/mod.rs:98-116): the nearest (t, key) over every shape.
-template <class C>
-__device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c) {
+// LDS: the kernel staged the hierarchy's node records in LDS (lnodes).
+template <bool LDS = false, class C>
+__device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c,
+                                     lfloat4* lnodes = nullptr) {
     RT_T0(C, t_s);
     bt = __builtin_huge_valf();
     bk = 0xFFFFFFFFu;
     RT_STAT(0);
     planes(S, o, d, bt, bk, c);
     if (S.use_bvh) {
-        bvh_walk<false, false>(S, o, d, bt, bk, 0.f, 0.f, c, nullptr);
+        bvh_walk<false, LDS>(S, o, d, bt, bk, 0.f, 0.f, c, lnodes);
         graze_pass(S, o, d, bt, bk, c);
     }
     linear_rest(S, o, d, bt, bk, c);
     RT_T1(C, c, cyc_scan, t_s);
+}
+
+// ------------------------------------------------------------------ light buffers
+// (rt_api.cpp build_light_buffers, DESIGN.md "Light buffers")
+
+// cube-map cell of a direction from the light (face = largest |component|, ties x > y > z)
+__device__ __forceinline__ uint32_t lb_cell(uint32_t res, V3 v) {
+    const float ax = fabsf(v.x), ay = fabsf(v.y), az = fabsf(v.z);
+    uint32_t f;
+    float a, b, m;
+    if (ax >= ay && ax >= az) {
+        f = v.x < 0.f ? 1u : 0u;
+        a = v.y;
+        b = v.z;
+        m = ax;
+    } else if (ay >= az) {
+        f = v.y < 0.f ? 3u : 2u;
+        a = v.x;
+        b = v.z;
+        m = ay;
+    } else {
+        f = v.z < 0.f ? 5u : 4u;
+        a = v.x;
+        b = v.y;
+        m = az;
+    }
+    const float inv = __builtin_amdgcn_rcpf(m), hr = 0.5f * (float)res;
+    const int i = min(max((int)((a * inv + 1.f) * hr), 0), (int)res - 1);
+    const int j = min(max((int)((b * inv + 1.f) * hr), 0), (int)res - 1);
+    return (f * res + (uint32_t)j) * res + (uint32_t)i;
+}
+
+// The light-buffer pass of a shadow scan.  A lane with a buffer (lb) tests the records
+// its cell lists; the wave takes its lanes' cells one after the other, each tested like
+// a hierarchy leaf by every lane (a record tested for a lane whose cell does not list it
+// changes nothing), until every lane is decided or done.  Afterwards an lb lane's
+// hierarchy primitives are settled.
+template <class C>
+__device__ __forceinline__ void lb_pass(const DevScene& S, uint32_t base, V3 o, V3 d, float on, float tlim, float l2,
+                                        bool lb, float& bt, uint32_t& bk, C& c) {
+    const uint32_t leaf = lb ? base + lb_cell(S.lb_res, neg(d)) : 0u;
+    bool want = lb && !shadow_decided(o, d, bt, l2);
+    uint64_t pend;
+    while ((pend = __ballot(want)) != 0) {
+        const uint32_t cur = (uint32_t)__builtin_amdgcn_readlane((int)leaf, (int)__builtin_ctzll(pend));
+        want = want && leaf != cur;
+        RT_T0(C, t_l);
+        const bool dec = shadow_decided(o, d, bt, l2);
+        bvh_leaf(S, cur, o, d, on, dec ? -1.f : fminf(bt, tlim), bt, bk, c);  // decided lanes do not vote
+        RT_T1(C, c, cyc_leaf, t_l);
+        want = want && !shadow_decided(o, d, bt, l2);
+    }
 }
 
 // ------------------------------------------------------------------ shadow scan
@@ -690,7 +745,8 @@ __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, u
 //    norms) and can neither shadow nor hide a nearer hit: the walk stops at tlim.
 // A wave leaves the scan when every active lane is decided.  Returns `shadowed`.
 template <bool LDS, class C>
-__device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lpos, C& c, lfloat4* lnodes) {
+__device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lpos, C& c, lfloat4* lnodes,
+                                            uint32_t lb_base = 0xFFFFFFFFu) {
     RT_T0(C, t_s);
     const float l2 = len2(sub(lpos, o));
     float bt = __builtin_huge_valf();
@@ -701,7 +757,15 @@ __device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lp
     if (S.use_bvh) {
         float on = sqrtf(len2(o));
         float tlim = (sqrtf(l2) * (1.f + 0.0009765625f) + 1e-5f * (on + 1.f)) / sqrtf(len2(d));
-        bvh_walk<true, LDS>(S, o, d, bt, bk, tlim, l2, c, lnodes);
+        bool lb = false;
+        if (S.lb_res) {
+            const float dx = o.x - S.bvh_cx, dy = o.y - S.bvh_cy, dz = o.z - S.bvh_cz;
+            const float D = sqrtf(dx * dx + dy * dy + dz * dz) + S.bvh_r;
+            lb = lb_base != 0xFFFFFFFFu && D <= S.lb_dmax && l2 <= RT_LB_LMAX * RT_LB_LMAX;
+            if (__ballot(lb)) lb_pass(S, lb_base, o, d, on, tlim, l2, lb, bt, bk, c);
+        }
+        if (__ballot(!lb && !shadow_decided(o, d, bt, l2)))
+            bvh_walk<true, LDS>(S, o, d, bt, bk, tlim, l2, c, lnodes, lb);
         done = shadow_decided(o, d, bt, l2);
         if (__ballot(!done) == 0) goto finish;
         graze_pass(S, o, d, bt, bk, c);

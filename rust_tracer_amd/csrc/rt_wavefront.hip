@@ -22,6 +22,7 @@
 // post-order combine keeps the reference's exact operation order (pixel values reach
 // |4000| in config 3, so a reassociated "throughput" formulation would break 1e-4).
 #include <algorithm>
+#include <cstring>
 #include <type_traits>
 
 #include "rt_common.hpp"
@@ -178,6 +179,9 @@ __device__ __forceinline__ void bc_scan(const ScanCnt& c) {
     bc_add(RT_OPS_CYC_LEAF, c.cyc_leaf);
     bc_add(RT_OPS_CYC_GRAZE, c.cyc_graze);
     bc_add(RT_OPS_CYC_SCAN, c.cyc_scan);
+    bc_add(RT_OPS_CYC_LOAD, c.cyc_load);
+    bc_add(RT_OPS_CYC_POST, c.cyc_post);
+    bc_add(RT_OPS_CYC_SELF, c.cyc_self);
 }
 
 __device__ __forceinline__ uint64_t lanemask_lt() {
@@ -233,10 +237,17 @@ __device__ __forceinline__ void own_shape_test(const DevScene& S, uint32_t key, 
 #ifndef RT_TRACE_WAVES
 #define RT_TRACE_WAVES 5  // 96 VGPRs, 20 B scratch (measured: 4 -> 8.02 ms, 5 -> 7.89, 6 -> 7.85 with 84 B)
 #endif
-template <bool COUNT>
+extern __shared__ float4 rt_dyn_lds[];
+
+template <bool COUNT, bool LDS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES, 8))) void trace_level_kernel(
     WaveParams P, uint32_t level) {
     const DevScene& S = P.S;
+    if (LDS) {  // stage the hierarchy's node records in LDS
+        for (int i = threadIdx.x; i < 4 * S.n_bvh_nodes; i += blockDim.x) rt_dyn_lds[i] = S.bvh_nodes[i];
+        __syncthreads();
+    }
+    lfloat4* lnodes = (lfloat4*)rt_dyn_lds;
     const uint32_t off = P.levels[2 * level];
     const uint32_t count = min(P.levels[2 * level + 1], off < P.capacity ? P.capacity - off : 0u);
     const uint32_t next_off = off + count;
@@ -254,6 +265,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
     for (uint32_t base = wave_base; base < count; base += stride) {
         const uint32_t t = base + lane;
         bool active = t < count;
+        typedef decltype(cnt) CntT;
+        RT_T0(CntT, t_load);
         V3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
         uint32_t parent = 0, pix = 0;
         const uint32_t n = off + t;
@@ -294,11 +307,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         uint32_t decided = 0;  // point lights whose shadow ray the own-shape test settled
         uint32_t mort = 0;  // Morton code of the shadow-ray origin (queue ordering key)
         V3 rro = v3(0, 0, 0), rrd = v3(0, 0, 0), tro = v3(0, 0, 0), trd = v3(0, 0, 0);
+        uint32_t it_load = 0, it_scan0 = 0, it_self0 = 0;  // phase accounting (instrumented variant)
+        if constexpr (CntT::kCount) {
+            it_load = rt_clock() - t_load;
+            cnt.cyc_load += it_load;
+            it_scan0 = cnt.cyc_scan;
+            it_self0 = cnt.cyc_self;
+        }
         if (active) {
             n_node++;
             float bt;
             uint32_t bk;
-            scan(S, ro, rd, bt, bk, cnt);
+            scan<LDS>(S, ro, rd, bt, bk, cnt, lnodes);
             if (bk == 0xFFFFFFFFu) {
                 node_flags(P.nodes, n, NODE_MISS);  // trace_ray -> BLACK; the parent slot stays 0
             } else {
@@ -313,6 +333,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 V3 ks = tex_eval(M.specular, h.tu, h.tv);
                 V3 ps = add(h.p, mul(h.n, 0.0002f));  // render.rs:147
                 if (P.shadow_keys) mort = P.key_mode >= 3 ? morton18(S, ps) : morton15(S, ps);
+#if RT_STATS
+                {  // hit points outside the Morton cube (clamped to its faces)
+                    const float dx = fabsf(ps.x - S.bvh_cx), dy = fabsf(ps.y - S.bvh_cy), dz = fabsf(ps.z - S.bvh_cz);
+                    const bool out = fmaxf(dx, fmaxf(dy, dz)) > S.bvh_r;
+                    atomicAdd(&rt_scan_stats[11 + (out ? 1 : 0)], 1ull);
+                    if (level == 0) atomicAdd(&rt_scan_stats[13 + (out ? 1 : 0)], 1ull);
+                }
+#endif
                 uint32_t flags = NODE_HIT;
                 float fr = 0.f, dr = 0.f, pw = 0.f, ft = 0.f;
                 P.node_ps[n] = make_float4(ps.x, ps.y, ps.z, 0.f);
@@ -320,11 +348,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 // the shape just hit settle it: a plane's t < 0 is the nearest hit; else any
                 // hit nearer than the light means the nearest one is too (shadow_scan)
                 uint32_t lit_pre = 0u;
+                RT_T0(CntT, t_self);
                 if (P.self_shadow) {
+                    // the own shape can only shadow a light behind the offset point's
+                    // surface (or any light, from inside a sphere); elsewhere the test is
+                    // skipped (never deciding is always exact: the shadow pass decides)
+                    const uint32_t own_kind = (uint32_t)S.shapes[bk >> 4].kind;
+                    const bool own_any = own_kind == RT_SHAPE_SPHERE && !h.entering;
+                    const bool own_ok = own_kind == RT_SHAPE_SPHERE || own_kind == RT_SHAPE_TRIANGLE;
                     for (int li = 0; li < S.n_lights; ++li) {
                         const LightRec& L = S.lights[li];
                         if (L.kind != RT_LIGHT_POINT) continue;
                         const V3 lpos = v3(L.px, L.py, L.pz);
+                        if (!own_ok || !(own_any || dot(sub(lpos, ps), h.n) <= 0.f)) continue;
                         const V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
                         const float l2 = len2(sub(lpos, ps));
                         float st = __builtin_huge_valf();
@@ -338,6 +374,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                     }
                     n_pre += (uint32_t)__builtin_popcount(decided);
                 }
+                RT_T1(CntT, cnt, cyc_self, t_self);
                 P.node_lit[n] = lit_pre;
                 if (P.node_aux) {  // ray forest: what render_ray_tree re-reads at shade time
                     P.node_aux[n] = make_float4(__uint_as_float((uint32_t)h.mat), h.tu, h.tv,
@@ -448,6 +485,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 }
             }
         }
+        if constexpr (CntT::kCount)  // the rest of the iteration: attributes, records, children, entries
+            cnt.cyc_post += (rt_clock() - t_load) - it_load - (cnt.cyc_scan - it_scan0) - (cnt.cyc_self - it_self0);
     }
     for (int o = 32; o > 0; o >>= 1) {
         n_node += __shfl_xor(n_node, o);
@@ -465,7 +504,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
 
 // Every shadow ray of the frame: PointLight::get_energy's scan + distance test, result as
 // a bit in the node record.
-extern __shared__ float4 rt_dyn_lds[];
 
 #ifndef RT_SHADOW_WAVES
 #define RT_SHADOW_WAVES 5  // 96 VGPRs (measured: 4 -> 8.36 ms, 5 -> 8.04, 6 -> 11.2 with spills)
@@ -497,7 +535,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
             V3 lpos = v3(L.px, L.py, L.pz);
             V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
             n_shadow++;
-            if (!shadow_scan<LDS>(S, ps, ldir, lpos, cnt, lnodes)) atomicOr(&P.node_lit[n], 1u << li);
+            if (!shadow_scan<LDS>(S, ps, ldir, lpos, cnt, lnodes, L.lb_base)) atomicOr(&P.node_lit[n], 1u << li);
         }
     }
     for (int o = 32; o > 0; o >>= 1) n_shadow += __shfl_xor(n_shadow, o);
@@ -710,25 +748,43 @@ hipError_t launch_wave_init(uint32_t* levels, uint32_t n_words, uint32_t total_i
 }
 
 hipError_t wave_occupancy(int* trace_blocks, int* shadow_blocks, int* combine_blocks) {
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(trace_blocks, trace_level_kernel<false>, 256, 0);
+    hipError_t e =
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(trace_blocks, trace_level_kernel<false, false>, 256, 0);
     if (e != hipSuccess) return e;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<false, false>, 256, 0);
     if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(combine_blocks, combine_level_kernel, 256, 0);
 }
 
+// hierarchy node records staged in LDS when they fit (RT_LDS_NODES=0: never; =trace /
+// =shadow: only that kernel, A/B)
+static bool lds_nodes_for(const WaveParams& p, const char* kernel) {
+    size_t lds = (size_t)p.S.n_bvh_nodes * 64;
+    const char* e = getenv("RT_LDS_NODES");
+    if (e && (e[0] == '0' || (std::strcmp(e, "1") != 0 && std::strcmp(e, kernel) != 0))) return false;
+    return p.S.use_bvh && lds > 0 && lds <= 36 * 1024;
+}
+
 hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream) {
-    if (p.count_mask & 1u)
-        hipLaunchKernelGGL(trace_level_kernel<true>, dim3(blocks), dim3(256), 0, stream, p, level);
-    else
-        hipLaunchKernelGGL(trace_level_kernel<false>, dim3(blocks), dim3(256), 0, stream, p, level);
+    const size_t lds = (size_t)p.S.n_bvh_nodes * 64;
+    const bool use = lds_nodes_for(p, "trace");
+    if (p.count_mask & 1u) {
+        if (use)
+            hipLaunchKernelGGL((trace_level_kernel<true, true>), dim3(blocks), dim3(256), lds, stream, p, level);
+        else
+            hipLaunchKernelGGL((trace_level_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, p, level);
+    } else {
+        if (use)
+            hipLaunchKernelGGL((trace_level_kernel<false, true>), dim3(blocks), dim3(256), lds, stream, p, level);
+        else
+            hipLaunchKernelGGL((trace_level_kernel<false, false>), dim3(blocks), dim3(256), 0, stream, p, level);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_wave_shadow(const WaveParams& p, int blocks, hipStream_t stream) {
-    size_t lds = (size_t)p.S.n_bvh_nodes * 64;
-    const char* e = getenv("RT_LDS_NODES");
-    bool use = p.S.use_bvh && lds > 0 && lds <= 36 * 1024 && !(e && e[0] == '0');
+    const size_t lds = (size_t)p.S.n_bvh_nodes * 64;
+    const bool use = lds_nodes_for(p, "shadow");
     const bool count = (p.count_mask & 2u) != 0;
     if (use && count)
         hipLaunchKernelGGL((shadow_kernel<true, true>), dim3(blocks), dim3(256), lds, stream, p);

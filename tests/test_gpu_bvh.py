@@ -145,3 +145,57 @@ def test_counting_kernels_render_the_same_frame():
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     assert np.array_equal(a.view(np.uint32), c.view(np.uint32))
     assert ca == cb == cc
+
+
+def _render_env(desc, w, h, depth, **env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        s = DeviceScene(desc)
+        try:
+            img, cnt, _, _ = s.render(w, h, depth)
+        finally:
+            s.close()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return img, cnt
+
+
+def _lights_in_the_cluster():
+    """Point lights among the primitives: one inside a glass sphere, one a hair outside a
+    matte sphere (no light buffer for them: a grown ball comes within rho of the light),
+    one far above (buffered); spheres, cubes and triangles around them."""
+    d = SceneDesc.synth(21, 120, 10, 30, 0.05, 0.4).editable()
+    glass = d.phong((0, 0, 0), (1, 1, 1), (1, 1, 1), 60.0, 0.7, 1.5)
+    matte = d.phong((0.05, 0.05, 0.05), (0.6, 0.5, 0.4), (1, 1, 1), 30.0, 0.0, 0.0)
+    d.sphere(glass, Matrix.translate(0.5, 0.2, -0.5) * Matrix.scale(0.6, 0.6, 0.6))
+    d.sphere(matte, Matrix.translate(-1.5, 0.8, -1.0) * Matrix.scale(0.3, 0.3, 0.3))
+    d.point_light((0.5, 0.2, -0.5), (0.6, 0.6, 0.9))        # inside the glass sphere
+    d.point_light((-1.5, 1.11, -1.0), (0.9, 0.5, 0.5))      # 0.01 above the matte sphere
+    d.point_light((0.0, 30.0, -4.0), (0.4, 0.4, 0.4))
+    return d
+
+
+@pytest.mark.parametrize("scene", ["config3", "grazing", "lights_in_cluster", "random"])
+def test_shadow_shortcuts_change_nothing(scene):
+    """Light buffers at several resolutions (RT_LB_RES, 0 = off) and the trace kernel's
+    own-shape shadow tests (RT_SELF_SHADOW=0 = off): bit-identical frames and counters."""
+    desc = {"config3": lambda: SceneDesc.synth_config(3), "grazing": _grazing_scene,
+            "lights_in_cluster": _lights_in_the_cluster,
+            "random": lambda: SceneDesc.synth(31, 400, 30, 120, 0.03, 0.5)}[scene]()
+    w, h, depth = 480, 270, 8
+    base, cb = _render_env(desc, w, h, depth, RT_LB_RES=0, RT_SELF_SHADOW=0)
+    for env in ({}, {"RT_LB_RES": 8}, {"RT_LB_RES": 64}, {"RT_LB_RES": 200}, {"RT_SELF_SHADOW": 0}):
+        img, cnt = _render_env(desc, w, h, depth, **env)
+        diff = np.flatnonzero(img.view(np.uint32) != base.view(np.uint32))
+        assert diff.size == 0, (env, diff.size)
+        assert cnt == cb, env
+    if scene == "lights_in_cluster":
+        ref, rcnt = OracleScene(desc).render(120, 68, 8, threads=8)
+        img, cnt = _render_env(desc, 120, 68, 8)
+        compare(img, ref)
+        assert cnt == rcnt

@@ -25,5 +25,6 @@ for depth in (1, 2, 8):
         print(f"  {name}: leaf visits {v[b + 2]}, lanes at leaves {v[b]}, needing the leaf {v[b + 1]}: "
               f"occupancy {v[b + 1] / max(1, v[b]):.3f}; per ray needed {v[b + 1] / max(1, n):.2f}, "
               f"executed {v[b] / max(1, n):.2f}")
+    print(f"  hit points: inside the Morton cube {v[11]}, outside {v[12]} (level 0: {v[13]} / {v[14]})")
     print(f"  hit paths per wave scan: dsph {v[1] / max(1, v[0]):.2f} gsph {v[2] / max(1, v[0]):.2f} "
           f"tri {v[3] / max(1, v[0]):.2f} cube-tri {v[4] / max(1, v[0]):.2f}")
