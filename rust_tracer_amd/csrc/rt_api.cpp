@@ -187,6 +187,12 @@ struct LbPrim {
 
 struct RunLayout {
     std::vector<float> dsph, gsph, tri, cube, nodes, graze_blk, graze_tri;
+    // grazing pass by direction cell: per graze pair its two normals / sin(phi_T)
+    // {nAx nBx nAy nBy} {nAz nBz - -}; per cell of a res x res cube map of directions a
+    // bitmask (graze_words words) of the pairs some direction in the cell can graze
+    std::vector<float> graze_pn;
+    std::vector<uint32_t> graze_mask;
+    uint32_t graze_res = 0, graze_words = 0;
     std::vector<uint32_t> leaves;
     std::vector<LbPrim> lb_prims;  // every hierarchy primitive (light buffers)
     uint32_t root = BVH_LEAF;
@@ -342,6 +348,8 @@ void emit_cube(std::vector<float>& v, const CubeIn& A, float lf, float sn) {
 // The normals are stored divided by sin(phi_T), so "(d.n')^2 < 1.0201 |d|^2" is the
 // per-triangle grazing test.  Block: {ax ay az s^2} {n'x0-3} {n'x4-7} {n'y0-3} {n'y4-7}
 // {n'z0-3} {n'z4-7} {-}; its triangles as 4 pairs in graze_tri.
+static void lb_face_dir(int f, double a, double b, double out[3]);
+
 void build_graze(const std::vector<TriIn>& tris, const std::vector<char>& in_tri, const std::vector<double>& gsin,
                  RunLayout& L) {
     struct G {
@@ -416,6 +424,8 @@ void build_graze(const std::vector<TriIn>& tris, const std::vector<char>& in_tri
         put4(L.graze_blk, nz[0], nz[1], nz[2], nz[3]);
         put4(L.graze_blk, nz[4], nz[5], nz[6], nz[7]);
         put4(L.graze_blk, 0.f, 0.f, 0.f, 0.f);
+        for (int k = 0; k < 8; k += 2)  // the pairs' normals for the direction-cell path
+            put4(L.graze_pn, nx[k], nx[k + 1], ny[k], ny[k + 1]), put4(L.graze_pn, nz[k], nz[k + 1], 0.f, 0.f);
         for (int k = 0; k < 8; k += 2) {
             const TriIn* A = (b0 + k < b1) ? g[b0 + k].t : nullptr;
             const TriIn* B = (b0 + k + 1 < b1) ? g[b0 + k + 1].t : nullptr;
@@ -427,6 +437,55 @@ void build_graze(const std::vector<TriIn>& tris, const std::vector<char>& in_tri
                 emit_tri_pair(L.graze_tri, pad, nullptr);
             }
         }
+    }
+    // direction cells (RT_GRAZE_RES per face side, 0: cone path only): pair p is set in
+    // a cell when a direction within the cell's angular radius rc (+1e-4) of its centre
+    // can meet one of its triangles' planes at sin(phi) < 1.01 sin(phi_T): |c.n| <=
+    // sin(asin(1.01 s) + rc + 1e-4).  Exact superset of the per-lane test.
+    const char* ge = std::getenv("RT_GRAZE_RES");
+    const int R = ge ? std::atoi(ge) : 64;
+    const size_t npairs = L.graze_pn.size() / 8;
+    if (R > 0 && R <= 256 && npairs > 0 && npairs <= 256) {
+        const uint32_t W = (uint32_t)((npairs + 31) / 32);
+        L.graze_res = (uint32_t)R;
+        L.graze_words = W;
+        L.graze_mask.assign((size_t)6 * R * R * W, 0u);
+        // per pair: unit normals and band limits
+        std::vector<double> pn(npairs * 6), plim(npairs * 2);
+        for (size_t p = 0; p < npairs; p++)
+            for (int k = 0; k < 2; k++) {
+                const size_t gi = 2 * p + k;  // index into g (blocks of 8, pairs in order)
+                if (gi >= g.size()) {
+                    plim[2 * p + k] = -1.0;  // padding
+                    continue;
+                }
+                for (int c = 0; c < 3; c++) pn[6 * p + 3 * k + c] = g[gi].n[c];
+                plim[2 * p + k] = std::asin(std::min(1.0, 1.01 * g[gi].s));
+            }
+        for (int f = 0; f < 6; f++)
+            for (int j = 0; j < R; j++)
+                for (int i = 0; i < R; i++) {
+                    const double a0 = -1.0 + 2.0 * i / R, a1 = -1.0 + 2.0 * (i + 1) / R;
+                    const double b0 = -1.0 + 2.0 * j / R, b1 = -1.0 + 2.0 * (j + 1) / R;
+                    double m[3], q[3];
+                    lb_face_dir(f, 0.5 * (a0 + a1), 0.5 * (b0 + b1), m);
+                    double rc = 0;
+                    for (double aa : {a0, a1})
+                        for (double bb : {b0, b1}) {
+                            lb_face_dir(f, aa, bb, q);
+                            rc = std::max(rc, std::acos(std::min(1.0, m[0] * q[0] + m[1] * q[1] + m[2] * q[2])));
+                        }
+                    rc = rc * 1.01 + 1e-6;
+                    uint32_t* mw = &L.graze_mask[(((size_t)f * R + j) * R + i) * W];
+                    for (size_t p = 0; p < npairs; p++)
+                        for (int k = 0; k < 2; k++) {
+                            if (plim[2 * p + k] < 0) continue;
+                            const double* n = &pn[6 * p + 3 * k];
+                            const double cn = std::fabs(m[0] * n[0] + m[1] * n[1] + m[2] * n[2]);
+                            const double ang = plim[2 * p + k] + rc + 1e-4;
+                            if (ang >= 1.5707963 || cn <= std::sin(ang)) mw[p / 32] |= 1u << (p % 32);
+                        }
+                }
     }
 }
 
@@ -838,7 +897,7 @@ struct Workspace {
     uint32_t capacity = 0;
     uint32_t* shadow = nullptr;      // shadow queue
     uint32_t shadow_capacity = 0;
-    uint32_t* levels = nullptr;      // 2 * (RT_MAX_DEPTH + 2) words
+    uint32_t* levels = nullptr;      // RT_LEVEL_TABLE_WORDS words
     uint32_t* overflow = nullptr;
     // queue ordering (rt_order.hip)
     uint32_t* task_keys = nullptr;   // [capacity] x2 buffers
@@ -1156,7 +1215,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
         size_t off;
     };
     static const unsigned long long zero_ops[RT_OPS_SLOTS * RT_OPS_STRIDE] = {0};
-    Sec secs[14] = {{dsph.data(), dsph.size() * 4, 0},       {gsph.data(), gsph.size() * 4, 0},
+    Sec secs[16] = {{dsph.data(), dsph.size() * 4, 0},       {gsph.data(), gsph.size() * 4, 0},
                     {tri.data(), tri.size() * 4, 0},         {cube.data(), cube.size() * 4, 0},
                     {plane.data(), plane.size() * 4, 0},     {cubetri.data(), cubetri.size() * 4, 0},
                     {shapes.data(), shapes.size() * sizeof(ShapeRec), 0},
@@ -1166,7 +1225,9 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
                     {lay.leaves.data(), lay.leaves.size() * 4, 0},
                     {lay.graze_blk.data(), lay.graze_blk.size() * 4, 0},
                     {zero_ops, sizeof(zero_ops), 0},
-                    {lay.graze_tri.data(), lay.graze_tri.size() * 4, 0}};
+                    {lay.graze_tri.data(), lay.graze_tri.size() * 4, 0},
+                    {lay.graze_pn.data(), lay.graze_pn.size() * 4, 0},
+                    {lay.graze_mask.data(), lay.graze_mask.size() * 4, 0}};
     size_t total = 0;
     for (auto& s : secs) {
         s.off = total;
@@ -1208,6 +1269,10 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     S.graze_blk = (const float4*)at(11);
     S.scan_ops = (unsigned long long*)at(12);
     S.graze_tri = (const float4*)at(13);
+    S.graze_pn = (const float4*)at(14);
+    S.graze_mask = (const uint32_t*)at(15);
+    S.graze_res = lay.graze_res;
+    S.graze_words = lay.graze_words;
     S.lb_res = lbuf.res;
     S.lb_dmax = lbuf.dmax;
     S.n_graze_blk = (int32_t)(lay.graze_blk.size() / 32);
@@ -1401,7 +1466,7 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         if (st != RT_OK) return st;
     }
     if (!w.levels) {
-        HIP_TRY(hipMalloc(&w.levels, 2 * (RT_MAX_DEPTH + 2) * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&w.levels, RT_LEVEL_TABLE_WORDS * sizeof(uint32_t)));
         HIP_TRY(hipMalloc(&w.overflow, 64));
     }
     // shadow queue: one entry per point light per hit node
@@ -1420,6 +1485,10 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     const bool sort_shadow = sort_on && !(ss && ss[0] == '0');
     p.key_mode = task_key_mode();
     p.self_shadow = self_shadow_enabled() ? 1u : 0u;
+    {
+        const char* e = std::getenv("RT_SCHED");
+        p.sched = e ? (uint32_t)std::atoi(e) : 0u;
+    }
     if (s->count_ops) {  // instrumented kernels; RT_COUNT=trace|shadow: only that kernel's tests
         const char* e = std::getenv("RT_COUNT");
         p.count_mask = !e ? 3u : (std::strcmp(e, "trace") == 0 ? 1u : (std::strcmp(e, "shadow") == 0 ? 2u : 3u));
@@ -1502,7 +1571,7 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     uint32_t levels = depth > 0 ? depth : 1;
     // Every launch sizes itself from the device-side level counts: the whole frame is
     // enqueued without a host round trip (levels past the deepest non-empty one are no-ops).
-    HIP_TRY(launch_wave_init(w.levels, 2 * (RT_MAX_DEPTH + 2), p.total_items, sample == 0 ? w.overflow : nullptr,
+    HIP_TRY(launch_wave_init(w.levels, RT_LEVEL_TABLE_WORDS, p.total_items, sample == 0 ? w.overflow : nullptr,
                              stream));
     HIP_TRY(launch_wave_trace(p, 0, tb, stream));
     for (uint32_t k = 1; k < levels; k++) {

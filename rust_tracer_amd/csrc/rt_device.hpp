@@ -84,6 +84,9 @@ struct DevScene {
     // m(D) = m1 D + m0 (distance units), see rt_scan.hpp
     float bvh_cx, bvh_cy, bvh_cz, bvh_r, bvh_g2, bvh_g1, bvh_g0, bvh_m1, bvh_m0;
     float graze_s2;            // 1.0201: (d.n')^2 < graze_s2 |d|^2 with n' = n / sin(phi_T): the ray grazes
+    const float4* graze_pn;    // per graze pair: {nAx nBx nAy nBy} {nAz nBz - -} (n / sin(phi_T))
+    const uint32_t* graze_mask;  // per direction cell: graze_words words of pair bits
+    uint32_t graze_res, graze_words;  // 0: the cone path (rt_scan.hpp graze_pass)
     unsigned long long* scan_ops;  // RT_OPS_* lane-weighted test counts
     // light buffers (shadow rays; rt_api.cpp build_light_buffers): per point light
     // 6 x lb_res x lb_res cells, each a leaf of bvh_leaves (LightRec::lb_base + cell)
@@ -119,6 +122,14 @@ enum : int {
     RT_OPS_SLOTS = 64,
     RT_OPS_STRIDE = 16
 };
+
+// The level table: (offset, count) per level, the shadow-queue count, then one work
+// counter per level and one for the shadow pass: waves take their next 64 tasks from it
+// (dynamic scheduling: a launch ends when the work does, not when its slowest static
+// share does).
+#define RT_LEVEL_WORDS (2 * (RT_MAX_DEPTH + 2))
+#define RT_WORK_WORD(k) (RT_LEVEL_WORDS + (k))  // k: level, or RT_MAX_DEPTH + 1: shadow pass
+#define RT_LEVEL_TABLE_WORDS (RT_LEVEL_WORDS + RT_MAX_DEPTH + 2)
 
 // Everything one launch needs.
 struct RenderParams {
@@ -177,8 +188,9 @@ struct WaveParams {
     float4* node_ps;                   // [capacity]: shadow-ray origin (w unused)
     uint32_t* node_lit;                // [capacity]: unshadowed-light bits
     uint32_t* shadow;                  // [shadow_capacity]: (node << 5) | light
-    uint32_t* levels;                  // [2 * (RT_MAX_DEPTH + 2)]: offset, count per level;
-                                       // levels[2 * (RT_MAX_DEPTH + 1)] = shadow-queue count
+    uint32_t* levels;                  // [RT_LEVEL_TABLE_WORDS]: offset, count per level;
+                                       // levels[2 * (RT_MAX_DEPTH + 1)] = shadow-queue count;
+                                       // then the work counters (RT_WORK_WORD)
     uint32_t* overflow;                // set when an append would exceed a capacity
     float* out;
     unsigned long long* ray_counters;  // [node, shadow, pixels], added to
@@ -201,6 +213,7 @@ struct WaveParams {
     // level 0 jitters the primary ray (spp > 1) and the level-0 combine accumulates
     uint32_t spp, sample, seed;
     uint32_t self_shadow;              // trace decides shadow rays its own shape settles (A/B: RT_SELF_SHADOW=0)
+    uint32_t sched;                    // work distribution of trace / shadow launches (rt_wavefront.hip sched_base)
 };
 
 // 15-bit Morton code of a point in the 32^3 grid over [c - r, c + r]^3 (clamped)

@@ -597,16 +597,86 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
     }
 }
 
+// cube-map cell of a direction (face = largest |component|, ties x > y > z); the host
+// builds light buffers and grazing masks over the same cells (rt_api.cpp lb_face_dir)
+__device__ __forceinline__ uint32_t lb_cell(uint32_t res, V3 v) {
+    const float ax = fabsf(v.x), ay = fabsf(v.y), az = fabsf(v.z);
+    uint32_t f;
+    float a, b, m;
+    if (ax >= ay && ax >= az) {
+        f = v.x < 0.f ? 1u : 0u;
+        a = v.y;
+        b = v.z;
+        m = ax;
+    } else if (ay >= az) {
+        f = v.y < 0.f ? 3u : 2u;
+        a = v.x;
+        b = v.z;
+        m = ay;
+    } else {
+        f = v.z < 0.f ? 5u : 4u;
+        a = v.x;
+        b = v.y;
+        m = az;
+    }
+    const float inv = __builtin_amdgcn_rcpf(m), hr = 0.5f * (float)res;
+    const int i = min(max((int)((a * inv + 1.f) * hr), 0), (int)res - 1);
+    const int j = min(max((int)((b * inv + 1.f) * hr), 0), (int)res - 1);
+    return (f * res + (uint32_t)j) * res + (uint32_t)i;
+}
+
 // Grazing pass: every hierarchy triangle whose plane some lane's ray meets at
 // sin(phi) < 1.01 sin(phi_min) is tested exactly for the wave (the hierarchy's bounds
 // do not cover it).  Triangles come in blocks of 8 with similar normals; a block whose
 // normal cone no lane's direction can graze is skipped after one dot product.
+// With direction cells (S.graze_res): the wave ORs the pair masks of its lanes' cells
+// (a superset of the pairs any lane grazes) and runs the per-triangle test on those.
+// The lane's first two mask words, loaded when its scan starts (latency hidden by the walk).
+struct GrazePre {
+    uint32_t m0, m1;
+};
+__device__ __forceinline__ GrazePre graze_prefetch(const DevScene& S, V3 d) {
+    GrazePre g{0u, 0u};
+    if (S.graze_res && S.n_graze_blk) {
+        const uint32_t* mp = S.graze_mask + (size_t)lb_cell(S.graze_res, d) * S.graze_words;
+        g.m0 = mp[0];
+        if (S.graze_words > 1) g.m1 = mp[1];
+    }
+    return g;
+}
+
 template <class C>
-__device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c) {
+__device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c,
+                                           GrazePre pre) {
     if (S.n_graze_blk == 0) return;
     RT_T0(C, t_g);
     const float dd = len2(d);
     const float lim = S.graze_s2 * dd;
+    if (S.graze_res) {
+        const uint32_t* mp = S.graze_mask + (size_t)lb_cell(S.graze_res, d) * S.graze_words;
+        cfloat4* tp = cptr(S.graze_tri);
+        cfloat4* pn = cptr(S.graze_pn);
+        for (uint32_t w = 0; w < S.graze_words; ++w) {
+            uint32_t m = w == 0 ? pre.m0 : (w == 1 ? pre.m1 : mp[w]);
+            for (int o2 = 32; o2 > 0; o2 >>= 1) m |= (uint32_t)__shfl_xor((int)m, o2);
+            m = (uint32_t)__builtin_amdgcn_readfirstlane((int)m);
+            RT_OPS(c, graze);
+            while (m) {
+                const uint32_t pi = 32u * w + (uint32_t)__builtin_ctz(m);
+                m &= m - 1u;
+                const float4 a = pn[2 * pi], b = pn[2 * pi + 1];
+                f2 nn = (bc(d.x) * f2{a.x, a.y} + bc(d.y) * f2{a.z, a.w}) + bc(d.z) * f2{b.x, b.y};
+                nn *= nn;
+                RT_OPS(c, graze_n);
+                if (__ballot(nn.x < lim || nn.y < lim)) {
+                    RT_OPS(c, tri);
+                    tri_pair(ld_tri(tp + 6 * pi), o, d, bt, bk);
+                }
+            }
+        }
+        RT_T1(C, c, cyc_graze, t_g);
+        return;
+    }
     cfloat4* g = cptr(S.graze_blk);
     cfloat4* tp = cptr(S.graze_tri);
     for (int b = 0; b < S.n_graze_blk; ++b, g += 8, tp += 24) {
@@ -670,10 +740,11 @@ __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, u
     bt = __builtin_huge_valf();
     bk = 0xFFFFFFFFu;
     RT_STAT(0);
+    const GrazePre gp = graze_prefetch(S, d);
     planes(S, o, d, bt, bk, c);
     if (S.use_bvh) {
         bvh_walk<false, LDS>(S, o, d, bt, bk, 0.f, 0.f, c, lnodes);
-        graze_pass(S, o, d, bt, bk, c);
+        graze_pass(S, o, d, bt, bk, c, gp);
     }
     linear_rest(S, o, d, bt, bk, c);
     RT_T1(C, c, cyc_scan, t_s);
@@ -681,33 +752,6 @@ __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, u
 
 // ------------------------------------------------------------------ light buffers
 // (rt_api.cpp build_light_buffers, DESIGN.md "Light buffers")
-
-// cube-map cell of a direction from the light (face = largest |component|, ties x > y > z)
-__device__ __forceinline__ uint32_t lb_cell(uint32_t res, V3 v) {
-    const float ax = fabsf(v.x), ay = fabsf(v.y), az = fabsf(v.z);
-    uint32_t f;
-    float a, b, m;
-    if (ax >= ay && ax >= az) {
-        f = v.x < 0.f ? 1u : 0u;
-        a = v.y;
-        b = v.z;
-        m = ax;
-    } else if (ay >= az) {
-        f = v.y < 0.f ? 3u : 2u;
-        a = v.x;
-        b = v.z;
-        m = ay;
-    } else {
-        f = v.z < 0.f ? 5u : 4u;
-        a = v.x;
-        b = v.y;
-        m = az;
-    }
-    const float inv = __builtin_amdgcn_rcpf(m), hr = 0.5f * (float)res;
-    const int i = min(max((int)((a * inv + 1.f) * hr), 0), (int)res - 1);
-    const int j = min(max((int)((b * inv + 1.f) * hr), 0), (int)res - 1);
-    return (f * res + (uint32_t)j) * res + (uint32_t)i;
-}
 
 // The light-buffer pass of a shadow scan.  A lane with a buffer (lb) tests the records
 // its cell lists; the wave takes its lanes' cells one after the other, each tested like
@@ -748,6 +792,7 @@ template <bool LDS, class C>
 __device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lpos, C& c, lfloat4* lnodes,
                                             uint32_t lb_base = 0xFFFFFFFFu) {
     RT_T0(C, t_s);
+    const GrazePre gp = graze_prefetch(S, d);
     const float l2 = len2(sub(lpos, o));
     float bt = __builtin_huge_valf();
     uint32_t bk = 0xFFFFFFFFu;
@@ -768,7 +813,7 @@ __device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lp
             bvh_walk<true, LDS>(S, o, d, bt, bk, tlim, l2, c, lnodes, lb);
         done = shadow_decided(o, d, bt, l2);
         if (__ballot(!done) == 0) goto finish;
-        graze_pass(S, o, d, bt, bk, c);
+        graze_pass(S, o, d, bt, bk, c, gp);
         done = shadow_decided(o, d, bt, l2);
         if (__ballot(!done) == 0) goto finish;
     }
