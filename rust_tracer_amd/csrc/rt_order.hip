@@ -178,14 +178,20 @@ hipError_t launch_sort(const uint32_t* levels, int32_t level, uint32_t cap, uint
     const SortRef r{levels, level, cap};
     const uint32_t mt = sort_max_tiles(cap);
     const int nb = (int)std::min<uint32_t>((uint32_t)blocks, mt > 0 ? mt : 1u);
-    const uint32_t passes = std::max(1u, std::min(4u, (bits + 7u) / 8u));
+    uint32_t passes = std::max(1u, std::min(4u, (bits + 7u) / 8u));
+    // RT_SORT_TOP=k (A/B): sort by the top k key bytes only (skip the low passes)
+    uint32_t skip = 0;
+    if (const char* e = getenv("RT_SORT_TOP")) {
+        const uint32_t k = (uint32_t)atoi(e);
+        if (k >= 1 && k < passes) skip = passes - k;
+    }
     const uint32_t* kin = keys;
     const uint32_t* vin = vals;
     int in_abs = 1;
-    for (uint32_t p = 0; p < passes; p++) {
+    for (uint32_t p = skip; p < passes; p++) {
         const uint32_t shift = 8u * p;
         const bool last = p + 1 == passes;
-        uint32_t* kout = last ? nullptr : tmp + (size_t)(p & 1u) * 2u * cap;
+        uint32_t* kout = last ? nullptr : tmp + (size_t)((p - skip) & 1u) * 2u * cap;
         uint32_t* vout = last ? vals_out : kout + cap;
         hipLaunchKernelGGL(sort_count_kernel, dim3(nb), dim3(SORT_THREADS), 0, stream, r, kin, in_abs, shift,
                            tile_counts, mt);

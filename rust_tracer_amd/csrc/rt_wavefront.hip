@@ -108,6 +108,22 @@ __device__ __forceinline__ uint32_t morton18(const DevScene& S, V3 p) {
     return (spread6((uint32_t)x) << 2) | (spread6((uint32_t)y) << 1) | spread6((uint32_t)z);
 }
 
+__device__ __forceinline__ uint32_t spread7(uint32_t v) {  // 7 bits -> every third bit
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+// 21-bit Morton code over the 128^3 grid of the same cube
+__device__ __forceinline__ uint32_t morton21(const DevScene& S, V3 p) {
+    float sc = 64.f / S.bvh_r;
+    int x = (int)fminf(fmaxf((p.x - S.bvh_cx) * sc + 64.f, 0.f), 127.f);
+    int y = (int)fminf(fmaxf((p.y - S.bvh_cy) * sc + 64.f, 0.f), 127.f);
+    int z = (int)fminf(fmaxf((p.z - S.bvh_cz) * sc + 64.f, 0.f), 127.f);
+    return (spread7((uint32_t)x) << 2) | (spread7((uint32_t)y) << 1) | spread7((uint32_t)z);
+}
+
 // task ordering key: 16 bits (modes 0-2) or 24 bits (mode 3)
 __device__ __forceinline__ uint32_t task_key(const WaveParams& P, V3 o, V3 d) {
     if (P.key_mode == 0) return (octant(d) << 13) | (morton15(P.S, o) >> 2);  // 16 bits: 2 radix passes
@@ -364,7 +380,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 V3 kd = tex_eval(M.diffuse, h.tu, h.tv);
                 V3 ks = tex_eval(M.specular, h.tu, h.tv);
                 V3 ps = add(h.p, mul(h.n, 0.0002f));  // render.rs:147
-                if (P.shadow_keys) mort = P.key_mode >= 3 ? morton18(S, ps) : morton15(S, ps);
+                if (P.shadow_keys)
+                    mort = P.shadow_fine == 21u ? morton21(S, ps) : (P.shadow_fine ? morton18(S, ps) : morton15(S, ps));
 #if RT_STATS
                 {  // hit points outside the Morton cube (clamped to its faces)
                     const float dx = fabsf(ps.x - S.bvh_cx), dy = fabsf(ps.y - S.bvh_cy), dz = fabsf(ps.z - S.bvh_cz);
@@ -510,7 +527,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                     if (slot < P.shadow_capacity) {
                         P.shadow[slot] = (n << 5) | (uint32_t)li;
                         if (P.shadow_keys)
-                            P.shadow_keys[slot] = P.key_mode >= 3 ? (((uint32_t)li << 18) | mort)
+                            P.shadow_keys[slot] = P.shadow_fine ? (((uint32_t)li << P.shadow_fine) | mort)
                                                                   : ((uint32_t)li << P.light_shift) | (mort >> (15u - P.light_shift));
                     } else
                         atomicOr(P.overflow, 2u);
