@@ -15,10 +15,13 @@ constexpr int BINS = 16;
 // operation for the whole wave, while leaf tests are straight-line packed arithmetic.
 // Measured (config 3, 1080p, ms/frame): node cost 40 / leaves <= 8: 7.88; 80: 7.20;
 // 120 / 16: 6.98; 200 / 16: 6.76; 200 / 32: 6.73; 300 / 32: 6.78; 500 / 64: 7.09.
+// Retuned with light buffers and the own-shape shadow tests (the walk now serves mostly
+// trace rays): 100 / 32: 5.07; 200 / 32: 4.76; 400 / 32: 4.65; 600 / 32: 4.68;
+// 400 / 64: 4.65; 800 / 64: 4.89.
 // RT_BVH_CNODE / RT_BVH_MAXLEAF override them (A/B measurements).
 double c_node() {
     const char* e = std::getenv("RT_BVH_CNODE");
-    return e ? std::atof(e) : 200.0;
+    return e ? std::atof(e) : 400.0;
 }
 size_t max_leaf() {
     const char* e = std::getenv("RT_BVH_MAXLEAF");
