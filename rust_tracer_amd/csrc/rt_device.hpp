@@ -214,6 +214,7 @@ struct WaveParams {
     // level 0 jitters the primary ray (spp > 1) and the level-0 combine accumulates
     uint32_t spp, sample, seed;
     uint32_t self_shadow;              // trace decides shadow rays its own shape settles (A/B: RT_SELF_SHADOW=0)
+    uint32_t inline_levels;            // trace levels < this trace their own shadow rays (RT_INLINE_SHADOW)
     uint32_t sched;                    // work distribution of trace / shadow launches (rt_wavefront.hip sched_base)
 };
 

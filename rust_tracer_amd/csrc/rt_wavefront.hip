@@ -423,6 +423,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                     }
                     n_pre += (uint32_t)__builtin_popcount(decided);
                 }
+                if (level < P.inline_levels) {  // the level's remaining shadow rays, right here
+                    for (int li = 0; li < S.n_lights; ++li) {
+                        const LightRec& L = S.lights[li];
+                        if (L.kind != RT_LIGHT_POINT || ((decided >> li) & 1u)) continue;
+                        const V3 lpos = v3(L.px, L.py, L.pz);
+                        const V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
+                        if (!shadow_scan<LDS>(S, ps, ldir, lpos, cnt, lnodes, L.lb_base)) lit_pre |= 1u << li;
+                        decided |= 1u << li;
+                        n_pre++;
+                    }
+                }
                 RT_T1(CntT, cnt, cyc_self, t_self);
                 P.node_lit[n] = lit_pre;
                 if (P.node_aux) {  // ray forest: what render_ray_tree re-reads at shade time

@@ -182,14 +182,18 @@ def _lights_in_the_cluster():
 
 @pytest.mark.parametrize("scene", ["config3", "grazing", "lights_in_cluster", "random"])
 def test_shadow_shortcuts_change_nothing(scene):
-    """Light buffers at several resolutions (RT_LB_RES, 0 = off) and the trace kernel's
-    own-shape shadow tests (RT_SELF_SHADOW=0 = off): bit-identical frames and counters."""
+    """Light buffers at several resolutions (RT_LB_RES, 0 = off), the trace kernel's
+    own-shape shadow tests (RT_SELF_SHADOW=0 = off), inline shadow rays (RT_INLINE_SHADOW:
+    levels traced inline) and the grazing pass's direction cells (RT_GRAZE_RES, 0 = cone
+    path): bit-identical frames and counters."""
     desc = {"config3": lambda: SceneDesc.synth_config(3), "grazing": _grazing_scene,
             "lights_in_cluster": _lights_in_the_cluster,
             "random": lambda: SceneDesc.synth(31, 400, 30, 120, 0.03, 0.5)}[scene]()
     w, h, depth = 480, 270, 8
     base, cb = _render_env(desc, w, h, depth, RT_LB_RES=0, RT_SELF_SHADOW=0)
-    for env in ({}, {"RT_LB_RES": 8}, {"RT_LB_RES": 64}, {"RT_LB_RES": 200}, {"RT_SELF_SHADOW": 0}):
+    for env in ({}, {"RT_LB_RES": 8}, {"RT_LB_RES": 64}, {"RT_LB_RES": 200}, {"RT_SELF_SHADOW": 0},
+                {"RT_INLINE_SHADOW": 0}, {"RT_INLINE_SHADOW": 8, "RT_LB_RES": 16}, {"RT_GRAZE_RES": 0},
+                {"RT_GRAZE_RES": 8}):
         img, cnt = _render_env(desc, w, h, depth, **env)
         diff = np.flatnonzero(img.view(np.uint32) != base.view(np.uint32))
         assert diff.size == 0, (env, diff.size)
