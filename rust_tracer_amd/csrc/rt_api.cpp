@@ -930,8 +930,12 @@ bool sort_tasks_enabled() {
 // RT_TASK_KEY overrides (A/B): config 3 1080p frame 10.35 / 10.77 / 10.39 ms.
 uint32_t task_key_mode() {
     const char* e = std::getenv("RT_TASK_KEY");
-    return e ? (uint32_t)std::atoi(e) : 1u;
+    return e ? (uint32_t)std::atoi(e) : 6u;
 }
+// 5 / 6 (default 6): face x 2x2 direction cells | 11-bit Morton code of the point
+// RT_KEY_AHEAD x (scene radius) ahead on the ray (default 0.5 / 0.25): rays that cross
+// the same region next share a key.  Config 3 (same box): mode 1 4.90 ms, 6 at 0.10 /
+// 0.15 / 0.20 / 0.25 / 0.35: 4.88 / 4.86 / 4.88 / 4.81 / 4.94, mode 5 (0.5) +1.5%.
 // 3 / 4: 24-bit keys -- task = face x 8x8 direction cells | 15-bit Morton origin (4:
 // origin-major), shadow = light | 18-bit Morton origin (3 sort passes).  Measured
 // (config 3, 1080p): 1 -> 5.78 ms, 3 -> 6.13, 4 -> 6.42: finer keys scatter the waves.
@@ -1484,6 +1488,10 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     const bool sort_tasks = sort_on && sort_tasks_enabled();
     const bool sort_shadow = sort_on && !(ss && ss[0] == '0');
     p.key_mode = task_key_mode();
+    {
+        const char* e = std::getenv("RT_KEY_AHEAD");
+        p.key_ahead = e ? (float)std::atof(e) : (p.key_mode == 5 ? 0.5f : 0.25f);
+    }
     p.self_shadow = self_shadow_enabled() ? 1u : 0u;
     {
         // primary hits are coherent (8x8 tiles): their shadow rays are traced inline by the
@@ -1507,13 +1515,13 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     uint32_t lbits = 0;
     while ((1u << lbits) < s->S.n_lights) lbits++;
     p.light_shift = lbits <= 1 ? 15u : (16u - lbits > 15u ? 15u : 16u - lbits);
-    uint32_t task_bits = p.key_mode >= 3 ? 24u : 16u, shadow_bits = 16u;
+    uint32_t task_bits = (p.key_mode == 3 || p.key_mode == 4) ? 24u : 16u, shadow_bits = 16u;
     {
         // light | 18-bit Morton by default (config 3: 4.80 ms vs 4.93 with the 16-bit key);
         // RT_SHADOW_KEY = 16 / 18 / 21 (A/B)
         const char* e = std::getenv("RT_SHADOW_KEY");
         const int v = e ? std::atoi(e) : 18;
-        p.shadow_fine = (p.key_mode >= 3 || v == 18) ? 18u : (v == 21 ? 21u : 0u);
+        p.shadow_fine = (p.key_mode == 3 || p.key_mode == 4 || v == 18) ? 18u : (v == 21 ? 21u : 0u);
         if (p.shadow_fine && p.shadow_fine + lbits > 32u) p.shadow_fine = 0u;
     }
     if (p.shadow_fine) shadow_bits = p.shadow_fine + lbits;

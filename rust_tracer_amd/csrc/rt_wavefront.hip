@@ -134,6 +134,13 @@ __device__ __forceinline__ uint32_t task_key(const WaveParams& P, V3 o, V3 d) {
     if (ax >= ay && ax >= az) { face = d.x < 0.f; u = d.y; v = d.z; m = ax; }
     else if (ay >= az) { face = 2u + (d.y < 0.f); u = d.x; v = d.z; m = ay; }
     else { face = 4u + (d.z < 0.f); u = d.x; v = d.y; m = az; }
+    if (P.key_mode == 5 || P.key_mode == 6) {  // Morton of a point ahead on the ray (A/B)
+        const float ahead = P.key_ahead * P.S.bvh_r;
+        const V3 q = add(o, mul(d, ahead));
+        uint32_t cu = u > 0.f ? 1u : 0u, cv = v > 0.f ? 1u : 0u;
+        uint32_t dir = (face << 2) | (cu << 1) | cv;
+        return (dir << 11) | (morton15(P.S, q) >> 4);
+    }
     if (P.key_mode >= 3) {  // face x 8x8 cells (< 384) and the 15-bit Morton origin
         float iu = u / m, iv = v / m;  // in [-1, 1]
         uint32_t qu = (uint32_t)fminf(fmaxf((iu + 1.f) * 4.f, 0.f), 7.f);
