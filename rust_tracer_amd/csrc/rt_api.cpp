@@ -527,7 +527,9 @@ static void lb_face_dir(int f, double a, double b, double out[3]) {
 
 void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, LightBuffers& B) {
     const char* e = std::getenv("RT_LB_RES");  // cells per face side; 0: no light buffers (A/B)
-    const int R = e ? std::atoi(e) : 32;
+    const int R = e ? std::atoi(e) : 48;
+    const char* re = std::getenv("RT_LB_REACH");  // "0": runs are never cut at the reach (A/B)
+    const bool reach_cut = !(re && re[0] == '0');
     B.base.assign(lights.size(), 0xFFFFFFFFu);
     if (!L.use || R <= 0 || R > 1024 || L.lb_prims.empty()) return;
     B.res = (uint32_t)R;
@@ -589,7 +591,7 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
         if (!ok) continue;
         // nearest first: every cell's list comes out sorted by distance from the light
         std::stable_sort(cones.begin(), cones.end(), [](const Cone& a, const Cone& b) { return a.near < b.near; });
-        std::vector<std::vector<std::pair<uint32_t, double>>> lists(nc);
+        std::vector<std::vector<std::pair<uint32_t, double>>> lists(nc);  // (code, nearest distance)
         for (const Cone& c : cones) {
             for (int f = 0; f < 6; f++) {
                 const int k = f >> 1;
@@ -615,30 +617,45 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
         }
         const uint32_t base = (uint32_t)(L.leaves.size() / 8);
         for (int cc = 0; cc < nc; cc++) {
+            // per type, nearest first; each copy carries its nearest distance to the light
+            // (down-rounded) in the record's spare slot: the device stops a run at the first
+            // record no undecided lane can reach
             std::vector<uint32_t> by[4];
-            for (const auto& q : lists[cc]) by[q.first >> 30].push_back(q.first & 0x3FFFFFFFu);
+            std::vector<float> nr[4];
+            for (const auto& q : lists[cc]) {
+                by[q.first >> 30].push_back(q.first & 0x3FFFFFFFu);
+                nr[q.first >> 30].push_back(reach_cut ? down_f(q.second) : 0.f);
+            }
             uint32_t rec[8];
             rec[0] = (uint32_t)(L.dsph.size() / 16);
-            for (uint32_t r : by[LB_DSPH]) {
+            for (size_t q = 0; q < by[LB_DSPH].size(); q++) {
+                const uint32_t r = by[LB_DSPH][q];
                 std::vector<float> t(L.dsph.begin() + 16 * (size_t)r, L.dsph.begin() + 16 * (size_t)r + 16);
+                t[15] = nr[LB_DSPH][q];
                 L.dsph.insert(L.dsph.end(), t.begin(), t.end());
             }
             rec[1] = (uint32_t)(L.dsph.size() / 16);
             rec[2] = (uint32_t)(L.gsph.size() / 16);
-            for (uint32_t r : by[LB_GSPH]) {
+            for (size_t q = 0; q < by[LB_GSPH].size(); q++) {
+                const uint32_t r = by[LB_GSPH][q];
                 std::vector<float> t(L.gsph.begin() + 16 * (size_t)r, L.gsph.begin() + 16 * (size_t)r + 16);
+                t[15] = nr[LB_GSPH][q];
                 L.gsph.insert(L.gsph.end(), t.begin(), t.end());
             }
             rec[3] = (uint32_t)(L.gsph.size() / 16);
             rec[4] = (uint32_t)(L.tri.size() / 24);
-            for (uint32_t r : by[LB_TRI]) {
+            for (size_t q = 0; q < by[LB_TRI].size(); q++) {
+                const uint32_t r = by[LB_TRI][q];
                 std::vector<float> t(L.tri.begin() + 24 * (size_t)r, L.tri.begin() + 24 * (size_t)r + 24);
+                t[20] = nr[LB_TRI][q];
                 L.tri.insert(L.tri.end(), t.begin(), t.end());
             }
             rec[5] = (uint32_t)(L.tri.size() / 24);
             rec[6] = (uint32_t)(L.cube.size() / 16);
-            for (uint32_t r : by[LB_CUBE]) {
+            for (size_t q = 0; q < by[LB_CUBE].size(); q++) {
+                const uint32_t r = by[LB_CUBE][q];
                 std::vector<float> t(L.cube.begin() + 16 * (size_t)r, L.cube.begin() + 16 * (size_t)r + 16);
+                t[15] = nr[LB_CUBE][q];
                 L.cube.insert(L.cube.end(), t.begin(), t.end());
             }
             rec[7] = (uint32_t)(L.cube.size() / 16);

@@ -753,11 +753,71 @@ __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, u
 // ------------------------------------------------------------------ light buffers
 // (rt_api.cpp build_light_buffers, DESIGN.md "Light buffers")
 
+__device__ __forceinline__ float wave_max(float x) {
+    for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+    return x;
+}
+
 // The light-buffer pass of a shadow scan.  A lane with a buffer (lb) tests the records
 // its cell lists; the wave takes its lanes' cells one after the other, each tested like
 // a hierarchy leaf by every lane (a record tested for a lane whose cell does not list it
 // changes nothing), until every lane is decided or done.  Afterwards an lb lane's
 // hierarchy primitives are settled.
+// A light-buffer cell: its runs, each nearest first, stopped at the first record whose
+// nearest distance to the light exceeds `reach` (no undecided lane's origin is farther
+// from the light, so nothing from there on can shadow one; the record's spare slot
+// holds that distance).
+template <class C>
+__device__ __forceinline__ void lb_leaf(const DevScene& S, uint32_t li, V3 o, V3 d, float on, float tmax,
+                                        float reach, float& bt, uint32_t& bk, C& c) {
+    cuint4* lp = (cuint4*)S.bvh_leaves + 2 * li;
+    const uint4 a = lp[0], b = lp[1];
+    if (a.x < a.y) {
+        cfloat4* p = cptr(S.dsph) + 4 * a.x;
+        SphPair cur = ld_sph(p);
+        for (uint32_t i = a.x; i < a.y; ++i) {
+            p += 4;
+            SphPair nxt = ld_sph(p);
+            if (cur.q3.w > reach) break;
+            RT_OPS(c, dsph);
+            sph_pair(cur, o, d, bt, bk);
+            cur = nxt;
+        }
+    }
+    if (a.z < a.w) {
+        cfloat4* p = cptr(S.gsph) + 4 * a.z;
+        Rec16 cur = ld_rec(p);
+        for (uint32_t i = a.z; i < a.w; ++i) {
+            p += 4;
+            Rec16 nxt = ld_rec(p);
+            if (cur.rk.w > reach) break;
+            RT_OPS(c, gsph);
+            sph_general(cur, o, d, bt, bk);
+            cur = nxt;
+        }
+    }
+    if (b.x < b.y) {
+        cfloat4* p = cptr(S.tri) + 6 * b.x;
+        TriPair cur = ld_tri(p);
+        for (uint32_t i = b.x; i < b.y; ++i) {
+            p += 6;
+            TriPair nxt = ld_tri(p);
+            if (cur.q5.x > reach) break;
+            RT_OPS(c, tri);
+            tri_pair(cur, o, d, bt, bk);
+            cur = nxt;
+        }
+    }
+    if (b.z < b.w) {
+        cfloat4* p = cptr(S.cube) + 4 * b.z;
+        for (uint32_t i = b.z; i < b.w; ++i, p += 4) {
+            const Rec16 r = ld_rec(p);
+            if (r.rk.w > reach) break;
+            cube_culled(r, o, d, on, tmax, bt, bk, c);
+        }
+    }
+}
+
 template <class C>
 __device__ __forceinline__ void lb_pass(const DevScene& S, uint32_t base, V3 o, V3 d, float on, float tlim, float l2,
                                         bool lb, float& bt, uint32_t& bk, C& c) {
@@ -769,7 +829,9 @@ __device__ __forceinline__ void lb_pass(const DevScene& S, uint32_t base, V3 o, 
         want = want && leaf != cur;
         RT_T0(C, t_l);
         const bool dec = shadow_decided(o, d, bt, l2);
-        bvh_leaf(S, cur, o, d, on, dec ? -1.f : fminf(bt, tlim), bt, bk, c);  // decided lanes do not vote
+        // the farthest undecided origin from the light (+ rounding margin)
+        const float reach = wave_max(dec ? 0.f : sqrtf(l2) * 1.001f + 1e-4f);
+        lb_leaf(S, cur, o, d, on, dec ? -1.f : fminf(bt, tlim), reach, bt, bk, c);  // decided lanes do not vote
         RT_T1(C, c, cyc_leaf, t_l);
         want = want && !shadow_decided(o, d, bt, l2);
     }
