@@ -1370,6 +1370,8 @@ rt_status rt_scene_set_scan_counting(rt_scene* s, int32_t enable) {
     return RT_OK;
 }
 
+static uint32_t* g_task_clock = nullptr;  // RT_TASK_CLOCK records (debug)
+
 static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
                                    uint32_t band_rows, uint32_t rank, uint32_t world, float* d_rgb,
                                    unsigned long long* d_counters, hipStream_t stream);
@@ -1520,6 +1522,29 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     {
         const char* e = std::getenv("RT_SCHED");
         p.sched = e ? (uint32_t)std::atoi(e) : 0u;
+    }
+    {
+        // debug: per wave-iteration wall-clock records of the trace kernel (rt_debug_task_clock)
+        static uint32_t* clk = nullptr;
+        static uint32_t clk_cap = 0;
+        const char* e = std::getenv("RT_TASK_CLOCK");
+        if (e && !clk) {
+            clk_cap = (uint32_t)std::atoi(e);
+            HIP_TRY(hipMalloc(&clk, (4 + 4 * (size_t)clk_cap) * sizeof(uint32_t)));
+            g_task_clock = clk;
+        }
+        p.task_clock = e ? clk : nullptr;
+        p.task_clock_cap = clk_cap;
+        if (p.task_clock) HIP_TRY(hipMemsetAsync(p.task_clock, 0, 16, stream));
+    }
+    {
+        // RT_TASK_W = narrowest trace task width (64: fixed 64-ray tasks), RT_TASK_FILL =
+        // tasks per wave slot below which a level's tasks are narrowed
+        const char* e = std::getenv("RT_TASK_W");
+        const int w = e ? std::atoi(e) : 64;
+        p.task_w_min = (w == 16 || w == 32) ? (uint32_t)w : 64u;
+        const char* f = std::getenv("RT_TASK_FILL");
+        p.task_w_fill = f ? (float)std::atof(f) : 1.f;
     }
     if (s->count_ops) {  // instrumented kernels; RT_COUNT=trace|shadow: only that kernel's tests
         const char* e = std::getenv("RT_COUNT");
@@ -1928,3 +1953,14 @@ rt_status rt_scene_set_material(rt_scene* s, uint32_t index, const rt_material* 
 }
 
 }  // extern "C"
+
+// debug (tools/task_clock.py): copy the trace kernel's per wave-iteration records of the
+// last RT_TASK_CLOCK render: out[0] = records written, then 4 words per record
+extern "C" int rt_debug_task_clock(uint32_t* out, uint32_t max_records) {
+    if (!g_task_clock) return 1;
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
+    return hipMemcpy(out, g_task_clock, (4 + 4 * (size_t)max_records) * sizeof(uint32_t), hipMemcpyDeviceToHost) ==
+                   hipSuccess
+               ? 0
+               : 1;
+}

@@ -217,6 +217,10 @@ struct WaveParams {
     uint32_t self_shadow;              // trace decides shadow rays its own shape settles (A/B: RT_SELF_SHADOW=0)
     uint32_t inline_levels;            // trace levels < this trace their own shadow rays (RT_INLINE_SHADOW)
     uint32_t sched;                    // work distribution of trace / shadow launches (rt_wavefront.hip sched_base)
+    uint32_t* task_clock;              // debug (RT_TASK_CLOCK): [0] count, then {level, base, ticks, lanes} per wave iteration
+    uint32_t task_clock_cap;
+    uint32_t task_w_min;               // narrowest trace task (rays per wave iteration; 64 = never narrowed)
+    float task_w_fill;                 // trace tasks are narrowed while a level has fewer than fill x wave slots of them
 };
 
 // 15-bit Morton code of a point in the 32^3 grid over [c - r, c + r]^3 (clamped)

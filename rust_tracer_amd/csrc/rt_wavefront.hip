@@ -223,22 +223,41 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 // records every CU reads at a time are few (scalar caches and L2 stay warm); every
 // scheme that spreads concurrent waves over the queue loses that.
 // Returns the base of the wave's iteration `it`, or >= count when done.
-__device__ __forceinline__ uint32_t sched_base(const WaveParams& P, uint32_t* counter, uint32_t count, uint32_t it) {
+__device__ __forceinline__ uint32_t sched_base(const WaveParams& P, uint32_t* counter, uint32_t count, uint32_t it,
+                                                  uint32_t W = 64u) {
     const uint32_t wave = threadIdx.x >> 6, waves_per_block = blockDim.x >> 6;
     if (P.sched == 1) {
         uint32_t base = 0;
-        if (lane_id() == 0) base = atomicAdd(counter, 64u);
+        if (lane_id() == 0) base = atomicAdd(counter, W);
         return (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
     }
     if (P.sched == 2) {
         const uint32_t nb = gridDim.x, per_xcd = (nb + 7u) / 8u;
         const uint32_t lb = (blockIdx.x % 8u) * per_xcd + blockIdx.x / 8u;  // XCD-major block order
-        const uint32_t chunk = 64u * waves_per_block;
+        const uint32_t chunk = W * waves_per_block;
         const uint32_t iters = (count + nb * chunk - 1u) / (nb * chunk);
         if (it >= iters) return 0xFFFFFFFFu;
-        return (lb * iters + it) * chunk + wave * 64u;
+        return (lb * iters + it) * chunk + wave * W;
     }
-    return ((blockIdx.x * waves_per_block + wave) + it * gridDim.x * waves_per_block) * 64u;
+    return ((blockIdx.x * waves_per_block + wave) + it * gridDim.x * waves_per_block) * W;
+}
+
+// debug (RT_TASK_CLOCK, librt_hip_clk.so from tools/task_clock.sh): one record per finished wave iteration -- level, base task,
+// start tick, ticks (wall clock), active lanes
+__device__ __forceinline__ void task_clock_mark(const WaveParams& P, uint32_t level, uint32_t it, uint32_t base,
+                                             uint64_t& clk0, uint32_t count) {
+    const uint64_t now = wall_clock64();
+    if (it > 0 && lane_id() == 0) {
+        const uint32_t i = atomicAdd(P.task_clock, 1u);
+        if (i < P.task_clock_cap) {
+            uint32_t* r = P.task_clock + 4 + 4 * (size_t)i;
+            r[0] = level;
+            r[1] = (uint32_t)clk0;  // start (low word)
+            r[2] = (uint32_t)(now - clk0);
+            r[3] = count > base ? min(count - base, 64u) : 0u;
+        }
+    }
+    clk0 = now;
 }
 
 // wave-aggregated append of `n` (< 64) consecutive slots per lane to a device counter:
@@ -311,15 +330,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
     bc_init();
     // point lights: one shadow ray each per hit (mod.rs:189-206); ambient lights: none
 
+    // Task width: a level with fewer tasks than wave slots runs one task per wave and its
+    // time is the slowest wave's walk, not a throughput; narrower tasks (fewer rays per
+    // wave, the rest of the lanes idle) shorten that walk while slots are left over.
+    uint32_t W = 64u;
+    {
+        const float slots = (float)(gridDim.x * (blockDim.x >> 6));
+        while (W > P.task_w_min && (float)count < P.task_w_fill * slots * (float)W) W >>= 1;
+    }
     // whole waves iterate together (the wave-aggregated appends see every lane)
+#if RT_TASK_CLOCK_BUILD
+    uint64_t clk0 = 0;
+    uint32_t clk_base = 0;
+#endif
     for (uint32_t it = 0;; ++it) {
-        const uint32_t base = sched_base(P, &P.levels[RT_WORK_WORD(level)], count, it);
+        const uint32_t base = sched_base(P, &P.levels[RT_WORK_WORD(level)], count, it, W);
+#if RT_TASK_CLOCK_BUILD
+        if (P.task_clock) task_clock_mark(P, level, it, clk_base, clk0, count);
+        clk_base = base;
+#endif
         if (base >= count) {
             if (P.sched == 2 && base != 0xFFFFFFFFu) continue;  // a block's tail past the queue end
             break;
         }
         const uint32_t t = base + lane;
-        bool active = t < count;
+        bool active = lane < W && t < count;
         typedef decltype(cnt) CntT;
         RT_T0(CntT, t_load);
         V3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
