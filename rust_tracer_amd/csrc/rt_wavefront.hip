@@ -398,6 +398,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         uint32_t mort = 0;  // Morton code of the shadow-ray origin (queue ordering key)
         V3 rro = v3(0, 0, 0), rrd = v3(0, 0, 0), tro = v3(0, 0, 0), trd = v3(0, 0, 0);
         uint32_t it_load = 0, it_scan0 = 0, it_self0 = 0;  // phase accounting (instrumented variant)
+        uint32_t it_scan_self = 0;  // scan cycles spent inside the self phase (inline shadow scans)
         if constexpr (CntT::kCount) {
             it_load = rt_clock() - t_load;
             cnt.cyc_load += it_load;
@@ -439,6 +440,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 // the shape just hit settle it: a plane's t < 0 is the nearest hit; else any
                 // hit nearer than the light means the nearest one is too (shadow_scan)
                 uint32_t lit_pre = 0u;
+                if constexpr (CntT::kCount) it_scan_self = cnt.cyc_scan;
                 RT_T0(CntT, t_self);
                 if (P.self_shadow) {
                     // the own shape can only shadow a light behind the offset point's
@@ -477,6 +479,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                     }
                 }
                 RT_T1(CntT, cnt, cyc_self, t_self);
+                if constexpr (CntT::kCount) it_scan_self = cnt.cyc_scan - it_scan_self;
                 P.node_lit[n] = lit_pre;
                 if (P.node_aux) {  // ray forest: what render_ray_tree re-reads at shade time
                     P.node_aux[n] = make_float4(__uint_as_float((uint32_t)h.mat), h.tu, h.tv,
@@ -588,7 +591,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
             }
         }
         if constexpr (CntT::kCount)  // the rest of the iteration: attributes, records, children, entries
-            cnt.cyc_post += (rt_clock() - t_load) - it_load - (cnt.cyc_scan - it_scan0) - (cnt.cyc_self - it_self0);
+            cnt.cyc_post += (rt_clock() - t_load) - it_load - (cnt.cyc_scan - it_scan0 - it_scan_self) -
+                            (cnt.cyc_self - it_self0);
     }
     for (int o = 32; o > 0; o >>= 1) {
         n_node += __shfl_xor(n_node, o);
