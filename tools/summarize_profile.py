@@ -22,7 +22,7 @@ RENDER = ("trace_level_kernel", "shadow_kernel", "combine_level_kernel", "wave_i
 
 def family(kernel_name):
     """short family name of a render-pipeline dispatch (None if not one)"""
-    if ("trace_level_kernel<true>" in kernel_name or "shadow_kernel<true, true>" in kernel_name
+    if ("trace_level_kernel<true" in kernel_name or "shadow_kernel<true, true>" in kernel_name
             or "shadow_kernel<false, true>" in kernel_name):
         return "instrumented variant (counted frame only)"
     for k in RENDER:
