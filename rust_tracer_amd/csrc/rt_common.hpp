@@ -154,7 +154,7 @@ __device__ __forceinline__ float4 ld4(const float* p) { return make_float4(p[0],
 
 // Recompute the full Intersection of the chosen shape with the reference formulas
 // (sphere.rs:57-98, plane.rs:59-84, triangle.rs:51-94, cube.rs:89-102).
-__device__ Hit hit_attrs(const DevScene& S, uint32_t key, V3 o, V3 d, bool need_sphere_tex) {
+__device__ __forceinline__ Hit hit_attrs(const DevScene& S, uint32_t key, V3 o, V3 d, bool need_sphere_tex) {
     Hit h;
     const ShapeRec& R = S.shapes[key >> 4];
     h.mat = R.mat;

@@ -397,6 +397,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         uint32_t decided = 0;  // point lights whose shadow ray the own-shape test settled
         uint32_t mort = 0;  // Morton code of the shadow-ray origin (queue ordering key)
         V3 rro = v3(0, 0, 0), rrd = v3(0, 0, 0), tro = v3(0, 0, 0), trd = v3(0, 0, 0);
+        V3 sh_ps = v3(0, 0, 0), sh_n = v3(0, 0, 0);  // the hit's shadow-ray origin and normal
+        bool sh_entering = false;
+        uint32_t sh_key = 0;
         uint32_t it_load = 0, it_scan0 = 0, it_self0 = 0;  // phase accounting (instrumented variant)
         uint32_t it_scan_self = 0;  // scan cycles spent inside the self phase (inline shadow scans)
         if constexpr (CntT::kCount) {
@@ -439,48 +442,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 // PointLight::get_energy (mod.rs:189-206) decided here when the planes and
                 // the shape just hit settle it: a plane's t < 0 is the nearest hit; else any
                 // hit nearer than the light means the nearest one is too (shadow_scan)
-                uint32_t lit_pre = 0u;
-                if constexpr (CntT::kCount) it_scan_self = cnt.cyc_scan;
-                RT_T0(CntT, t_self);
-                if (P.self_shadow) {
-                    // the own shape can only shadow a light behind the offset point's
-                    // surface (or any light, from inside a sphere); elsewhere the test is
-                    // skipped (never deciding is always exact: the shadow pass decides)
-                    const uint32_t own_kind = (uint32_t)S.shapes[bk >> 4].kind;
-                    const bool own_any = own_kind == RT_SHAPE_SPHERE && !h.entering;
-                    const bool own_ok = own_kind == RT_SHAPE_SPHERE || own_kind == RT_SHAPE_TRIANGLE;
-                    for (int li = 0; li < S.n_lights; ++li) {
-                        const LightRec& L = S.lights[li];
-                        if (L.kind != RT_LIGHT_POINT) continue;
-                        const V3 lpos = v3(L.px, L.py, L.pz);
-                        if (!own_ok || !(own_any || dot(sub(lpos, ps), h.n) <= 0.f)) continue;
-                        const V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
-                        const float l2 = len2(sub(lpos, ps));
-                        float st = __builtin_huge_valf();
-                        uint32_t sk = 0xFFFFFFFFu;
-                        planes(S, ps, ldir, st, sk, cnt);
-                        if (!(st < 0.f)) own_shape_test(S, bk, ps, ldir, st, sk, cnt);
-                        if (shadow_decided(ps, ldir, st, l2)) {
-                            decided |= 1u << li;
-                            if (!shadow_hit(ps, ldir, st, l2)) lit_pre |= 1u << li;
-                        }
-                    }
-                    n_pre += (uint32_t)__builtin_popcount(decided);
-                }
-                if (level < P.inline_levels) {  // the level's remaining shadow rays, right here
-                    for (int li = 0; li < S.n_lights; ++li) {
-                        const LightRec& L = S.lights[li];
-                        if (L.kind != RT_LIGHT_POINT || ((decided >> li) & 1u)) continue;
-                        const V3 lpos = v3(L.px, L.py, L.pz);
-                        const V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
-                        if (!shadow_scan<LDS>(S, ps, ldir, lpos, cnt, lnodes, L.lb_base)) lit_pre |= 1u << li;
-                        decided |= 1u << li;
-                        n_pre++;
-                    }
-                }
-                RT_T1(CntT, cnt, cyc_self, t_self);
-                if constexpr (CntT::kCount) it_scan_self = cnt.cyc_scan - it_scan_self;
-                P.node_lit[n] = lit_pre;
+                sh_ps = ps;
+                sh_n = h.n;
+                sh_entering = h.entering;
+                sh_key = bk;
                 if (P.node_aux) {  // ray forest: what render_ray_tree re-reads at shade time
                     P.node_aux[n] = make_float4(__uint_as_float((uint32_t)h.mat), h.tu, h.tv,
                                                 __uint_as_float(h.entering ? 1u : 0u));
@@ -557,6 +522,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
             } else {
                 atomicOr(P.overflow, 1u);
             }
+        }
+        // ---- shadow rays the own shape decides, and (levels < inline_levels) the rest:
+        // after the node record and the children are out, so that little stays live
+        // across the shadow scans
+        if (hit) {
+            uint32_t lit_pre = 0u;
+            if constexpr (CntT::kCount) it_scan_self = cnt.cyc_scan;
+            RT_T0(CntT, t_self);
+            if (P.self_shadow) {
+                // the own shape can only shadow a light behind the offset point's
+                // surface (or any light, from inside a sphere); elsewhere the test is
+                // skipped (never deciding is always exact: the shadow pass decides)
+                const uint32_t own_kind = (uint32_t)S.shapes[sh_key >> 4].kind;
+                const bool own_any = own_kind == RT_SHAPE_SPHERE && !sh_entering;
+                const bool own_ok = own_kind == RT_SHAPE_SPHERE || own_kind == RT_SHAPE_TRIANGLE;
+                for (int li = 0; li < S.n_lights; ++li) {
+                    const LightRec& L = S.lights[li];
+                    if (L.kind != RT_LIGHT_POINT) continue;
+                    const V3 lpos = v3(L.px, L.py, L.pz);
+                    if (!own_ok || !(own_any || dot(sub(lpos, sh_ps), sh_n) <= 0.f)) continue;
+                    const V3 ldir = norm(sub(lpos, sh_ps));  // mod.rs:191
+                    const float l2 = len2(sub(lpos, sh_ps));
+                    float st = __builtin_huge_valf();
+                    uint32_t sk = 0xFFFFFFFFu;
+                    planes(S, sh_ps, ldir, st, sk, cnt);
+                    if (!(st < 0.f)) own_shape_test(S, sh_key, sh_ps, ldir, st, sk, cnt);
+                    if (shadow_decided(sh_ps, ldir, st, l2)) {
+                        decided |= 1u << li;
+                        if (!shadow_hit(sh_ps, ldir, st, l2)) lit_pre |= 1u << li;
+                    }
+                }
+                n_pre += (uint32_t)__builtin_popcount(decided);
+            }
+            if (level < P.inline_levels) {  // the level's remaining shadow rays, right here
+                for (int li = 0; li < S.n_lights; ++li) {
+                    const LightRec& L = S.lights[li];
+                    if (L.kind != RT_LIGHT_POINT || ((decided >> li) & 1u)) continue;
+                    const V3 lpos = v3(L.px, L.py, L.pz);
+                    const V3 ldir = norm(sub(lpos, sh_ps));  // mod.rs:191
+                    if (!shadow_scan<LDS>(S, sh_ps, ldir, lpos, cnt, lnodes, L.lb_base)) lit_pre |= 1u << li;
+                    decided |= 1u << li;
+                    n_pre++;
+                }
+            }
+            RT_T1(CntT, cnt, cyc_self, t_self);
+            if constexpr (CntT::kCount) it_scan_self = cnt.cyc_scan - it_scan_self;
+            P.node_lit[n] = lit_pre;
         }
         // ---- one shadow entry per point light, grouped by light within the wave
         // ([light a: this wave's hits in lane order][light b: ...]) so that a shadow wave
