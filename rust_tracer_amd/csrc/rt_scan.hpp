@@ -310,6 +310,25 @@ __device__ __forceinline__ unsigned long long* ops_slot(const DevScene& S) {
     return S.scan_ops + (blockIdx.x % RT_OPS_SLOTS) * RT_OPS_STRIDE;
 }
 
+// Leaf loops load record i + 1 while testing record i (RT_LEAF_PREFETCH=1, default) or
+// load each record at the top of its iteration (0: half the SGPRs, A/B)
+#ifndef RT_LEAF_PREFETCH
+#define RT_LEAF_PREFETCH 1
+#endif
+#if RT_LEAF_PREFETCH
+#define RT_PF_INIT(T, ld, p) T cur = ld(p);
+#define RT_PF_NEXT(T, ld, p, K) \
+    p += K;                     \
+    T nxt = ld(p);
+#define RT_PF_ADV cur = nxt;
+#else
+#define RT_PF_INIT(T, ld, p)
+#define RT_PF_NEXT(T, ld, p, K) \
+    T cur = ld(p);              \
+    p += K;
+#define RT_PF_ADV
+#endif
+
 // ------------------------------------------------------------------ linear runs
 // Group loops prefetch record i+1 before testing record i; every section is padded by
 // one group so the look-ahead load stays inside the allocation.
@@ -318,13 +337,12 @@ __device__ __forceinline__ void run_dsph(const DevScene& S, int b, int e, V3 o, 
                                          C& c) {
     if (b >= e) return;
     cfloat4* p = cptr(S.dsph) + 4 * b;
-    SphPair cur = ld_sph(p);
+    RT_PF_INIT(SphPair, ld_sph, p)
     for (int i = b; i < e; ++i) {
-        p += 4;
-        SphPair nxt = ld_sph(p);
+        RT_PF_NEXT(SphPair, ld_sph, p, 4)
         RT_OPS(c, dsph);
         sph_pair(cur, o, d, bt, bk);
-        cur = nxt;
+        RT_PF_ADV
     }
 }
 template <class C>
@@ -332,13 +350,12 @@ __device__ __forceinline__ void run_gsph(const DevScene& S, int b, int e, V3 o, 
                                          C& c) {
     if (b >= e) return;
     cfloat4* p = cptr(S.gsph) + 4 * b;
-    Rec16 cur = ld_rec(p);
+    RT_PF_INIT(Rec16, ld_rec, p)
     for (int i = b; i < e; ++i) {
-        p += 4;
-        Rec16 nxt = ld_rec(p);
+        RT_PF_NEXT(Rec16, ld_rec, p, 4)
         RT_OPS(c, gsph);
         sph_general(cur, o, d, bt, bk);
-        cur = nxt;
+        RT_PF_ADV
     }
 }
 template <class C>
@@ -346,13 +363,12 @@ __device__ __forceinline__ void run_tri(const DevScene& S, int b, int e, V3 o, V
                                         C& c) {
     if (b >= e) return;
     cfloat4* p = cptr(S.tri) + 6 * b;
-    TriPair cur = ld_tri(p);
+    RT_PF_INIT(TriPair, ld_tri, p)
     for (int i = b; i < e; ++i) {
-        p += 6;
-        TriPair nxt = ld_tri(p);
+        RT_PF_NEXT(TriPair, ld_tri, p, 6)
         RT_OPS(c, tri);
         tri_pair(cur, o, d, bt, bk);
-        cur = nxt;
+        RT_PF_ADV
     }
 }
 template <class C>
@@ -360,15 +376,14 @@ __device__ __forceinline__ void run_cube(const DevScene& S, int b, int e, V3 o, 
                                          C& c) {
     if (b >= e) return;
     cfloat4* p = cptr(S.cube) + 4 * b;
-    Rec16 cur = ld_rec(p);
+    RT_PF_INIT(Rec16, ld_rec, p)
     for (int i = b; i < e; ++i) {
-        p += 4;
-        Rec16 nxt = ld_rec(p);
+        RT_PF_NEXT(Rec16, ld_rec, p, 4)
         RT_OPS(c, cube);
         V3 to = pt_mul(cur.r0, cur.r1, cur.r2, o);
         V3 td = vec3_mul(cur.r0, cur.r1, cur.r2, d);
         cube_scan(to, td, keyof(cur.rk.x), bt, bk);
-        cur = nxt;
+        RT_PF_ADV
     }
 }
 
@@ -774,38 +789,35 @@ __device__ __forceinline__ void lb_leaf(const DevScene& S, uint32_t li, V3 o, V3
     const uint4 a = lp[0], b = lp[1];
     if (a.x < a.y) {
         cfloat4* p = cptr(S.dsph) + 4 * a.x;
-        SphPair cur = ld_sph(p);
+        RT_PF_INIT(SphPair, ld_sph, p)
         for (uint32_t i = a.x; i < a.y; ++i) {
-            p += 4;
-            SphPair nxt = ld_sph(p);
+            RT_PF_NEXT(SphPair, ld_sph, p, 4)
             if (cur.q3.w > reach) break;
             RT_OPS(c, dsph);
             sph_pair(cur, o, d, bt, bk);
-            cur = nxt;
+            RT_PF_ADV
         }
     }
     if (a.z < a.w) {
         cfloat4* p = cptr(S.gsph) + 4 * a.z;
-        Rec16 cur = ld_rec(p);
+        RT_PF_INIT(Rec16, ld_rec, p)
         for (uint32_t i = a.z; i < a.w; ++i) {
-            p += 4;
-            Rec16 nxt = ld_rec(p);
+            RT_PF_NEXT(Rec16, ld_rec, p, 4)
             if (cur.rk.w > reach) break;
             RT_OPS(c, gsph);
             sph_general(cur, o, d, bt, bk);
-            cur = nxt;
+            RT_PF_ADV
         }
     }
     if (b.x < b.y) {
         cfloat4* p = cptr(S.tri) + 6 * b.x;
-        TriPair cur = ld_tri(p);
+        RT_PF_INIT(TriPair, ld_tri, p)
         for (uint32_t i = b.x; i < b.y; ++i) {
-            p += 6;
-            TriPair nxt = ld_tri(p);
+            RT_PF_NEXT(TriPair, ld_tri, p, 6)
             if (cur.q5.x > reach) break;
             RT_OPS(c, tri);
             tri_pair(cur, o, d, bt, bk);
-            cur = nxt;
+            RT_PF_ADV
         }
     }
     if (b.z < b.w) {
