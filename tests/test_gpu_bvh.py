@@ -193,7 +193,8 @@ def test_shadow_shortcuts_change_nothing(scene):
     base, cb = _render_env(desc, w, h, depth, RT_LB_RES=0, RT_SELF_SHADOW=0)
     for env in ({}, {"RT_LB_RES": 8}, {"RT_LB_RES": 64}, {"RT_LB_RES": 200}, {"RT_SELF_SHADOW": 0},
                 {"RT_INLINE_SHADOW": 0}, {"RT_INLINE_SHADOW": 8, "RT_LB_RES": 16}, {"RT_GRAZE_RES": 0},
-                {"RT_GRAZE_RES": 8}):
+                {"RT_GRAZE_RES": 8}, {"RT_LB_REACH": 0}, {"RT_LB_REACH": 0, "RT_LB_RES": 128},
+                {"RT_TASK_W": 16, "RT_TASK_FILL": 64}):
         img, cnt = _render_env(desc, w, h, depth, **env)
         diff = np.flatnonzero(img.view(np.uint32) != base.view(np.uint32))
         assert diff.size == 0, (env, diff.size)
