@@ -1635,8 +1635,12 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     HIP_TRY(launch_wave_init(w.levels, RT_LEVEL_TABLE_WORDS, p.total_items, sample == 0 ? w.overflow : nullptr,
                              stream));
     HIP_TRY(launch_wave_trace(p, 0, tb, stream));
+    // RT_SORT_LEVELS: bit k set = level k's queue is sorted (A/B; default every level)
+    const char* sl = std::getenv("RT_SORT_LEVELS");
+    const uint64_t sort_levels = sl ? std::strtoull(sl, nullptr, 0) : ~0ull;
     for (uint32_t k = 1; k < levels; k++) {
-        if (sort_tasks) {
+        p.perm = nullptr;  // production order unless this level is sorted
+        if (sort_tasks && ((sort_levels >> (k < 64 ? k : 63)) & 1ull)) {
             HIP_TRY(launch_sort(w.levels, (int32_t)k, w.capacity, task_bits, w.task_keys, nullptr, sort_scratch, w.perm,
                                 tile_counts, digit_totals, 4 * s->num_cus, stream));
             p.perm = w.perm;
