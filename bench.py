@@ -8,7 +8,11 @@ src/render.rs:43-45).  Synthetic scene, no dataset.
 
 A step = one full frame: every rank renders its block-cyclic row bands with the HIP
 level-synchronous pipeline (culling hierarchy + ordered ray queues), then (N > 1) the bands are gathered to rank 0 over RCCL and un-permuted.
-The frame is fixed as N grows ("scaling": "strong").
+The frame is fixed as N grows ("scaling": "strong").  Consecutive frames are rendered with
+--inflight F frames in flight: F scene handles (one workspace each) on F HIP streams, so
+the latency-bound tails of one frame's trace levels overlap the next frames' work.  Every
+frame is rendered and (N > 1) gathered in full; `frame_latency_ms` reports one frame's
+own duration beside the throughput.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -54,6 +58,9 @@ def parse():
     p.add_argument("--spp", type=int, default=None, help="samples per pixel (default: 64 for config 5, else 1)")
     p.add_argument("--seed", type=int, default=None, help="jitter seed (default: 3 for config 5)")
     p.add_argument("--band-rows", type=int, default=8)
+    p.add_argument("--inflight", type=int, default=None,
+                   help="frames in flight (F scene handles / HIP streams; default 4 at N = 1 -- the "
+                        "box's 4 hardware queues -- and 3 at N > 1, leaving a queue to RCCL); 1 = one at a time")
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU oracle timing")
     p.add_argument("--cpu-rows-step", type=int, default=None,
                    help="CPU baseline renders every k-th row of the frame")
@@ -140,8 +147,14 @@ def main():
 
     desc = SceneDesc.synth_config(args.config)
     scene = DeviceScene(desc, device=dev.index)
-    tiler = FrameTiler(scene, args.width, args.height, args.depth, args.band_rows, rank, world, dev,
-                       spp=args.spp, seed=args.seed)
+    inflight = max(1, args.inflight or (4 if world == 1 else 3))
+    tilers = [FrameTiler(scene if i == 0 else DeviceScene(desc, device=dev.index), args.width, args.height,
+                         args.depth, args.band_rows, rank, world, dev, spp=args.spp, seed=args.seed)
+              for i in range(inflight)]
+    tiler = tilers[0]
+    main_stream = torch.cuda.current_stream(dev)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(inflight)]
+    reuse = [None] * inflight  # event after the gather that last read slot i's band buffer
 
     def barrier():
         if world > 1:
@@ -150,8 +163,33 @@ def main():
             else:
                 dist.barrier()
 
-    for _ in range(args.warmup):
-        tiler.step()
+    def run_frames(n, lat=None):
+        """n frames, frame k on slot k % inflight (its own scene handle, workspace, stream);
+        N > 1: each frame's gather + un-permute on the main stream once its slot is done."""
+        for s in streams:
+            s.wait_stream(main_stream)
+        for k in range(n):
+            i = k % inflight
+            with torch.cuda.stream(streams[i]):
+                if reuse[i] is not None:
+                    streams[i].wait_event(reuse[i])
+                if lat is not None:
+                    lat[k][0].record(streams[i])
+                tilers[i].render_local()       # the render pipeline, on slot i's stream
+                if lat is not None:
+                    lat[k][1].record(streams[i])
+            if world > 1:
+                main_stream.wait_stream(streams[i])
+                tilers[i].assemble()
+                reuse[i] = torch.cuda.Event()
+                reuse[i].record(main_stream)
+        for s in streams:
+            main_stream.wait_stream(s)
+
+    # slot set-up (untimed, like the scene upload): each extra slot's workspace is sized by
+    # its first frame
+    run_frames(inflight)
+    run_frames(args.warmup)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -165,23 +203,26 @@ def main():
         torch.cuda.synchronize()
         ops = scene.scan_ops()
         scene.set_scan_counting(False)
-    tiler.counters.zero_()
+    for t in tilers:
+        t.counters.zero_()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    lat = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record()
-        tiler.render_local()       # the render pipeline, on torch's current stream
-        ev[k][1].record()
-        tiler.assemble()
+    ev[0].record(main_stream)
+    run_frames(args.steps, lat)
+    ev[1].record(main_stream)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    cnt = tiler.counters.double()
+    # the timed region's HIP events (main stream, joined with every slot stream) / K: the
+    # render pipeline's time per frame at steady state; one frame's own span beside it
+    kernel_ms = ev[0].elapsed_time(ev[1]) / args.steps
+    latency_ms = sum(a.elapsed_time(b) for a, b in lat) / args.steps
+    cnt = sum(t.counters.double() for t in tilers)
     local_scans = float(cnt[0] + cnt[1]) / args.steps   # this rank's launch (for the roofline)
     red_dev = dev if args.backend == "nccl" else torch.device("cpu")
     stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=red_dev)
@@ -191,14 +232,16 @@ def main():
         dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
     frame_check = None
     if args.check:
-        frame = tiler.step()
+        # the timed frames' last assembled frame of every slot, then a fresh single frame,
+        # against one rt_render_spp launch of the whole frame
+        frames = [t.frame.cpu().numpy() if t.frame is not None else None for t in tilers]
+        frames.append(tiler.step().cpu().numpy() if rank == 0 else tiler.step())
         torch.cuda.synchronize()
         if rank == 0:
             import numpy as np
             ref, _, _, _ = scene.render(args.width, args.height, args.depth, device=dev.index, spp=args.spp,
                                         seed=args.seed)
-            got = frame.cpu().numpy()
-            frame_check = bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32)))
+            frame_check = all(bool(np.array_equal(f.view(np.uint32), ref.view(np.uint32))) for f in frames)
     elapsed, kernel_ms_max = stats.tolist()
     node_rays, shadow_rays, pixels = cnt.tolist()
 
@@ -223,6 +266,8 @@ def main():
             "kernel": ("one frame: trace_level_kernel per level + queue sorts + shadow_kernel + "
                        "combine_level_kernel per level"),
             "kernel_ms": round(kernel_ms, 4),
+            "kernel_ms_is": (f"timed-region HIP events / steps with {inflight} frames in flight"
+                             if inflight > 1 else "timed-region HIP events / steps"),
             "flops_per_launch": per_launch_flops,
             "tests_per_launch": {k: v for k, v in ops.items() if not k.startswith("cycles")} if ops else None,
             "cycles_per_launch": {k: v for k, v in ops.items() if k.startswith("cycles")} if ops else None,
@@ -257,6 +302,7 @@ def main():
                 "width": args.width, "height": args.height, "depth": args.depth,
                 "leaf_primitives": 100 if args.config == 2 else 1000,
                 "spp": args.spp, "seed": args.seed, "band_rows": args.band_rows,
+                "frames_in_flight": inflight, "frame_latency_ms": round(latency_ms, 4),
                 "msamples_per_s": round(args.width * args.height * args.spp * steps / elapsed / 1e6, 3),
                 "parallelism": f"row-bands x{world}" + ((" + RCCL gather" if args.backend == "nccl"
                                                           else f" + {args.backend} gather (rehearsal)")

@@ -77,12 +77,24 @@ def main(tag):
     # split the dispatches into frames at each wave_init (bench.py: warm-up + one counted
     # frame + timed frames); a family's ms per frame averages the frames it ran in (the
     # counted frame runs the instrumented kernels instead of the default ones)
+    # frames in flight (bench.py --inflight) run on their own streams: split per stream
     frame_sums = []
+    open_frame = {}
     for r in sorted(keep, key=lambda r: int(r["Start_Timestamp"])):
         fam = family(r["Kernel_Name"])
-        if fam == "wave_init_kernel" or not frame_sums:
-            frame_sums.append(defaultdict(int))
-        frame_sums[-1][fam] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        sid = r.get("Stream_Id", "0")
+        if fam == "wave_init_kernel" or sid not in open_frame:
+            open_frame[sid] = defaultdict(int)
+            frame_sums.append(open_frame[sid])
+        open_frame[sid][fam] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    # the timed frames: every dispatch after the counted (instrumented) frame; their wall
+    # span / their number is what bench.py's timed-region HIP events measure per frame
+    inst_end = max((int(r["End_Timestamp"]) for r in keep
+                    if family(r["Kernel_Name"]).startswith("instrumented")), default=0)
+    timed = [r for r in keep if int(r["Start_Timestamp"]) > inst_end]
+    n_timed = sum(1 for r in timed if "wave_init_kernel" in r["Kernel_Name"])
+    span_ms = ((max(int(r["End_Timestamp"]) for r in timed) - min(int(r["Start_Timestamp"]) for r in timed))
+               / max(1, n_timed) / 1e6) if timed else 0.0
     frames = len(frame_sums)
     fams = {f for fs in frame_sums for f in fs}
     fam_ms = {f: sum(fs[f] for fs in frame_sums if f in fs) / sum(1 for fs in frame_sums if f in fs) / 1e6
@@ -117,7 +129,11 @@ def main(tag):
         "|---|---|",
     ] + [f"| {k} | {v:.3f} |" for k, v in sorted(fam_ms.items(), key=lambda x: -x[1])] + [
         "",
-        f"Sum of the default kernels per frame: {timed_ms:.3f} ms (bench HIP events: {frame_ms} ms).",
+        f"Sum of the default kernels per frame: {timed_ms:.3f} ms (kernel-busy time; with "
+        f"{bench['config'].get('frames_in_flight', 1)} frames in flight the frames' kernels overlap).",
+        "",
+        f"Timed frames ({n_timed}) in the trace run: wall span per frame {span_ms:.3f} ms "
+        f"(bench HIP events over the timed region: {frame_ms} ms per frame).",
         "",
         "## PMC (per frame, separate passes, render kernels only)",
         "",
