@@ -59,8 +59,8 @@ def parse():
     p.add_argument("--seed", type=int, default=None, help="jitter seed (default: 3 for config 5)")
     p.add_argument("--band-rows", type=int, default=8)
     p.add_argument("--inflight", type=int, default=None,
-                   help="frames in flight (F scene handles / HIP streams; default 4 at N = 1 -- the "
-                        "box's 4 hardware queues -- and 3 at N > 1, leaving a queue to RCCL); 1 = one at a time")
+                   help="frames in flight (F scene handles / HIP streams; default 4 = the box's hardware "
+                        "queues per process); 1 = one at a time")
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU oracle timing")
     p.add_argument("--cpu-rows-step", type=int, default=None,
                    help="CPU baseline renders every k-th row of the frame")
@@ -147,7 +147,7 @@ def main():
 
     desc = SceneDesc.synth_config(args.config)
     scene = DeviceScene(desc, device=dev.index)
-    inflight = max(1, args.inflight or (4 if world == 1 else 3))
+    inflight = max(1, args.inflight or 4)
     tilers = [FrameTiler(scene if i == 0 else DeviceScene(desc, device=dev.index), args.width, args.height,
                          args.depth, args.band_rows, rank, world, dev, spp=args.spp, seed=args.seed)
               for i in range(inflight)]

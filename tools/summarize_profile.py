@@ -37,6 +37,41 @@ def family(kernel_name):
     return None
 
 
+def trace_frames(keep):
+    """per-frame ms of each render kernel family, and the timed frames' wall span per frame"""
+    # kernel-trace: split the dispatches into frames at each wave_init (bench.py: slot
+    # set-up + warm-up + one counted frame + timed frames); frames in flight (bench.py
+    # --inflight) run on their own streams, so the split is per stream; a family's ms per
+    # frame averages the frames it ran in (the counted frame runs the instrumented kernels)
+    frame_sums = []
+    open_frame = {}
+    for r in sorted(keep, key=lambda r: int(r["Start_Timestamp"])):
+        fam = family(r["Kernel_Name"])
+        sid = r.get("Stream_Id", "0")
+        if fam == "wave_init_kernel" or sid not in open_frame:
+            open_frame[sid] = defaultdict(int)
+            frame_sums.append(open_frame[sid])
+        open_frame[sid][fam] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    # the timed frames: every dispatch after the counted (instrumented) frame; their wall
+    # span / their number is what bench.py's timed-region HIP events measure per frame
+    inst_end = max((int(r["End_Timestamp"]) for r in keep
+                    if family(r["Kernel_Name"]).startswith("instrumented")), default=0)
+    timed = [r for r in keep if int(r["Start_Timestamp"]) > inst_end]
+    n_timed = sum(1 for r in timed if "wave_init_kernel" in r["Kernel_Name"])
+    span_ms = ((max(int(r["End_Timestamp"]) for r in timed) - min(int(r["Start_Timestamp"]) for r in timed))
+               / max(1, n_timed) / 1e6) if timed else 0.0
+    fams = {f for fs in frame_sums for f in fs}
+    fam_ms = {f: sum(fs[f] for fs in frame_sums if f in fs) / sum(1 for fs in frame_sums if f in fs) / 1e6
+              for f in fams}
+    timed_ms = sum(v for f, v in fam_ms.items() if not f.startswith("instrumented"))
+    return len(frame_sums), fam_ms, timed_ms, n_timed, span_ms
+
+
+def render_rows(path):
+    rows = list(csv.DictReader(open(path)))
+    return [r for r in rows if any(k in r["Kernel_Name"] for k in RENDER)]
+
+
 def main(tag):
     src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles", tag)
@@ -73,33 +108,7 @@ def main(tag):
         for k in agg:
             pmc_frames[k] = max(1, len(inits))
         pmc.update({k: v / pmc_frames[k] for k, v in agg.items()})
-    # kernel-trace: per-frame time of each render kernel family (the trace run did 1 + 3 frames)
-    # split the dispatches into frames at each wave_init (bench.py: warm-up + one counted
-    # frame + timed frames); a family's ms per frame averages the frames it ran in (the
-    # counted frame runs the instrumented kernels instead of the default ones)
-    # frames in flight (bench.py --inflight) run on their own streams: split per stream
-    frame_sums = []
-    open_frame = {}
-    for r in sorted(keep, key=lambda r: int(r["Start_Timestamp"])):
-        fam = family(r["Kernel_Name"])
-        sid = r.get("Stream_Id", "0")
-        if fam == "wave_init_kernel" or sid not in open_frame:
-            open_frame[sid] = defaultdict(int)
-            frame_sums.append(open_frame[sid])
-        open_frame[sid][fam] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    # the timed frames: every dispatch after the counted (instrumented) frame; their wall
-    # span / their number is what bench.py's timed-region HIP events measure per frame
-    inst_end = max((int(r["End_Timestamp"]) for r in keep
-                    if family(r["Kernel_Name"]).startswith("instrumented")), default=0)
-    timed = [r for r in keep if int(r["Start_Timestamp"]) > inst_end]
-    n_timed = sum(1 for r in timed if "wave_init_kernel" in r["Kernel_Name"])
-    span_ms = ((max(int(r["End_Timestamp"]) for r in timed) - min(int(r["Start_Timestamp"]) for r in timed))
-               / max(1, n_timed) / 1e6) if timed else 0.0
-    frames = len(frame_sums)
-    fams = {f for fs in frame_sums for f in fs}
-    fam_ms = {f: sum(fs[f] for fs in frame_sums if f in fs) / sum(1 for fs in frame_sums if f in fs) / 1e6
-              for f in fams}
-    timed_ms = sum(v for f, v in fam_ms.items() if not f.startswith("instrumented"))
+    frames, fam_ms, timed_ms, n_timed, span_ms = trace_frames(keep)
     fetch_b = pmc.get("FETCH_SIZE", 0.0) * 1024
     write_b = pmc.get("WRITE_SIZE", 0.0) * 1024
     traffic = {
@@ -133,8 +142,32 @@ def main(tag):
         f"{bench['config'].get('frames_in_flight', 1)} frames in flight the frames' kernels overlap).",
         "",
         f"Timed frames ({n_timed}) in the trace run: wall span per frame {span_ms:.3f} ms "
-        f"(bench HIP events over the timed region: {frame_ms} ms per frame).",
+        f"(bench HIP events over the timed region: {frame_ms} ms per frame; the tracer's per-dispatch "
+        f"bookkeeping stretches overlapped frames -- at --inflight 1 below the two agree).",
         "",
+    ]
+    t1 = os.path.join(src, "trace1", "run_kernel_trace.csv")
+    b1 = os.path.join(src, "bench1.json")
+    if os.path.exists(t1) and os.path.exists(b1):
+        bench1 = json.load(open(b1))
+        shutil.copy(os.path.join(src, "trace1", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats_inflight1.csv"))
+        shutil.copy(b1, os.path.join(dst, "bench_inflight1.json"))
+        f1, fam1, sum1, nt1, span1 = trace_frames(render_rows(t1))
+        lines += [
+            "## One frame at a time (bench.py --inflight 1; rocprofv3 kernel trace of the same command)",
+            "",
+            f"bench.py --inflight 1: {bench1['value']} Mpixels/s, render pipeline {bench1['roofline']['kernel_ms']} ms "
+            f"per frame (HIP events).",
+            "",
+            "| kernel family | ms per frame |",
+            "|---|---|",
+        ] + [f"| {k} | {v:.3f} |" for k, v in sorted(fam1.items(), key=lambda x: -x[1])] + [
+            "",
+            f"Sum of the default kernels per frame: {sum1:.3f} ms; timed frames ({nt1}) wall span per frame "
+            f"{span1:.3f} ms (bench HIP events: {bench1['roofline']['kernel_ms']} ms).",
+            "",
+        ]
+    lines += [
         "## PMC (per frame, separate passes, render kernels only)",
         "",
         "| counter | value |",
