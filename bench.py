@@ -49,7 +49,7 @@ OP_FLOPS = {"node_pairs": 24, "dsph_pairs": 2 * 57, "gsph": 57, "tri_pairs": 2 *
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", type=int, default=3, help="BASELINE config (2..5 synth scenes)")
     p.add_argument("--width", type=int, default=None, help="default: the config's (1920 / 3840)")
