@@ -62,6 +62,8 @@ def parse():
                    help="frames in flight (F scene handles / HIP streams; default 4 = the box's hardware "
                         "queues per process); 1 = one at a time")
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU oracle timing")
+    p.add_argument("--cpu-threads", type=int, default=None,
+                   help="threads of the multi-core CPU baseline (default: OMP_NUM_THREADS, else <= 16)")
     p.add_argument("--cpu-rows-step", type=int, default=None,
                    help="CPU baseline renders every k-th row of the frame")
     p.add_argument("--backend", default="nccl", help="nccl (RCCL) or gloo (CPU rehearsal)")
@@ -111,6 +113,38 @@ def cpu_baseline(args, desc):
                   f"benchmark frame, {cnt['pixels'] // args.spp} pixels x {args.spp} spp, {dt:.1f} s, single thread "
                   f"(C++ restatement of src/render.rs, g++ -O2 -ffp-contract=off); "
                   f"host: {os.cpu_count()} logical CPUs",
+        "seconds": round(dt, 2),
+        "multicore": cpu_baseline_mt(args, o),
+    }
+
+
+def cpu_threads(args):
+    if args.cpu_threads:
+        return args.cpu_threads
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return min(16, len(os.sched_getaffinity(0)))
+
+
+def cpu_baseline_mt(args, o):
+    """The same oracle, rows dealt over T host threads (pixel-parallel over
+    the host cores), on every k/T-th row: about the single-thread run's wall time."""
+    threads = cpu_threads(args)
+    if threads <= 1:
+        return None
+    step = max(1, args.cpu_rows_step // threads)
+    rows = range(0, args.height, step)
+    t0 = time.perf_counter()
+    _, cnt = o.render(args.width, args.height, args.depth, rows=(0, args.height, step), threads=threads,
+                      spp=args.spp, seed=args.seed)
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(cnt["pixels"] / args.spp / dt / 1e6, 6),
+        "unit": "Mpixels/s",
+        "cores": threads,
+        "sample": f"{len(rows)} of {args.height} rows (every {step}th), {cnt['pixels'] // args.spp} pixels x "
+                  f"{args.spp} spp, {dt:.1f} s, {threads} threads (the box's CPU share per GPU)",
         "seconds": round(dt, 2),
     }
 
