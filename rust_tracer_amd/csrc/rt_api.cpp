@@ -1629,6 +1629,15 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     int tb = s->num_cus * s->occ_trace;
     int sb = s->num_cus * s->occ_shadow;
     int cb = s->num_cus * s->occ_combine;
+    {
+        // A/B: RT_GRID_PCT = persistent grids at this % of a full chip (trace, shadow)
+        const char* e = std::getenv("RT_GRID_PCT");
+        const int pct = e ? std::atoi(e) : 100;
+        if (pct > 0 && pct < 100) {
+            tb = std::max(1, tb * pct / 100);
+            sb = std::max(1, sb * pct / 100);
+        }
+    }
     uint32_t levels = depth > 0 ? depth : 1;
     // Every launch sizes itself from the device-side level counts: the whole frame is
     // enqueued without a host round trip (levels past the deepest non-empty one are no-ops).

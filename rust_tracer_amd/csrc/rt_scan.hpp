@@ -647,6 +647,9 @@ __device__ __forceinline__ uint32_t lb_cell(uint32_t res, V3 v) {
 // With direction cells (S.graze_res): the wave ORs the pair masks of its lanes' cells
 // (a superset of the pairs any lane grazes) and runs the per-triangle test on those.
 // The lane's first two mask words, loaded when its scan starts (latency hidden by the walk).
+#ifndef RT_GRAZE_PF
+#define RT_GRAZE_PF 0  // A/B: prefetch the next grazing pair's normals (measured: no gain, 2.97 vs 2.97 ms at F = 4, 4.54 vs 4.52 at F = 1)
+#endif
 struct GrazePre {
     uint32_t m0, m1;
 };
@@ -676,6 +679,35 @@ __device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float&
             for (int o2 = 32; o2 > 0; o2 >>= 1) m |= (uint32_t)__shfl_xor((int)m, o2);
             m = (uint32_t)__builtin_amdgcn_readfirstlane((int)m);
             RT_OPS(c, graze);
+#if RT_GRAZE_PF
+            // software-pipelined: the next pair's normals are requested before this pair's
+            // test (wave-uniform SMEM loads; the order of the tests is unchanged)
+            if (m) {
+                uint32_t pi = 32u * w + (uint32_t)__builtin_ctz(m);
+                m &= m - 1u;
+                float4 a = pn[2 * pi], b = pn[2 * pi + 1];
+                for (;;) {
+                    const bool more = m != 0u;
+                    uint32_t npi = pi;
+                    if (more) {
+                        npi = 32u * w + (uint32_t)__builtin_ctz(m);
+                        m &= m - 1u;
+                    }
+                    const float4 na = pn[2 * npi], nb = pn[2 * npi + 1];
+                    f2 nn = (bc(d.x) * f2{a.x, a.y} + bc(d.y) * f2{a.z, a.w}) + bc(d.z) * f2{b.x, b.y};
+                    nn *= nn;
+                    RT_OPS(c, graze_n);
+                    if (__ballot(nn.x < lim || nn.y < lim)) {
+                        RT_OPS(c, tri);
+                        tri_pair(ld_tri(tp + 6 * pi), o, d, bt, bk);
+                    }
+                    if (!more) break;
+                    pi = npi;
+                    a = na;
+                    b = nb;
+                }
+            }
+#else
             while (m) {
                 const uint32_t pi = 32u * w + (uint32_t)__builtin_ctz(m);
                 m &= m - 1u;
@@ -688,6 +720,7 @@ __device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float&
                     tri_pair(ld_tri(tp + 6 * pi), o, d, bt, bk);
                 }
             }
+#endif
         }
         RT_T1(C, c, cyc_graze, t_g);
         return;
