@@ -177,18 +177,16 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from rust_tracer_amd import DeviceScene, SceneDesc
-    from rust_tracer_amd.dist import FrameTiler
+    from rust_tracer_amd.dist import FramePipeline
 
     desc = SceneDesc.synth_config(args.config)
     scene = DeviceScene(desc, device=dev.index)
     inflight = max(1, args.inflight or 4)
-    tilers = [FrameTiler(scene if i == 0 else DeviceScene(desc, device=dev.index), args.width, args.height,
-                         args.depth, args.band_rows, rank, world, dev, spp=args.spp, seed=args.seed)
-              for i in range(inflight)]
+    pipe = FramePipeline(scene, desc, args.width, args.height, args.depth, args.band_rows, rank, world, dev,
+                         spp=args.spp, seed=args.seed, inflight=inflight)
+    tilers = pipe.tilers
     tiler = tilers[0]
     main_stream = torch.cuda.current_stream(dev)
-    streams = [torch.cuda.Stream(device=dev) for _ in range(inflight)]
-    reuse = [None] * inflight  # event after the gather that last read slot i's band buffer
 
     def barrier():
         if world > 1:
@@ -197,28 +195,7 @@ def main():
             else:
                 dist.barrier()
 
-    def run_frames(n, lat=None):
-        """n frames, frame k on slot k % inflight (its own scene handle, workspace, stream);
-        N > 1: each frame's gather + un-permute on the main stream once its slot is done."""
-        for s in streams:
-            s.wait_stream(main_stream)
-        for k in range(n):
-            i = k % inflight
-            with torch.cuda.stream(streams[i]):
-                if reuse[i] is not None:
-                    streams[i].wait_event(reuse[i])
-                if lat is not None:
-                    lat[k][0].record(streams[i])
-                tilers[i].render_local()       # the render pipeline, on slot i's stream
-                if lat is not None:
-                    lat[k][1].record(streams[i])
-            if world > 1:
-                main_stream.wait_stream(streams[i])
-                tilers[i].assemble()
-                reuse[i] = torch.cuda.Event()
-                reuse[i].record(main_stream)
-        for s in streams:
-            main_stream.wait_stream(s)
+    run_frames = pipe.run
 
     # slot set-up (untimed, like the scene upload): each extra slot's workspace is sized by
     # its first frame
@@ -237,8 +214,7 @@ def main():
         torch.cuda.synchronize()
         ops = scene.scan_ops()
         scene.set_scan_counting(False)
-    for t in tilers:
-        t.counters.zero_()
+    pipe.zero_counters()
 
     lat = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
@@ -256,7 +232,7 @@ def main():
     # render pipeline's time per frame at steady state; one frame's own span beside it
     kernel_ms = ev[0].elapsed_time(ev[1]) / args.steps
     latency_ms = sum(a.elapsed_time(b) for a, b in lat) / args.steps
-    cnt = sum(t.counters.double() for t in tilers)
+    cnt = pipe.counters.double()
     local_scans = float(cnt[0] + cnt[1]) / args.steps   # this rank's launch (for the roofline)
     red_dev = dev if args.backend == "nccl" else torch.device("cpu")
     stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=red_dev)

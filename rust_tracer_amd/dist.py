@@ -88,3 +88,67 @@ class FrameTiler:
     def step(self):
         self.render_local()
         return self.assemble()
+
+
+class FramePipeline:
+    """Consecutive frames with `inflight` frames in flight (DESIGN.md "Frames in flight").
+
+    Slot i = its own scene handle (rt_scene_create: its own workspace; one handle never
+    runs two renders at once, mirroring the reference's !Sync Scene) + its own HIP stream
+    + its own FrameTiler.  Frame k renders on slot k % inflight.  At world > 1 each frame's
+    gather + un-permute runs on the caller's stream once its slot is done, and the slot's
+    next render waits on an event recorded after that gather (the gather reads the slot's
+    band buffer).  Every frame is rendered and gathered in full."""
+
+    def __init__(self, scene: DeviceScene, desc, width, height, depth, band_rows=8, rank=0, world=1,
+                 device=None, spp=1, seed=0, inflight=4):
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.inflight = max(1, int(inflight))
+        self.world = world
+        self.tilers = [FrameTiler(scene if i == 0 else DeviceScene(desc, device=self.device.index), width, height,
+                                  depth, band_rows, rank, world, self.device, spp=spp, seed=seed)
+                       for i in range(self.inflight)]
+        self.streams = [torch.cuda.Stream(device=self.device) for _ in range(self.inflight)]
+        self._reuse = [None] * self.inflight
+
+    @property
+    def counters(self):
+        """node rays, shadow rays, pixels summed over the slots"""
+        return sum(t.counters for t in self.tilers)
+
+    def zero_counters(self):
+        for t in self.tilers:
+            t.counters.zero_()
+
+    def run(self, n, latency_events=None):
+        """Enqueue n frames (asynchronous); the caller's stream waits for all of them.
+        latency_events[k] = (start, end) events recorded around frame k's render."""
+        main = torch.cuda.current_stream(self.device)
+        for s in self.streams:
+            s.wait_stream(main)
+        for k in range(n):
+            i = k % self.inflight
+            st = self.streams[i]
+            with torch.cuda.stream(st):
+                if self._reuse[i] is not None:
+                    st.wait_event(self._reuse[i])
+                if latency_events is not None:
+                    latency_events[k][0].record(st)
+                self.tilers[i].render_local()
+                if latency_events is not None:
+                    latency_events[k][1].record(st)
+            if self.world > 1:
+                main.wait_stream(st)
+                self.tilers[i].assemble()
+                self._reuse[i] = torch.cuda.Event()
+                self._reuse[i].record(main)
+        for s in self.streams:
+            main.wait_stream(s)
+
+    def frames(self):
+        """each slot's last assembled frame (rank 0; None elsewhere)"""
+        return [t.frame for t in self.tilers]
+
+    def close(self):
+        for t in self.tilers[1:]:
+            t.scene.close()
