@@ -10,9 +10,11 @@ A step = one full frame: every rank renders its block-cyclic row bands with the 
 level-synchronous pipeline (culling hierarchy + ordered ray queues), then (N > 1) the bands are gathered to rank 0 over RCCL and un-permuted.
 The frame is fixed as N grows ("scaling": "strong").  Consecutive frames are rendered with
 --inflight F frames in flight: F scene handles (one workspace each) on F HIP streams, so
-the latency-bound tails of one frame's trace levels overlap the next frames' work.  Every
-frame is rendered and (N > 1) gathered in full; `frame_latency_ms` reports one frame's
-own duration beside the throughput.
+the latency-bound tails of one frame's trace levels overlap the next frames' work, and
+each pass renders --batch B frames in one pipeline (rt_render_bands_batch_async: the frame
+index sits above every queue-key bit, so no wave mixes frames).  Every frame is rendered
+and (N > 1) gathered in full; `pass_latency_ms` reports one pass's own duration beside
+the throughput.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -58,6 +60,9 @@ def parse():
     p.add_argument("--spp", type=int, default=None, help="samples per pixel (default: 64 for config 5, else 1)")
     p.add_argument("--seed", type=int, default=None, help="jitter seed (default: 3 for config 5)")
     p.add_argument("--band-rows", type=int, default=8)
+    p.add_argument("--batch", type=int, default=None,
+                   help="frames per pipeline pass (rt_render_bands_batch_async, <= 4; default: 1 at N = 1 "
+                        "or spp > 1, else 4 while a pass stays within 4 x 1080p of pixels per rank)")
     p.add_argument("--inflight", type=int, default=None,
                    help="frames in flight (F scene handles / HIP streams; default 4 = the box's hardware "
                         "queues per process); 1 = one at a time")
@@ -176,14 +181,21 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    from rust_tracer_amd import DeviceScene, SceneDesc
+    from rust_tracer_amd import DeviceScene, SceneDesc, band_rows_per_rank
     from rust_tracer_amd.dist import FramePipeline
 
     desc = SceneDesc.synth_config(args.config)
     scene = DeviceScene(desc, device=dev.index)
     inflight = max(1, args.inflight or 4)
+    if args.batch is None:
+        # N > 1 shares are latency-bound: 4 frames per pass (bounded workspace: <= 4 x 1080p
+        # of pixels per pass and rank); a whole frame per GPU gains ~2% from batching, so
+        # N = 1 renders one frame per pass (DESIGN.md "Frame batches")
+        share = band_rows_per_rank(args.height, args.band_rows, world) * args.width
+        args.batch = 1 if (args.spp > 1 or world == 1) else max(1, min(4, (4 * 1920 * 1088) // share))
     pipe = FramePipeline(scene, desc, args.width, args.height, args.depth, args.band_rows, rank, world, dev,
-                         spp=args.spp, seed=args.seed, inflight=inflight)
+                         spp=args.spp, seed=args.seed, inflight=inflight, batch=args.batch)
+    batch = pipe.batch
     tilers = pipe.tilers
     tiler = tilers[0]
     main_stream = torch.cuda.current_stream(dev)
@@ -197,9 +209,9 @@ def main():
 
     run_frames = pipe.run
 
-    # slot set-up (untimed, like the scene upload): each extra slot's workspace is sized by
-    # its first frame
-    run_frames(inflight)
+    # slot set-up (untimed, like the scene upload): each slot's workspace is sized by its
+    # first full pass
+    run_frames(inflight * batch)
     run_frames(args.warmup)
     torch.cuda.synchronize()
     barrier()
@@ -216,8 +228,7 @@ def main():
         scene.set_scan_counting(False)
     pipe.zero_counters()
 
-    lat = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    lat = []  # one (start, end) event pair per pass
     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     t0 = time.perf_counter()
     ev[0].record(main_stream)
@@ -231,7 +242,7 @@ def main():
     # the timed region's HIP events (main stream, joined with every slot stream) / K: the
     # render pipeline's time per frame at steady state; one frame's own span beside it
     kernel_ms = ev[0].elapsed_time(ev[1]) / args.steps
-    latency_ms = sum(a.elapsed_time(b) for a, b in lat) / args.steps
+    latency_ms = sum(a.elapsed_time(b) for a, b in lat) / max(1, len(lat))  # one pass of `batch` frames
     cnt = pipe.counters.double()
     local_scans = float(cnt[0] + cnt[1]) / args.steps   # this rank's launch (for the roofline)
     red_dev = dev if args.backend == "nccl" else torch.device("cpu")
@@ -244,8 +255,10 @@ def main():
     if args.check:
         # the timed frames' last assembled frame of every slot, then a fresh single frame,
         # against one rt_render_spp launch of the whole frame
-        frames = [t.frame.cpu().numpy() if t.frame is not None else None for t in tilers]
-        frames.append(tiler.step().cpu().numpy() if rank == 0 else tiler.step())
+        frames = [f.cpu().numpy() for f in pipe.frames()]
+        single = tiler.step()
+        if rank == 0:
+            frames.append(single.cpu().numpy())
         torch.cuda.synchronize()
         if rank == 0:
             import numpy as np
@@ -276,8 +289,8 @@ def main():
             "kernel": ("one frame: trace_level_kernel per level + queue sorts + shadow_kernel + "
                        "combine_level_kernel per level"),
             "kernel_ms": round(kernel_ms, 4),
-            "kernel_ms_is": (f"timed-region HIP events / steps with {inflight} frames in flight"
-                             if inflight > 1 else "timed-region HIP events / steps"),
+            "kernel_ms_is": (f"timed-region HIP events / steps ({inflight} passes of {batch} frames in flight)"
+                             if inflight * batch > 1 else "timed-region HIP events / steps"),
             "flops_per_launch": per_launch_flops,
             "tests_per_launch": {k: v for k, v in ops.items() if not k.startswith("cycles")} if ops else None,
             "cycles_per_launch": {k: v for k, v in ops.items() if k.startswith("cycles")} if ops else None,
@@ -312,7 +325,8 @@ def main():
                 "width": args.width, "height": args.height, "depth": args.depth,
                 "leaf_primitives": 100 if args.config == 2 else 1000,
                 "spp": args.spp, "seed": args.seed, "band_rows": args.band_rows,
-                "frames_in_flight": inflight, "frame_latency_ms": round(latency_ms, 4),
+                "frames_in_flight": inflight * batch, "passes_in_flight": inflight,
+                "frames_per_pass": batch, "pass_latency_ms": round(latency_ms, 4),
                 "msamples_per_s": round(args.width * args.height * args.spp * steps / elapsed / 1e6, 3),
                 "parallelism": f"row-bands x{world}" + ((" + RCCL gather" if args.backend == "nccl"
                                                           else f" + {args.backend} gather (rehearsal)")

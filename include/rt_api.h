@@ -174,6 +174,16 @@ rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* camera,
                                 uint32_t world, float* d_rgb, uint64_t* d_counters,
                                 void* stream);
 
+/* Frame batch: n_frames (1..4) frames of one resolution, each with its own camera, in one
+ * pipeline pass (the per-level launch and latency floor is paid once per batch; the frame
+ * index sits above every queue-key bit, so no wave mixes frames).  d_rgb holds n_frames
+ * consecutive band buffers of rt_band_rows_per_rank(y_res, band_rows, world) x x_res x 3
+ * floats; each equals rt_render_bands_async of that frame's camera bit for bit.  No
+ * reference counterpart: a throughput form of render() (src/render.rs:31) over frames. */
+rt_status rt_render_bands_batch_async(const rt_scene* scene, const rt_camera* cams, uint32_t n_frames,
+                                      uint32_t depth, uint32_t band_rows, uint32_t rank, uint32_t world,
+                                      float* d_rgb, uint64_t* d_counters, void* stream);
+
 /* Stochastic supersampling (BASELINE config 5; the reference has no equivalent, SURVEY.md
  * §7 step 6).  Sample k (0 <= k < spp) of pixel (u, v) is Camera::get_ray's ray through
  * (u + jx, v + jy) -- x = x_min + ((float)u + jx) * x_delta, y = y_max - ((float)v + jy) *

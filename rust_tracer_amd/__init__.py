@@ -319,6 +319,15 @@ class DeviceScene:
                                                 C.c_void_p(stream_ptr)), "rt_render_bands_spp_async")
 
 
+    def render_bands_batch_async(self, cams, depth, band_rows, rank, world, d_rgb_ptr, d_counters_ptr, stream_ptr):
+        """rt_render_bands_batch_async: len(cams) frames (<= 4, one resolution) in one pipeline
+        pass into len(cams) consecutive band buffers."""
+        arr = (abi.rt_camera * len(cams))(*cams)
+        check(self._L.rt_render_bands_batch_async(self.h, arr, len(cams), depth, band_rows, rank, world,
+                                                  C.c_void_p(d_rgb_ptr), C.c_void_p(d_counters_ptr),
+                                                  C.c_void_p(stream_ptr)), "rt_render_bands_batch_async")
+
+
 class DeviceForest:
     """A RayForest kept on the device (rt_forest_*): built once, shaded any number of times."""
 

@@ -124,6 +124,8 @@ def lib():
                                 P(C.c_float), P(C.c_uint8)]
     L.rt_render_bands_spp_async.argtypes = [vp, P(rt_camera), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                             C.c_uint32, C.c_uint32, vp, vp, vp]
+    L.rt_render_bands_batch_async.argtypes = [vp, P(rt_camera), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                              C.c_uint32, vp, vp, vp]
     L.rt_band_rows_per_rank.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
     L.rt_band_rows_per_rank.restype = C.c_uint32
     L.rt_unpermute_bands_async.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,

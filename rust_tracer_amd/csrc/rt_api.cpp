@@ -1437,7 +1437,8 @@ static rt_status launch_bands(rt_scene* s, const rt_camera* cam, uint32_t depth,
 static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
                                uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
                                hipStream_t stream, WaveParams* forest_params, uint32_t* forest_levels,
-                               uint32_t spp = 1, uint32_t sample = 0, uint32_t seed = 0);
+                               uint32_t spp = 1, uint32_t sample = 0, uint32_t seed = 0, uint32_t frames = 1,
+                               const rt_camera* cams = nullptr);
 
 // spp samples: one pipeline run per sample, in sample order (the level-0 combine adds
 // sample k's colour to the running sum of samples 0..k-1 and the last one divides)
@@ -1455,7 +1456,9 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
 static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
                                uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
                                hipStream_t stream, WaveParams* forest_params, uint32_t* forest_levels,
-                               uint32_t spp, uint32_t sample, uint32_t seed) {
+                               uint32_t spp, uint32_t sample, uint32_t seed, uint32_t frames,
+                               const rt_camera* cams) {
+    if (frames == 0 || frames > RT_MAX_FRAMES || (frames > 1 && (!cams || forest_params))) return RT_ERR_INVALID_ARG;
     WaveParams p;
     std::memset(&p, 0, sizeof(p));
     p.spp = spp;
@@ -1478,6 +1481,25 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     p.rows_local = rt_band_rows_per_rank(cam->y_res, band_rows, world);
     p.tiles_x = (cam->x_res + 7) / 8;
     uint64_t total = (uint64_t)p.tiles_x * ((p.rows_local + 7) / 8) * 64u;
+    p.frames = frames;
+    p.frame_items = (uint32_t)total;
+    p.frame_floats = (size_t)p.rows_local * p.width * 3u;
+    if (frames > 1) {
+        if ((uint64_t)cam->x_res * cam->y_res >= (1ull << RT_FRAME_SHIFT)) return RT_ERR_UNSUPPORTED;
+        for (uint32_t f = 0; f < frames; f++) {
+            if (cams[f].x_res != cam->x_res || cams[f].y_res != cam->y_res) return RT_ERR_INVALID_ARG;
+            FrameCam& c = p.cams[f];
+            c.ox = cams[f].origin[0];
+            c.oy = cams[f].origin[1];
+            c.oz = cams[f].origin[2];
+            c.x_min = cams[f].x_min;
+            c.y_max = cams[f].y_max;
+            c.x_delta = (cams[f].x_max - cams[f].x_min) / (float)cams[f].x_res;  // render.rs:179-180
+            c.y_delta = (cams[f].y_max - cams[f].y_min) / (float)cams[f].y_res;
+            c.pad = 0.f;
+        }
+    }
+    total *= frames;
     if (total >= (1ull << 30)) return RT_ERR_UNSUPPORTED;
     p.total_items = (uint32_t)total;
     // node / task pool: level 0 plus room for ~11 secondary nodes per pixel on average
@@ -1567,6 +1589,15 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         if (p.shadow_fine && p.shadow_fine + lbits > 32u) p.shadow_fine = 0u;
     }
     if (p.shadow_fine) shadow_bits = p.shadow_fine + lbits;
+    if (frames > 1) {  // the frame index above every key bit: a wave never mixes frames
+        uint32_t fbits = 0;
+        while ((1u << fbits) < frames) fbits++;
+        p.task_frame_shift = task_bits;
+        p.shadow_frame_shift = shadow_bits;
+        task_bits += fbits;
+        shadow_bits += fbits;
+        if (shadow_bits > 32u) return RT_ERR_UNSUPPORTED;
+    }
     if (sort_tasks && w.sort_capacity < w.capacity) {
         for (uint32_t** b : {&w.task_keys, &w.perm}) {
             if (*b) (void)hipFree(*b);
@@ -1689,6 +1720,26 @@ rt_status rt_render_bands_spp_async(const rt_scene* scene, const rt_camera* cam,
     HIP_TRY(hipSetDevice(s->device));
     return launch_bands(s, cam, depth, spp, seed, band_rows, rank, world, d_rgb,
                         reinterpret_cast<unsigned long long*>(d_counters), (hipStream_t)stream);
+}
+
+rt_status rt_render_bands_batch_async(const rt_scene* scene, const rt_camera* cams, uint32_t n_frames,
+                                      uint32_t depth, uint32_t band_rows, uint32_t rank, uint32_t world,
+                                      float* d_rgb, uint64_t* d_counters, void* stream) {
+    rt_scene* s = const_cast<rt_scene*>(scene);
+    if (!s || !cams || n_frames == 0 || n_frames > RT_MAX_FRAMES) return RT_ERR_INVALID_ARG;
+    if (n_frames == 1)
+        return rt_render_bands_spp_async(scene, cams, depth, 1, 0, band_rows, rank, world, d_rgb, d_counters, stream);
+    const rt_camera* cam = cams;
+    if (!d_rgb || band_rows == 0 || world == 0 || rank >= world) return RT_ERR_INVALID_ARG;
+    if (cam->x_res == 0 || cam->y_res == 0) return RT_ERR_INVALID_ARG;
+    if (depth > RT_MAX_DEPTH) return RT_ERR_UNSUPPORTED;
+    if (use_megakernel()) return RT_ERR_UNSUPPORTED;
+    HIP_TRY(hipSetDevice(s->device));
+    rt_status st = ensure_ws(s, 0, 0);
+    if (st != RT_OK) return st;
+    return wave_pipeline(s, s->ws, cam, depth, band_rows, rank, world, d_rgb,
+                         reinterpret_cast<unsigned long long*>(d_counters), (hipStream_t)stream, nullptr, nullptr, 1,
+                         0, 0, n_frames, cams);
 }
 
 rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* cam, uint32_t depth,

@@ -174,10 +174,23 @@ struct NodeRec {
 // nodes to allocate for `cap` slots (whole 64-node blocks)
 inline size_t node_alloc_count(uint32_t cap) { return ((size_t)cap + 63u) & ~(size_t)63u; }
 
+// frame batches (rt_render_bands_batch_async): up to RT_MAX_FRAMES frames of one
+// resolution in one pipeline pass; a task carries its frame in Task.pixel's top bits
+#define RT_MAX_FRAMES 4
+#define RT_FRAME_SHIFT 28
+struct FrameCam {
+    float ox, oy, oz, x_min, y_max, x_delta, y_delta, pad;
+};
 struct WaveParams {
     DevScene S;
     float cam_ox, cam_oy, cam_oz;
     float x_min, y_max, x_delta, y_delta;
+    uint32_t frames;                   // frames in this pass (1: rt_render_bands_async)
+    uint32_t frame_items;              // level-0 items per frame (total_items / frames)
+    uint32_t task_frame_shift;         // task key |= frame << this (frames > 1)
+    uint32_t shadow_frame_shift;       // shadow key |= frame << this (frames > 1)
+    size_t frame_floats;               // output floats per frame (rows_local x width x 3)
+    FrameCam cams[RT_MAX_FRAMES];      // frames > 1: each frame's camera (render.rs:155-186)
     uint32_t width, height, depth;
     uint32_t band_rows, rank, world, rows_local;
     uint32_t tiles_x, total_items;     // level-0 tasks (8x8 tiles over width x rows_local)

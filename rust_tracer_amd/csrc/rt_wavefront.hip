@@ -362,7 +362,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         const uint32_t n = off + t;
         if (active) {
             if (level == 0) {
-                PixelRef px = pixel_of(P, t);
+                const uint32_t fr = P.frames > 1 ? t / P.frame_items : 0u;
+                PixelRef px = pixel_of(P, t - fr * P.frame_items);
                 if (!px.valid) {
                     node_flags(P.nodes, n, NODE_NONE);
                     active = false;
@@ -378,11 +379,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                             fu = fu + spp_jitter(P.seed, pix, P.sample, 0u);
                             fv = fv + spp_jitter(P.seed, pix, P.sample, 1u);
                         }
-                        float x = P.x_min + fu * P.x_delta;
-                        float y = P.y_max - fv * P.y_delta;
-                        V3 cam = v3(P.cam_ox, P.cam_oy, P.cam_oz);
-                        ro = cam;
-                        rd = norm(sub(v3(x, y, 0.f), cam));
+                        if (P.frames > 1) {
+                            const FrameCam& C = P.cams[fr];
+                            float x = C.x_min + fu * C.x_delta;
+                            float y = C.y_max - fv * C.y_delta;
+                            V3 cam = v3(C.ox, C.oy, C.oz);
+                            ro = cam;
+                            rd = norm(sub(v3(x, y, 0.f), cam));
+                        } else {
+                            float x = P.x_min + fu * P.x_delta;
+                            float y = P.y_max - fv * P.y_delta;
+                            V3 cam = v3(P.cam_ox, P.cam_oy, P.cam_oz);
+                            ro = cam;
+                            rd = norm(sub(v3(x, y, 0.f), cam));
+                        }
+                        pix |= fr << RT_FRAME_SHIFT;  // children carry the frame
                     }
                 }
             } else {
@@ -507,7 +518,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
             if (slot < P.capacity) {
                 Task T = {rro.x, rro.y, rro.z, rrd.x, rrd.y, rrd.z, (n << 1) | 0u, pix};
                 P.tasks[slot] = T;
-                if (P.task_keys) P.task_keys[slot] = task_key(P, rro, rrd);
+                if (P.task_keys)
+                    P.task_keys[slot] = task_key(P, rro, rrd) | ((pix >> RT_FRAME_SHIFT) << P.task_frame_shift);
             } else {
                 atomicOr(P.overflow, 1u);
             }
@@ -518,7 +530,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
             if (slot < P.capacity) {
                 Task T = {tro.x, tro.y, tro.z, trd.x, trd.y, trd.z, (n << 1) | 1u, pix};
                 P.tasks[slot] = T;
-                if (P.task_keys) P.task_keys[slot] = task_key(P, tro, trd);
+                if (P.task_keys)
+                    P.task_keys[slot] = task_key(P, tro, trd) | ((pix >> RT_FRAME_SHIFT) << P.task_frame_shift);
             } else {
                 atomicOr(P.overflow, 1u);
             }
@@ -595,8 +608,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                     if (slot < P.shadow_capacity) {
                         P.shadow[slot] = (n << 5) | (uint32_t)li;
                         if (P.shadow_keys)
-                            P.shadow_keys[slot] = P.shadow_fine ? (((uint32_t)li << P.shadow_fine) | mort)
-                                                                  : ((uint32_t)li << P.light_shift) | (mort >> (15u - P.light_shift));
+                            P.shadow_keys[slot] = (P.shadow_fine ? (((uint32_t)li << P.shadow_fine) | mort)
+                                                                   : ((uint32_t)li << P.light_shift) | (mort >> (15u - P.light_shift)))
+                                                  | ((pix >> RT_FRAME_SHIFT) << P.shadow_frame_shift);
                     } else
                         atomicOr(P.overflow, 2u);
                 }
@@ -677,10 +691,13 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
         const uint32_t n = off + t;
         const float4 c0 = *node_c(P.nodes, n, NC_AMB);
         const uint32_t flags = __float_as_uint(c0.w);
+        // frame batches: level-0 node t belongs to frame t / frame_items
+        const uint32_t fr = (level == 0 && P.frames > 1) ? t / P.frame_items : 0u;
+        float* const out = P.out + (size_t)fr * P.frame_floats;
         if (flags & NODE_NONE) {  // padding of the band buffer: defined as 0
-            PixelRef px = pixel_of(P, t);
+            PixelRef px = pixel_of(P, t - fr * P.frame_items);
             if (level == 0 && px.u < P.width && px.lr < P.rows_local) {
-                float* o = P.out + ((size_t)px.lr * P.width + px.u) * 3u;
+                float* o = out + ((size_t)px.lr * P.width + px.u) * 3u;
                 o[0] = 0.f;
                 o[1] = 0.f;
                 o[2] = 0.f;
@@ -728,8 +745,8 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
             continue;  // a missed child reports BLACK: the parent's slot already holds 0
         }
         if (level == 0) {
-            PixelRef px = pixel_of(P, t);
-            float* o = P.out + ((size_t)px.lr * P.width + px.u) * 3u;
+            PixelRef px = pixel_of(P, t - fr * P.frame_items);
+            float* o = out + ((size_t)px.lr * P.width + px.u) * 3u;
             if (P.spp > 1) {  // the f32 sum of the samples in sample order, then / spp
                 if (P.sample > 0) c = v3(o[0] + c.x, o[1] + c.y, o[2] + c.z);
                 if (P.sample + 1 == P.spp) {

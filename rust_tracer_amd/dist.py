@@ -38,7 +38,7 @@ class FrameTiler:
     """Renders this rank's share of a frame and gathers the frame on rank 0."""
 
     def __init__(self, scene: DeviceScene, width, height, depth, band_rows=8, rank=0, world=1,
-                 device=None, spp=1, seed=0):
+                 device=None, spp=1, seed=0, batch=1):
         self.scene = scene
         self.spp, self.seed = spp, seed
         self.w, self.h, self.depth = width, height, depth
@@ -46,43 +46,61 @@ class FrameTiler:
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.rpr = band_rows_per_rank(height, band_rows, world)
         assert self.rpr == band_rows_per_rank_py(height, band_rows, world)
+        # frames per pipeline pass (rt_render_bands_batch_async; 1 = rt_render_bands_async)
+        self.batch = max(1, min(int(batch), 4))
+        if spp > 1:
+            self.batch = 1
         self.cam = abi.camera(width, height)
-        self.local = torch.zeros((self.rpr, width, 3), dtype=torch.float32, device=self.device)
+        self.locals = torch.zeros((self.batch, self.rpr, width, 3), dtype=torch.float32, device=self.device)
+        self.local = self.locals[0]
         self.counters = torch.zeros(3, dtype=torch.int64, device=self.device)
         self.gathered = None
-        self.frame = None
+        self.frames = None          # [batch, H, W, 3]: the last pass's assembled frames (rank 0)
         if rank == 0 and world > 1:
             self.gathered = torch.zeros((world, self.rpr, width, 3), dtype=torch.float32,
                                         device=self.device)
-            self.frame = torch.zeros((height, width, 3), dtype=torch.float32, device=self.device)
+            self.frames = torch.zeros((self.batch, height, width, 3), dtype=torch.float32, device=self.device)
         elif world == 1:
-            self.frame = self.local[:height]
+            self.frames = self.locals[:, :height]
+        self.frame = self.frames[0] if self.frames is not None else None
+        self.last = 1               # frames in the last pass
 
-    def render_local(self):
+    def render_local(self, n=1):
+        """Render n (<= batch) frames of this rank's bands on the current stream."""
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        self.scene.render_bands_async(self.cam, self.depth, self.band_rows, self.rank, self.world,
-                                      self.local.data_ptr(), self.counters.data_ptr(), stream,
-                                      spp=self.spp, seed=self.seed)
+        self.last = n
+        if n == 1:
+            self.scene.render_bands_async(self.cam, self.depth, self.band_rows, self.rank, self.world,
+                                          self.local.data_ptr(), self.counters.data_ptr(), stream,
+                                          spp=self.spp, seed=self.seed)
+        else:
+            assert n <= self.batch
+            self.scene.render_bands_batch_async([self.cam] * n, self.depth, self.band_rows, self.rank,
+                                                self.world, self.locals.data_ptr(), self.counters.data_ptr(),
+                                                stream)
 
     def assemble(self):
-        """Gather every rank's bands on rank 0 and restore row order (no-op at world 1)."""
+        """Gather every rank's bands of the last pass's frames on rank 0 and restore row
+        order (no-op at world 1)."""
         if self.world == 1:
             return self.frame
-        if dist.get_backend() == "gloo":
-            # CPU rehearsal of the exchange (several ranks sharing one GPU); RCCL runs the
-            # same gather directly on device buffers
-            host = self.local.cpu()
-            glist = [torch.empty_like(host) for _ in range(self.world)] if self.rank == 0 else None
-            dist.gather(host, gather_list=glist, dst=0)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        for b in range(self.last):
+            local = self.locals[b]
+            if dist.get_backend() == "gloo":
+                # CPU rehearsal of the exchange (several ranks sharing one GPU); RCCL runs
+                # the same gather directly on device buffers
+                host = local.cpu()
+                glist = [torch.empty_like(host) for _ in range(self.world)] if self.rank == 0 else None
+                dist.gather(host, gather_list=glist, dst=0)
+                if self.rank == 0:
+                    self.gathered.copy_(torch.stack(glist))
+            else:
+                glist = list(self.gathered.unbind(0)) if self.rank == 0 else None
+                dist.gather(local, gather_list=glist, dst=0)
             if self.rank == 0:
-                self.gathered.copy_(torch.stack(glist))
-        else:
-            glist = list(self.gathered.unbind(0)) if self.rank == 0 else None
-            dist.gather(self.local, gather_list=glist, dst=0)
-        if self.rank == 0:
-            stream = torch.cuda.current_stream(self.device).cuda_stream
-            unpermute_bands_async(self.gathered.data_ptr(), self.w, self.h, self.band_rows,
-                                  self.world, self.frame.data_ptr(), stream)
+                unpermute_bands_async(self.gathered.data_ptr(), self.w, self.h, self.band_rows,
+                                      self.world, self.frames[b].data_ptr(), stream)
         return self.frame
 
     def step(self):
@@ -101,13 +119,14 @@ class FramePipeline:
     band buffer).  Every frame is rendered and gathered in full."""
 
     def __init__(self, scene: DeviceScene, desc, width, height, depth, band_rows=8, rank=0, world=1,
-                 device=None, spp=1, seed=0, inflight=4):
+                 device=None, spp=1, seed=0, inflight=4, batch=1):
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.inflight = max(1, int(inflight))
         self.world = world
         self.tilers = [FrameTiler(scene if i == 0 else DeviceScene(desc, device=self.device.index), width, height,
-                                  depth, band_rows, rank, world, self.device, spp=spp, seed=seed)
+                                  depth, band_rows, rank, world, self.device, spp=spp, seed=seed, batch=batch)
                        for i in range(self.inflight)]
+        self.batch = self.tilers[0].batch
         self.streams = [torch.cuda.Stream(device=self.device) for _ in range(self.inflight)]
         self._reuse = [None] * self.inflight
 
@@ -121,22 +140,29 @@ class FramePipeline:
             t.counters.zero_()
 
     def run(self, n, latency_events=None):
-        """Enqueue n frames (asynchronous); the caller's stream waits for all of them.
-        latency_events[k] = (start, end) events recorded around frame k's render."""
+        """Enqueue n frames (asynchronous) in passes of up to `batch` frames, pass k on slot
+        k % inflight; the caller's stream waits for all of them.  latency_events: a list
+        that receives one (start, end) event pair per pass."""
         main = torch.cuda.current_stream(self.device)
         for s in self.streams:
             s.wait_stream(main)
-        for k in range(n):
+        k = 0
+        while n > 0:
+            b = min(self.batch, n)
+            n -= b
             i = k % self.inflight
+            k += 1
             st = self.streams[i]
             with torch.cuda.stream(st):
                 if self._reuse[i] is not None:
                     st.wait_event(self._reuse[i])
                 if latency_events is not None:
-                    latency_events[k][0].record(st)
-                self.tilers[i].render_local()
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ev[0].record(st)
+                self.tilers[i].render_local(b)
                 if latency_events is not None:
-                    latency_events[k][1].record(st)
+                    ev[1].record(st)
+                    latency_events.append(ev)
             if self.world > 1:
                 main.wait_stream(st)
                 self.tilers[i].assemble()
@@ -146,8 +172,8 @@ class FramePipeline:
             main.wait_stream(s)
 
     def frames(self):
-        """each slot's last assembled frame (rank 0; None elsewhere)"""
-        return [t.frame for t in self.tilers]
+        """every frame of each slot's last pass, assembled (rank 0; [] elsewhere)"""
+        return [t.frames[b] for t in self.tilers if t.frames is not None for b in range(t.last)]
 
     def close(self):
         for t in self.tilers[1:]:

@@ -90,6 +90,7 @@ def main(tag):
             d["Duration_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             w.writerow(d)
     bench = json.load(open(os.path.join(src, "bench.json")))
+    fpp = int(bench["config"].get("frames_per_pass", 1))  # frames per pipeline pass (wave_init)
     pmc = {}
     pmc_frames = {}
     for p in ("pmc_sq", "pmc_fetch", "pmc_write"):
@@ -103,12 +104,18 @@ def main(tag):
         agg = defaultdict(float)
         for r in kept:
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
-        # frames in this pass (bench.py --steps 2 --warmup 0 --count-frame 0: 2 default frames)
+        # frames in this pass (bench.py --steps 4 --warmup 0 --inflight 1 --count-frame 0:
+        # full passes of frames_per_pass frames, one wave_init each)
         inits = {r["Dispatch_Id"] for r in kept if "wave_init_kernel" in r["Kernel_Name"]}
         for k in agg:
-            pmc_frames[k] = max(1, len(inits))
+            pmc_frames[k] = max(1, len(inits)) * fpp
         pmc.update({k: v / pmc_frames[k] for k, v in agg.items()})
     frames, fam_ms, timed_ms, n_timed, span_ms = trace_frames(keep)
+    # passes -> frames (the instrumented counted frame is a one-frame pass)
+    fam_ms = {f: (v if f.startswith("instrumented") else v / fpp) for f, v in fam_ms.items()}
+    timed_ms /= fpp
+    span_ms /= fpp
+    n_timed *= fpp
     fetch_b = pmc.get("FETCH_SIZE", 0.0) * 1024
     write_b = pmc.get("WRITE_SIZE", 0.0) * 1024
     traffic = {
@@ -139,7 +146,8 @@ def main(tag):
     ] + [f"| {k} | {v:.3f} |" for k, v in sorted(fam_ms.items(), key=lambda x: -x[1])] + [
         "",
         f"Sum of the default kernels per frame: {timed_ms:.3f} ms (kernel-busy time; with "
-        f"{bench['config'].get('frames_in_flight', 1)} frames in flight the frames' kernels overlap).",
+        f"{bench['config'].get('frames_in_flight', 1)} frames in flight, {fpp} per pass, the frames' kernels "
+        f"overlap).",
         "",
         f"Timed frames ({n_timed}) in the trace run: wall span per frame {span_ms:.3f} ms "
         f"(bench HIP events over the timed region: {frame_ms} ms per frame; the tracer's per-dispatch "
