@@ -1484,8 +1484,10 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     p.frames = frames;
     p.frame_items = (uint32_t)total;
     p.frame_floats = (size_t)p.rows_local * p.width * 3u;
-    if (frames > 1) {
-        if ((uint64_t)cam->x_res * cam->y_res >= (1ull << RT_FRAME_SHIFT)) return RT_ERR_UNSUPPORTED;
+    if (frames > 1 && (uint64_t)cam->x_res * cam->y_res >= (1ull << RT_FRAME_SHIFT)) return RT_ERR_UNSUPPORTED;
+    {
+        // level 0 reads every frame's camera from cams[] (frames == 1: cams[0] = cam)
+        if (frames == 1) cams = cam;
         for (uint32_t f = 0; f < frames; f++) {
             if (cams[f].x_res != cam->x_res || cams[f].y_res != cam->y_res) return RT_ERR_INVALID_ARG;
             FrameCam& c = p.cams[f];

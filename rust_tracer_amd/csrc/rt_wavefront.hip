@@ -379,20 +379,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                             fu = fu + spp_jitter(P.seed, pix, P.sample, 0u);
                             fv = fv + spp_jitter(P.seed, pix, P.sample, 1u);
                         }
-                        if (P.frames > 1) {
-                            const FrameCam& C = P.cams[fr];
-                            float x = C.x_min + fu * C.x_delta;
-                            float y = C.y_max - fv * C.y_delta;
-                            V3 cam = v3(C.ox, C.oy, C.oz);
-                            ro = cam;
-                            rd = norm(sub(v3(x, y, 0.f), cam));
-                        } else {
-                            float x = P.x_min + fu * P.x_delta;
-                            float y = P.y_max - fv * P.y_delta;
-                            V3 cam = v3(P.cam_ox, P.cam_oy, P.cam_oz);
-                            ro = cam;
-                            rd = norm(sub(v3(x, y, 0.f), cam));
-                        }
+                        // the frame's camera (cams[0] = the camera when frames == 1); a
+                        // wave's 64 items are one tile of one frame: fr is wave-uniform
+                        const FrameCam& C = P.cams[__builtin_amdgcn_readfirstlane(fr)];
+                        float x = C.x_min + fu * C.x_delta;
+                        float y = C.y_max - fv * C.y_delta;
+                        V3 cam = v3(C.ox, C.oy, C.oz);
+                        ro = cam;
+                        rd = norm(sub(v3(x, y, 0.f), cam));
                         pix |= fr << RT_FRAME_SHIFT;  // children carry the frame
                     }
                 }
