@@ -12,7 +12,7 @@ The frame is fixed as N grows ("scaling": "strong").  Consecutive frames are ren
 --inflight F frames in flight: F scene handles (one workspace each) on F HIP streams, so
 the latency-bound tails of one frame's trace levels overlap the next frames' work, and
 each pass renders --batch B frames in one pipeline (rt_render_bands_batch_async: the frame
-index sits above every queue-key bit, so no wave mixes frames).  Every frame is rendered
+index sits above every queue-key bit, so each frame's rays stay contiguous in the queues).  Every frame is rendered
 and (N > 1) gathered in full; `pass_latency_ms` reports one pass's own duration beside
 the throughput.
 
@@ -68,12 +68,15 @@ def parse():
                         "queues per process); 1 = one at a time")
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU oracle timing")
     p.add_argument("--cpu-threads", type=int, default=None,
-                   help="threads of the multi-core CPU baseline (default: OMP_NUM_THREADS, else <= 16)")
+                   help="threads of the multi-core CPU baseline (default: every core in the affinity mask)")
     p.add_argument("--cpu-rows-step", type=int, default=None,
                    help="CPU baseline renders every k-th row of the frame")
     p.add_argument("--backend", default="nccl", help="nccl (RCCL) or gloo (CPU rehearsal)")
     p.add_argument("--check", type=int, default=0,
                    help="rank 0 compares the assembled frame with a single-launch render")
+    p.add_argument("--seam-stats", type=int, default=1,
+                   help="N = 1: also time one frame at a time, rt_render with its host copy, the scene "
+                        "build, and the depth-9 reading of 'primary+8 bounces' (untimed extras)")
     p.add_argument("--count-frame", type=int, default=1,
                    help="0: skip the instrumented (counting) frame; roofline test counts are then null "
                         "(used by the rocprofv3 counter passes so they see only the default kernels)")
@@ -120,22 +123,22 @@ def cpu_baseline(args, desc):
                   f"host: {os.cpu_count()} logical CPUs",
         "seconds": round(dt, 2),
         "multicore": cpu_baseline_mt(args, o),
+        "per_gpu_share": cpu_baseline_mt(args, o, threads=min(16, cpu_threads(args)),
+                                         label="the box's CPU share per GPU"),
     }
 
 
 def cpu_threads(args):
+    """Every host core this process may run on (OpenMP over all host cores)."""
     if args.cpu_threads:
         return args.cpu_threads
-    env = os.environ.get("OMP_NUM_THREADS")
-    if env and env.isdigit() and int(env) > 0:
-        return int(env)
-    return min(16, len(os.sched_getaffinity(0)))
+    return len(os.sched_getaffinity(0))
 
 
-def cpu_baseline_mt(args, o):
+def cpu_baseline_mt(args, o, threads=None, label="every host core this process may use (sched_getaffinity)"):
     """The same oracle, rows dealt over T host threads (pixel-parallel over
     the host cores), on every k/T-th row: about the single-thread run's wall time."""
-    threads = cpu_threads(args)
+    threads = threads or cpu_threads(args)
     if threads <= 1:
         return None
     step = max(1, args.cpu_rows_step // threads)
@@ -149,9 +152,62 @@ def cpu_baseline_mt(args, o):
         "unit": "Mpixels/s",
         "cores": threads,
         "sample": f"{len(rows)} of {args.height} rows (every {step}th), {cnt['pixels'] // args.spp} pixels x "
-                  f"{args.spp} spp, {dt:.1f} s, {threads} threads (the box's CPU share per GPU)",
+                  f"{args.spp} spp, {dt:.1f} s, {threads} threads ({label})",
         "seconds": round(dt, 2),
     }
+
+
+def seam_stats(args, scene, pipe, tiler, dev):
+    """Numbers of the drop-in seam beside the throughput headline (untimed extras, N = 1):
+    - one frame at a time: the pipeline with nothing overlapping it (HIP events);
+    - rt_render: the reference's render() seam (src/render.rs:31) with its device-to-host
+      copy of the float frame, wall clock per call (main.rs:250-253 times render only);
+    - the scene build: rt_scene_create (host hierarchy, light buffers, grazing masks, upload)
+      and rt_scene_clone (a second handle, device-to-device);
+    - 'primary+8 bounces' read literally: depth 9 (reference depth 8 = primary + 7 levels,
+      render.rs:43-45), frames in flight as the headline."""
+    out = {}
+    main = torch.cuda.current_stream(dev)
+    tiler.step()
+    torch.cuda.synchronize()
+    n1 = 5
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(main)
+    for _ in range(n1):
+        tiler.step()
+    e1.record(main)
+    torch.cuda.synchronize()
+    out["one_frame_at_a_time_ms"] = round(e0.elapsed_time(e1) / n1, 4)
+    out["one_frame_at_a_time_mpixels_per_s"] = round(args.width * args.height / (out["one_frame_at_a_time_ms"] / 1e3) / 1e6, 3)
+    if args.spp == 1:
+        scene.render(args.width, args.height, args.depth)  # sizes rt_render's frame buffers
+        walls = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            scene.render(args.width, args.height, args.depth)
+            walls.append((time.perf_counter() - t0) * 1e3)
+        out["rt_render_with_host_copy_ms"] = round(min(walls), 3)
+        out["rt_render_with_host_copy_mpixels_per_s"] = round(args.width * args.height / (min(walls) / 1e3) / 1e6, 3)
+    t0 = time.perf_counter()
+    c = scene.clone(dev.index)
+    out["scene_clone_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
+    c.close()
+    if args.spp == 1 and args.depth == 8:
+        for t in pipe.tilers:
+            t.depth = 9
+        pipe.run(pipe.inflight * pipe.batch)
+        torch.cuda.synchronize()
+        k = 10
+        e0.record(main)
+        pipe.run(k)
+        e1.record(main)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / k
+        for t in pipe.tilers:
+            t.depth = args.depth
+        out["depth9_ms_per_frame"] = round(ms, 4)
+        out["depth9_mpixels_per_s"] = round(args.width * args.height / (ms / 1e3) / 1e6, 3)
+    return out
 
 
 def load_traffic(path, workload):
@@ -185,7 +241,10 @@ def main():
     from rust_tracer_amd.dist import FramePipeline
 
     desc = SceneDesc.synth_config(args.config)
-    scene = DeviceScene(desc, device=dev.index)
+    torch.cuda.synchronize()
+    t_sc = time.perf_counter()
+    scene = DeviceScene(desc, device=dev.index)   # host build (hierarchy, light buffers) + upload
+    scene_create_ms = (time.perf_counter() - t_sc) * 1e3
     inflight = max(1, args.inflight or 4)
     if args.batch is None:
         # N > 1 shares are latency-bound: 4 frames per pass (bounded workspace: <= 4 x 1080p
@@ -265,7 +324,12 @@ def main():
             ref, _, _, _ = scene.render(args.width, args.height, args.depth, device=dev.index, spp=args.spp,
                                         seed=args.seed)
             frame_check = all(bool(np.array_equal(f.view(np.uint32), ref.view(np.uint32))) for f in frames)
-    elapsed, kernel_ms_max = stats.tolist()
+    seam = seam_stats(args, scene, pipe, tiler, dev) if (args.seam_stats and world == 1) else None
+    for t in tilers:  # every stream-ordered pass of the run, incl. the timed ones, was complete
+        t.scene.sync_status()
+    if seam is not None:
+        seam["scene_create_ms"] = round(scene_create_ms, 2)
+        elapsed, kernel_ms_max = stats.tolist()
     node_rays, shadow_rays, pixels = cnt.tolist()
 
     if rank == 0:
@@ -339,6 +403,8 @@ def main():
         }
         if frame_check is not None:
             out["frame_check"] = frame_check
+        if seam is not None:
+            out["seam"] = seam
         if world == 1 and args.cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, desc)
         print(json.dumps(out), flush=True)

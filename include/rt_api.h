@@ -44,7 +44,10 @@ enum {
     RT_ERR_NO_DEVICE = 4,        /* no HIP device / HIP runtime failure at init */
     RT_ERR_HIP = 5,              /* a HIP runtime call failed */
     RT_ERR_OUT_OF_MEMORY = 6,
-    RT_ERR_BAD_MATERIAL = 7      /* material index out of range */
+    RT_ERR_BAD_MATERIAL = 7,     /* material index out of range */
+    RT_ERR_CAPACITY = 8          /* a ray queue overflowed its pool: the frame is incomplete
+                                    (render.rs:40-103 traces every ray; this build never
+                                    returns a truncated frame as RT_OK) */
 };
 
 /* Largest `depth` the device path accepts (the DFS continuation stack has
@@ -155,6 +158,28 @@ typedef struct rt_scene rt_scene;
 rt_status rt_scene_create(const rt_scene_desc* desc, int32_t device, rt_scene** out);
 rt_status rt_scene_destroy(rt_scene* scene);
 
+/* A second handle of the same scene on `device` (-1 = current), copied device-to-device (no
+ * host rebuild): its own workspace and stream, so two handles can render concurrently
+ * (frames in flight) or on two GPUs. */
+rt_status rt_scene_clone(const rt_scene* src, int32_t device, rt_scene** out);
+
+/* Multi-GPU render behind the same seam.  One host thread drives
+ * every listed device: the scene is built once and uploaded to each device; rt_render /
+ * rt_render_spp on the returned handle deal the frame's rows in block-cyclic bands of 8
+ * over the devices (band b -> devices[b % n]), render them concurrently, gather the bands
+ * on devices[0] with RCCL (ncclGather over xGMI, communicators from ncclCommInitAll) and
+ * un-permute them there before the copy to the caller's buffers.  The result equals the
+ * one-device rt_render bit for bit (pixels are independent).  n_devices == 1 is
+ * rt_scene_create.  A device listed twice shares that GPU between two band shares, which
+ * then exchange bands by device copies (RCCL puts one rank per device; a test
+ * configuration).  The stream-ordered entry points act on devices[0] only. */
+rt_status rt_scene_create_multi(const rt_scene_desc* desc, const int32_t* devices, uint32_t n_devices,
+                                rt_scene** out);
+/* Devices a scene renders on (1 unless made by rt_scene_create_multi), and whether its band
+ * exchange runs over RCCL. */
+int32_t rt_scene_device_count(const rt_scene* scene);
+int32_t rt_scene_uses_rccl(const rt_scene* scene);
+
 /* render.rs:31-38: fill `rgb` (h*w*3 float, row-major [v][u][c]) with
  * trace_ray(get_ray(u, v), depth) for every pixel.  `rgb8` (optional, may be NULL)
  * receives Color::as_u8 (color.rs:43-46) of every pixel, row-major RGB8. */
@@ -167,6 +192,7 @@ rt_status rt_render(const rt_scene* scene, const rt_camera* camera, uint32_t dep
  * belongs to rank b % world.  This rank's bands are written back to back into
  * `d_rgb` (band-major, rows of x_res*3 floats), rt_band_rows_per_rank() rows in all
  * (the last bands are padded; padded rows are written as 0).
+ * Stream-ordered: a ray-queue overflow is reported later by rt_scene_sync_status.
  * `d_counters` (optional) is a device array of 3 uint64 that the kernel ADDS
  * node_rays, shadow_rays, pixels into. */
 rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* camera,
@@ -176,13 +202,34 @@ rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* camera,
 
 /* Frame batch: n_frames (1..4) frames of one resolution, each with its own camera, in one
  * pipeline pass (the per-level launch and latency floor is paid once per batch; the frame
- * index sits above every queue-key bit, so no wave mixes frames).  d_rgb holds n_frames
+ * index sits above every queue-key bit, so frames stay contiguous in the sorted queues --
+ * an ordering property only; level 0 is frame-uniform per wave).  d_rgb holds n_frames
  * consecutive band buffers of rt_band_rows_per_rank(y_res, band_rows, world) x x_res x 3
  * floats; each equals rt_render_bands_async of that frame's camera bit for bit.  No
  * reference counterpart: a throughput form of render() (src/render.rs:31) over frames. */
 rt_status rt_render_bands_batch_async(const rt_scene* scene, const rt_camera* cams, uint32_t n_frames,
                                       uint32_t depth, uint32_t band_rows, uint32_t rank, uint32_t world,
                                       float* d_rgb, uint64_t* d_counters, void* stream);
+
+/* The general stream-ordered render (every *_async render above is a special case of it):
+ * n_frames (1..4) frames of one resolution, each with its own camera, spp jittered samples
+ * per pixel (spp > 1 needs n_frames == 1), this rank's row bands (as rt_render_bands_async).
+ *  - d_rgb:  n_frames band buffers of f32 RGB (may be NULL when spp == 1 and d_rgb8 is set:
+ *            then only the bytes are written);
+ *  - d_rgb8: optional, n_frames band buffers of RGB8 = Color::as_u8 (color.rs:43-46) of each
+ *            pixel, written by the render's last pass (no separate quantise launch) -- 3 B per
+ *            pixel for the multi-GPU gather instead of 12.
+ * A queue overflow cannot be returned by a stream-ordered call: it is latched in the scene
+ * and reported by rt_scene_sync_status. */
+rt_status rt_render_bands_ex_async(const rt_scene* scene, const rt_camera* cams, uint32_t n_frames, uint32_t depth,
+                                   uint32_t spp, uint32_t seed, uint32_t band_rows, uint32_t rank, uint32_t world,
+                                   float* d_rgb, uint8_t* d_rgb8, uint64_t* d_counters, void* stream);
+
+/* Waits for every stream-ordered render enqueued on `scene` so far and reports whether one of
+ * them overflowed a ray queue: RT_ERR_CAPACITY (that frame is incomplete; the flag is then
+ * cleared) or RT_OK.  rt_render / rt_render_spp never need it: they grow the pool and render
+ * again. */
+rt_status rt_scene_sync_status(rt_scene* scene);
 
 /* Stochastic supersampling (BASELINE config 5; the reference has no equivalent, SURVEY.md
  * §7 step 6).  Sample k (0 <= k < spp) of pixel (u, v) is Camera::get_ray's ray through
@@ -211,6 +258,10 @@ uint32_t rt_band_rows_per_rank(uint32_t y_res, uint32_t band_rows, uint32_t worl
 rt_status rt_unpermute_bands_async(const float* d_gathered, uint32_t x_res, uint32_t y_res,
                                    uint32_t band_rows, uint32_t world, float* d_frame,
                                    void* stream);
+
+/* rt_unpermute_bands_async for RGB8 band buffers (rt_render_bands_ex_async's d_rgb8). */
+rt_status rt_unpermute_bands_u8_async(const uint8_t* d_gathered, uint32_t x_res, uint32_t y_res,
+                                      uint32_t band_rows, uint32_t world, uint8_t* d_frame, void* stream);
 
 /* Saves a row-major RGB8 frame (Color::as_u8 values) as PNG, BMP or PPM, chosen by the
  * file extension (.png default) -- bmp.rs:8-19 / main.rs:71-74 (host code). */

@@ -239,13 +239,42 @@ class SceneDesc:
 
 
 class DeviceScene:
-    """An uploaded scene (rt_scene_create) on one HIP device."""
+    """An uploaded scene (rt_scene_create) on one HIP device, or -- `devices` a list --
+    replicated over several (rt_scene_create_multi: render() then tiles the frame across
+    them and gathers it over RCCL, from this one thread)."""
 
-    def __init__(self, desc, device=-1):
+    def __init__(self, desc, device=-1, devices=None, _handle=None):
         self._L = lib()
         self.h = C.c_void_p()
         self.desc = desc
-        check(self._L.rt_scene_create(desc.ptr(), device, C.byref(self.h)), "rt_scene_create")
+        if _handle is not None:
+            self.h = _handle
+        elif devices is not None:
+            arr = (C.c_int32 * len(devices))(*devices)
+            check(self._L.rt_scene_create_multi(desc.ptr(), arr, len(devices), C.byref(self.h)),
+                  "rt_scene_create_multi")
+        else:
+            check(self._L.rt_scene_create(desc.ptr(), device, C.byref(self.h)), "rt_scene_create")
+
+    def clone(self, device=-1):
+        """rt_scene_clone: another handle of this scene (own workspace and stream), copied on
+        the device without rebuilding it."""
+        h = C.c_void_p()
+        check(self._L.rt_scene_clone(self.h, device, C.byref(h)), "rt_scene_clone")
+        return DeviceScene(self.desc, _handle=h)
+
+    @property
+    def device_count(self):
+        return int(self._L.rt_scene_device_count(self.h))
+
+    @property
+    def uses_rccl(self):
+        return bool(self._L.rt_scene_uses_rccl(self.h))
+
+    def sync_status(self):
+        """rt_scene_sync_status: wait for this scene's stream-ordered renders; raises
+        RtError(RT_ERR_CAPACITY) if one of them overflowed a ray queue (incomplete frame)."""
+        check(self._L.rt_scene_sync_status(self.h), "rt_scene_sync_status")
 
     def close(self):
         if self.h:
@@ -318,6 +347,16 @@ class DeviceScene:
                                                 C.c_void_p(d_rgb_ptr), C.c_void_p(d_counters_ptr),
                                                 C.c_void_p(stream_ptr)), "rt_render_bands_spp_async")
 
+
+    def render_bands_ex_async(self, cams, depth, band_rows, rank, world, d_rgb_ptr, d_rgb8_ptr, d_counters_ptr,
+                              stream_ptr, spp=1, seed=0):
+        """rt_render_bands_ex_async: len(cams) frames; f32 bands (d_rgb_ptr, may be 0 when
+        spp == 1 and d_rgb8_ptr is given) and / or fused RGB8 bands (d_rgb8_ptr)."""
+        arr = (abi.rt_camera * len(cams))(*cams)
+        check(self._L.rt_render_bands_ex_async(self.h, arr, len(cams), depth, spp, seed, band_rows, rank, world,
+                                               C.c_void_p(d_rgb_ptr or None), C.c_void_p(d_rgb8_ptr or None),
+                                               C.c_void_p(d_counters_ptr or None), C.c_void_p(stream_ptr)),
+              "rt_render_bands_ex_async")
 
     def render_bands_batch_async(self, cams, depth, band_rows, rank, world, d_rgb_ptr, d_counters_ptr, stream_ptr):
         """rt_render_bands_batch_async: len(cams) frames (<= 4, one resolution) in one pipeline
@@ -409,6 +448,12 @@ def unpermute_bands_async(d_gathered_ptr, x_res, y_res, band_rows, world, d_fram
     check(lib().rt_unpermute_bands_async(C.c_void_p(d_gathered_ptr), x_res, y_res, band_rows, world,
                                          C.c_void_p(d_frame_ptr), C.c_void_p(stream_ptr)),
           "rt_unpermute_bands_async")
+
+
+def unpermute_bands_u8_async(d_gathered_ptr, x_res, y_res, band_rows, world, d_frame_ptr, stream_ptr):
+    check(lib().rt_unpermute_bands_u8_async(C.c_void_p(d_gathered_ptr), x_res, y_res, band_rows, world,
+                                            C.c_void_p(d_frame_ptr), C.c_void_p(stream_ptr)),
+          "rt_unpermute_bands_u8_async")
 
 
 def quantize_u8_async(d_rgb_ptr, n, d_rgb8_ptr, stream_ptr):

@@ -14,8 +14,9 @@ RT_OK = 0
 STATUS_NAMES = {
     0: "RT_OK", 1: "RT_ERR_INVALID_ARG", 2: "RT_ERR_SINGULAR_MATRIX",
     3: "RT_ERR_UNSUPPORTED", 4: "RT_ERR_NO_DEVICE", 5: "RT_ERR_HIP",
-    6: "RT_ERR_OUT_OF_MEMORY", 7: "RT_ERR_BAD_MATERIAL",
+    6: "RT_ERR_OUT_OF_MEMORY", 7: "RT_ERR_BAD_MATERIAL", 8: "RT_ERR_CAPACITY",
 }
+RT_ERR_CAPACITY = 8
 RT_MAX_DEPTH = 64
 
 RT_TEX_CONST, RT_TEX_CHECKERBOARD = 0, 1
@@ -126,6 +127,16 @@ def lib():
                                             C.c_uint32, C.c_uint32, vp, vp, vp]
     L.rt_render_bands_batch_async.argtypes = [vp, P(rt_camera), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                               C.c_uint32, vp, vp, vp]
+    L.rt_render_bands_ex_async.argtypes = [vp, P(rt_camera), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                           C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp]
+    L.rt_scene_sync_status.argtypes = [vp]
+    L.rt_scene_clone.argtypes = [vp, C.c_int32, P(vp)]
+    L.rt_scene_create_multi.argtypes = [P(rt_scene_desc), P(C.c_int32), C.c_uint32, P(vp)]
+    L.rt_scene_device_count.argtypes = [vp]
+    L.rt_scene_device_count.restype = C.c_int32
+    L.rt_scene_uses_rccl.argtypes = [vp]
+    L.rt_scene_uses_rccl.restype = C.c_int32
+    L.rt_unpermute_bands_u8_async.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp]
     L.rt_band_rows_per_rank.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
     L.rt_band_rows_per_rank.restype = C.c_uint32
     L.rt_unpermute_bands_async.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,

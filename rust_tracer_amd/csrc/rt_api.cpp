@@ -22,6 +22,7 @@
 #include "../../include/rt_api.h"
 #include "rt_bvh.hpp"
 #include "rt_device.hpp"
+#include "rt_internal.hpp"
 
 namespace rtdev {
 hipError_t launch_render(const RenderParams& p, int blocks, hipStream_t stream);
@@ -29,6 +30,8 @@ hipError_t render_occupancy(uint32_t depth, int* blocks_per_cu);
 hipError_t launch_unpermute(const float* in, uint32_t x_res, uint32_t y_res, uint32_t band_rows,
                             uint32_t world, uint32_t rows_per_rank, float* out, hipStream_t stream);
 hipError_t launch_quantize(const float* in, size_t n, uint8_t* out, hipStream_t stream);
+hipError_t launch_unpermute_u8(const uint8_t* in, uint32_t x_res, uint32_t y_res, uint32_t band_rows,
+                               uint32_t world, uint32_t rows_per_rank, uint8_t* out, hipStream_t stream);
 bool rt_cube_table_check(const float* table);
 hipError_t wave_occupancy(int* trace_blocks, int* shadow_blocks, int* combine_blocks);
 hipError_t launch_wave_shadow(const WaveParams& p, int blocks, hipStream_t stream);
@@ -37,7 +40,7 @@ hipError_t launch_wave_init(uint32_t* levels, uint32_t n_words, uint32_t total_i
 hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream);
 hipError_t launch_wave_combine(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream);
 hipError_t launch_forest_shade(const WaveParams& p, uint32_t level, int blocks, float* frame, hipStream_t stream);
-hipError_t launch_forest_mark(const uint32_t* node_key, const uint32_t* node_pixel, const NodeRec* nodes,
+hipError_t launch_forest_mark(const uint32_t* node_key, const uint32_t* node_pixel, const uint32_t* node_flags,
                               uint32_t n_nodes, const uint8_t* key_mask, uint32_t n_keys, uint8_t* mark,
                               uint32_t* sizes, hipStream_t stream);
 hipError_t launch_sort(const uint32_t* levels, int32_t level, uint32_t cap, uint32_t bits, const uint32_t* keys,
@@ -906,16 +909,19 @@ struct Workspace {
     size_t out8_bytes = 0;
     unsigned long long* counters = nullptr;  // [node, shadow, pixels, wave iterations]
     uint32_t* work = nullptr;        // persistent-kernel work counter
-    // level-synchronous pipeline
+    // level-synchronous pipeline: the node arrays of rt_device.hpp
     Task* tasks = nullptr;
-    NodeRec* nodes = nullptr;
-    float4* node_ps = nullptr;       // [capacity] shadow-ray origins
+    uint32_t* node_flags = nullptr;  // [capacity]
+    float4* node_ps = nullptr;       // [capacity] shadow-ray origins, texture u
+    float4* node_n = nullptr;        // [capacity] normals, texture v
+    float4* node_d = nullptr;        // [capacity] ray directions, parents
     uint32_t* node_lit = nullptr;    // [capacity] unshadowed-light bits
+    float4* node_ec = nullptr;       // [2 x capacity] children's colours
     uint32_t capacity = 0;
     uint32_t* shadow = nullptr;      // shadow queue
     uint32_t shadow_capacity = 0;
     uint32_t* levels = nullptr;      // RT_LEVEL_TABLE_WORDS words
-    uint32_t* overflow = nullptr;
+    uint32_t* overflow = nullptr;    // [0] this pass's queue overflows, [1] sticky (rt_scene_sync_status)
     // queue ordering (rt_order.hip)
     uint32_t* task_keys = nullptr;   // [capacity] x2 buffers
     uint32_t* perm = nullptr;
@@ -927,7 +933,7 @@ struct Workspace {
     size_t sort_tmp_words = 0;
     // ray forest only (rt_forest): per-node shade inputs, grown with the pool
     bool forest = false;
-    float4* node_aux = nullptr;
+    float4* node_dc = nullptr;       // [2 x capacity] children's directions
     uint32_t* node_key = nullptr;
     uint32_t* node_pixel = nullptr;
 };
@@ -991,7 +997,14 @@ struct rt_scene {
     Workspace ws;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_last = nullptr;  // recorded after every stream-ordered render (rt_scene_sync_status)
+    bool ev_last_set = false;
+    uint32_t pool_floor = 0;       // node-pool size the next pass grows to (after a reported overflow)
+    rt_multi_state* multi = nullptr;  // rt_scene_create_multi: the other devices' clones (rt_multi.cpp)
 };
+
+rt_multi_state*& rt_scene_multi(rt_scene* s) { return s->multi; }
+int rt_scene_device_of(const rt_scene* s) { return s->device; }
 
 namespace {
 
@@ -1022,6 +1035,16 @@ rt_status select_device(int32_t device, int* resolved) {
     return RT_OK;
 }
 
+// Bits of the light index in a shadow entry ((node << bits) | light, rt_wavefront.hip).
+uint32_t light_bits(const rt_scene* s) {
+    uint32_t b = 1;
+    while ((1u << b) < (uint32_t)s->S.n_lights) b++;
+    return b;
+}
+// Largest node pool: node indices must fit a shadow entry beside the light index (and
+// (node << 1) | slot a parent reference).
+uint64_t pool_cap_limit(const rt_scene* s) { return std::min<uint64_t>(1ull << (32 - light_bits(s)), 1ull << 30); }
+
 int variant_of(uint32_t depth) {
     int maxf = (int)depth - 1;
     return maxf <= 7 ? 0 : (maxf <= 15 ? 1 : 2);
@@ -1050,31 +1073,26 @@ rt_status ensure_ws(rt_scene* s, size_t out_floats, size_t out8_bytes) {
     return RT_OK;
 }
 
-// (Re)allocates every per-node array with `cap` slots: tasks, node records, shadow-ray
-// origins, unshadowed-light bits.  The per-node sort buffers follow lazily
-// (sort_capacity < capacity), the shadow queue from capacity * point lights.
+// (Re)allocates every per-node array with `cap` slots: tasks, the node arrays
+// (rt_device.hpp).  The per-node sort buffers follow lazily (sort_capacity < capacity),
+// the shadow queue from capacity * point lights.
 rt_status grow_node_pool(Workspace& w, uint32_t cap) {
-    (void)hipFree(w.tasks);
-    (void)hipFree(w.nodes);
-    (void)hipFree(w.node_ps);
-    (void)hipFree(w.node_lit);
-    w.tasks = nullptr;
-    w.nodes = nullptr;
-    w.node_ps = nullptr;
-    w.node_lit = nullptr;
+    for (void** b : {(void**)&w.tasks, (void**)&w.node_flags, (void**)&w.node_ps, (void**)&w.node_n,
+                     (void**)&w.node_d, (void**)&w.node_lit, (void**)&w.node_ec, (void**)&w.node_dc,
+                     (void**)&w.node_key, (void**)&w.node_pixel}) {
+        if (*b) (void)hipFree(*b);
+        *b = nullptr;
+    }
     w.capacity = 0;
     HIP_TRY(hipMalloc(&w.tasks, (size_t)cap * sizeof(Task)));
-    HIP_TRY(hipMalloc(&w.nodes, node_alloc_count(cap) * sizeof(NodeRec)));
+    HIP_TRY(hipMalloc(&w.node_flags, (size_t)cap * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&w.node_ps, (size_t)cap * sizeof(float4)));
+    HIP_TRY(hipMalloc(&w.node_n, (size_t)cap * sizeof(float4)));
+    HIP_TRY(hipMalloc(&w.node_d, (size_t)cap * sizeof(float4)));
     HIP_TRY(hipMalloc(&w.node_lit, (size_t)cap * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&w.node_ec, 2 * (size_t)cap * sizeof(float4)));
     if (w.forest) {
-        (void)hipFree(w.node_aux);
-        (void)hipFree(w.node_key);
-        (void)hipFree(w.node_pixel);
-        w.node_aux = nullptr;
-        w.node_key = nullptr;
-        w.node_pixel = nullptr;
-        HIP_TRY(hipMalloc(&w.node_aux, (size_t)cap * sizeof(float4)));
+        HIP_TRY(hipMalloc(&w.node_dc, 2 * (size_t)cap * sizeof(float4)));
         HIP_TRY(hipMalloc(&w.node_key, (size_t)cap * sizeof(uint32_t)));
         HIP_TRY(hipMalloc(&w.node_pixel, (size_t)cap * sizeof(uint32_t)));
     }
@@ -1085,9 +1103,10 @@ rt_status grow_node_pool(Workspace& w, uint32_t cap) {
 // Frees every device / pinned buffer of a workspace.
 void free_workspace(Workspace& w) {
     for (void* b : {(void*)w.out, (void*)w.out8, (void*)w.counters, (void*)w.work, (void*)w.tasks, (void*)w.shadow,
-                    (void*)w.nodes, (void*)w.levels, (void*)w.overflow, (void*)w.node_ps, (void*)w.node_lit,
-                    (void*)w.task_keys, (void*)w.perm, (void*)w.shadow_keys, (void*)w.shadow_sorted, (void*)w.sort_tmp,
-                    (void*)w.node_aux, (void*)w.node_key, (void*)w.node_pixel})
+                    (void*)w.node_flags, (void*)w.levels, (void*)w.overflow, (void*)w.node_ps, (void*)w.node_n,
+                    (void*)w.node_d, (void*)w.node_lit, (void*)w.node_ec, (void*)w.task_keys, (void*)w.perm,
+                    (void*)w.shadow_keys, (void*)w.shadow_sorted, (void*)w.sort_tmp, (void*)w.node_dc,
+                    (void*)w.node_key, (void*)w.node_pixel})
         if (b) (void)hipFree(b);
     w = Workspace();
 }
@@ -1108,6 +1127,7 @@ const char* rt_status_str(rt_status s) {
         case RT_ERR_HIP: return "RT_ERR_HIP";
         case RT_ERR_OUT_OF_MEMORY: return "RT_ERR_OUT_OF_MEMORY";
         case RT_ERR_BAD_MATERIAL: return "RT_ERR_BAD_MATERIAL";
+        case RT_ERR_CAPACITY: return "RT_ERR_CAPACITY";
         default: return "RT_ERR_UNKNOWN";
     }
 }
@@ -1124,6 +1144,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     if ((d->n_materials && !d->materials) || (d->n_shapes && !d->shapes) || (d->n_lights && !d->lights))
         return RT_ERR_INVALID_ARG;
     if (d->n_shapes >= (1u << 27)) return RT_ERR_UNSUPPORTED;
+    if (d->n_materials > RT_MAX_MATERIALS) return RT_ERR_UNSUPPORTED;  // node_flags holds the index
 
     // ---- host preprocessing: per-shape records
     std::vector<float> dsph, gsph, tri, cube, plane, cubetri;
@@ -1323,18 +1344,22 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&sc->ev0));
     HIP_TRY(hipEventCreate(&sc->ev1));
+    HIP_TRY(hipEventCreateWithFlags(&sc->ev_last, hipEventDisableTiming));
     *out = sc.release();
     return RT_OK;
 }
 
 rt_status rt_scene_destroy(rt_scene* s) {
     if (!s) return RT_ERR_INVALID_ARG;
+    if (s->multi) rt_multi_free(s->multi);
+    s->multi = nullptr;
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     free_workspace(s->ws);
     if (s->dmem) (void)hipFree(s->dmem);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->ev_last) (void)hipEventDestroy(s->ev_last);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
     return RT_OK;
@@ -1366,29 +1391,42 @@ int32_t rt_scene_uses_bvh(const rt_scene* s) { return (s && s->S.use_bvh) ? 1 : 
 
 rt_status rt_scene_set_scan_counting(rt_scene* s, int32_t enable) {
     if (!s) return RT_ERR_INVALID_ARG;
+    if (s->multi) (void)rt_multi_each(s->multi, [&](rt_scene* c) { return rt_scene_set_scan_counting(c, enable); });
     s->count_ops = enable != 0;
     return RT_OK;
 }
 
 static uint32_t* g_task_clock = nullptr;  // RT_TASK_CLOCK records (debug)
 
+// Where one render pass's results go: the float frame (or band buffer), optionally its
+// Color::as_u8 bytes (fused into the level-0 combine), ray counters, and whether queue
+// overflows are latched into the scene's sticky status (the stream-ordered entry points;
+// rt_render retries instead).
+struct PassOut {
+    float* rgb;
+    uint8_t* rgb8;
+    unsigned long long* counters;
+    bool latch;
+};
+
 static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
-                                   uint32_t band_rows, uint32_t rank, uint32_t world, float* d_rgb,
-                                   unsigned long long* d_counters, hipStream_t stream);
+                                   uint32_t band_rows, uint32_t rank, uint32_t world, const PassOut& o,
+                                   hipStream_t stream);
 
 static rt_status launch_bands(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
-                              uint32_t band_rows, uint32_t rank, uint32_t world, float* d_rgb,
-                              unsigned long long* d_counters, hipStream_t stream) {
-    if (!s || !cam || !d_rgb || band_rows == 0 || world == 0 || rank >= world) return RT_ERR_INVALID_ARG;
+                              uint32_t band_rows, uint32_t rank, uint32_t world, const PassOut& o,
+                              hipStream_t stream) {
+    float* d_rgb = o.rgb;
+    unsigned long long* d_counters = o.counters;
+    if (!s || !cam || (!d_rgb && !o.rgb8) || band_rows == 0 || world == 0 || rank >= world) return RT_ERR_INVALID_ARG;
     if (spp == 0) return RT_ERR_INVALID_ARG;
     if (cam->x_res == 0 || cam->y_res == 0) return RT_ERR_INVALID_ARG;
     if (depth > RT_MAX_DEPTH) return RT_ERR_UNSUPPORTED;
     if ((uint64_t)cam->x_res * cam->y_res * 3 >= (1ull << 32)) return RT_ERR_UNSUPPORTED;
     rt_status st = ensure_ws(s, 0, 0);
     if (st != RT_OK) return st;
-    if (!use_megakernel())
-        return launch_bands_wave(s, cam, depth, spp, seed, band_rows, rank, world, d_rgb, d_counters, stream);
-    if (spp != 1) return RT_ERR_UNSUPPORTED;  // the per-pixel megakernel traces one sample
+    if (!use_megakernel()) return launch_bands_wave(s, cam, depth, spp, seed, band_rows, rank, world, o, stream);
+    if (spp != 1 || o.rgb8 || !d_rgb) return RT_ERR_UNSUPPORTED;  // the per-pixel megakernel traces one sample, f32 out
     RenderParams p;
     std::memset(&p, 0, sizeof(p));
     p.S = s->S;
@@ -1435,29 +1473,28 @@ static rt_status launch_bands(rt_scene* s, const rt_camera* cam, uint32_t depth,
 // per-node shade inputs, always read the level sizes on the host, skip the combine pass
 // and leave the parameters (with the device level table) in *forest_params.
 static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
-                               uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
-                               hipStream_t stream, WaveParams* forest_params, uint32_t* forest_levels,
-                               uint32_t spp = 1, uint32_t sample = 0, uint32_t seed = 0, uint32_t frames = 1,
+                               uint32_t rank, uint32_t world, const PassOut& o, hipStream_t stream,
+                               WaveParams* forest_params, uint32_t* forest_levels, uint32_t spp = 1,
+                               uint32_t sample = 0, uint32_t seed = 0, uint32_t frames = 1,
                                const rt_camera* cams = nullptr);
 
 // spp samples: one pipeline run per sample, in sample order (the level-0 combine adds
 // sample k's colour to the running sum of samples 0..k-1 and the last one divides)
 static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
-                                   uint32_t band_rows, uint32_t rank, uint32_t world, float* d_rgb,
-                                   unsigned long long* d_counters, hipStream_t stream) {
+                                   uint32_t band_rows, uint32_t rank, uint32_t world, const PassOut& o,
+                                   hipStream_t stream) {
     for (uint32_t k = 0; k < spp; k++) {
-        rt_status st = wave_pipeline(s, s->ws, cam, depth, band_rows, rank, world, d_rgb, d_counters, stream, nullptr,
-                                     nullptr, spp, k, seed);
+        rt_status st = wave_pipeline(s, s->ws, cam, depth, band_rows, rank, world, o, stream, nullptr, nullptr, spp, k,
+                                     seed);
         if (st != RT_OK) return st;
     }
     return RT_OK;
 }
 
 static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
-                               uint32_t rank, uint32_t world, float* d_rgb, unsigned long long* d_counters,
-                               hipStream_t stream, WaveParams* forest_params, uint32_t* forest_levels,
-                               uint32_t spp, uint32_t sample, uint32_t seed, uint32_t frames,
-                               const rt_camera* cams) {
+                               uint32_t rank, uint32_t world, const PassOut& o, hipStream_t stream,
+                               WaveParams* forest_params, uint32_t* forest_levels, uint32_t spp, uint32_t sample,
+                               uint32_t seed, uint32_t frames, const rt_camera* cams) {
     if (frames == 0 || frames > RT_MAX_FRAMES || (frames > 1 && (!cams || forest_params))) return RT_ERR_INVALID_ARG;
     WaveParams p;
     std::memset(&p, 0, sizeof(p));
@@ -1465,13 +1502,6 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     p.sample = sample;
     p.seed = seed;
     p.S = s->S;
-    p.cam_ox = cam->origin[0];
-    p.cam_oy = cam->origin[1];
-    p.cam_oz = cam->origin[2];
-    p.x_min = cam->x_min;
-    p.y_max = cam->y_max;
-    p.x_delta = (cam->x_max - cam->x_min) / (float)cam->x_res;  // render.rs:179-180
-    p.y_delta = (cam->y_max - cam->y_min) / (float)cam->y_res;
     p.width = cam->x_res;
     p.height = cam->y_res;
     p.depth = depth;
@@ -1505,9 +1535,15 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     if (total >= (1ull << 30)) return RT_ERR_UNSUPPORTED;
     p.total_items = (uint32_t)total;
     // node / task pool: level 0 plus room for ~11 secondary nodes per pixel on average
-    // (config 3 needs 2.7); an overflow is reported, never silently truncated
+    // (config 3 needs 2.7); an overflow is reported, never silently truncated.  A shadow
+    // entry packs (node << light_bits) | light, so nodes stay below 2^(32 - light_bits).
+    p.light_bits = light_bits(s);
+    const uint64_t max_cap = pool_cap_limit(s);
+    if (total >= max_cap) return RT_ERR_UNSUPPORTED;
     uint64_t want = std::max<uint64_t>(total * 12u, 1u << 20);
-    if (want > 0x7FFFFFFFu) want = 0x7FFFFFFFu;
+    if (const char* e = std::getenv("RT_NODE_CAP")) want = std::max<uint64_t>(total + 1, std::strtoull(e, nullptr, 0));
+    if (&w == &s->ws) want = std::max<uint64_t>(want, s->pool_floor);
+    if (want > max_cap) want = max_cap;
     if (w.capacity < want) {  // grows only (rt_render may have grown it after an overflow)
         rt_status st = grow_node_pool(w, (uint32_t)want);
         if (st != RT_OK) return st;
@@ -1515,6 +1551,7 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     if (!w.levels) {
         HIP_TRY(hipMalloc(&w.levels, RT_LEVEL_TABLE_WORDS * sizeof(uint32_t)));
         HIP_TRY(hipMalloc(&w.overflow, 64));
+        HIP_TRY(hipMemset(w.overflow, 0, 64));
     }
     // shadow queue: one entry per point light per hit node
     uint64_t want_sh = std::min<uint64_t>((uint64_t)w.capacity * s->n_point_lights, 0x7FFFFFFFu);
@@ -1640,15 +1677,20 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     p.shadow_capacity = w.shadow_capacity;
     p.shadow = w.shadow;
     p.tasks = w.tasks;
-    p.nodes = w.nodes;
+    p.node_flags = w.node_flags;
     p.node_ps = w.node_ps;
+    p.node_n = w.node_n;
+    p.node_d = w.node_d;
     p.node_lit = w.node_lit;
+    p.node_ec = w.node_ec;
     p.levels = w.levels;
     p.overflow = w.overflow;
-    p.out = d_rgb;
-    p.ray_counters = d_counters;
+    p.overflow_sticky = o.latch ? w.overflow + 1 : nullptr;
+    p.out = o.rgb;
+    p.out8 = o.rgb8;
+    p.ray_counters = o.counters;
     if (w.forest) {
-        p.node_aux = w.node_aux;
+        p.node_dc = w.node_dc;
         p.node_key = w.node_key;
         p.node_pixel = w.node_pixel;
     }
@@ -1714,34 +1756,51 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     return RT_OK;
 }
 
+rt_status rt_render_bands_ex_async(const rt_scene* scene, const rt_camera* cams, uint32_t n_frames, uint32_t depth,
+                                   uint32_t spp, uint32_t seed, uint32_t band_rows, uint32_t rank, uint32_t world,
+                                   float* d_rgb, uint8_t* d_rgb8, uint64_t* d_counters, void* stream) {
+    rt_scene* s = const_cast<rt_scene*>(scene);
+    if (!s || !cams || n_frames == 0 || n_frames > RT_MAX_FRAMES || spp == 0) return RT_ERR_INVALID_ARG;
+    if (!d_rgb && (!d_rgb8 || spp > 1)) return RT_ERR_INVALID_ARG;  // spp > 1 accumulates in d_rgb
+    if (n_frames > 1 && spp != 1) return RT_ERR_INVALID_ARG;
+    const rt_camera* cam = cams;
+    if (band_rows == 0 || world == 0 || rank >= world) return RT_ERR_INVALID_ARG;
+    if (cam->x_res == 0 || cam->y_res == 0) return RT_ERR_INVALID_ARG;
+    if (depth > RT_MAX_DEPTH) return RT_ERR_UNSUPPORTED;
+    if ((uint64_t)cam->x_res * cam->y_res * 3 >= (1ull << 32)) return RT_ERR_UNSUPPORTED;
+    HIP_TRY(hipSetDevice(s->device));
+    rt_status st = ensure_ws(s, 0, 0);
+    if (st != RT_OK) return st;
+    hipStream_t hs = (hipStream_t)stream;
+    const PassOut o{d_rgb, d_rgb8, reinterpret_cast<unsigned long long*>(d_counters), true};
+    if (n_frames == 1) {
+        if (use_megakernel() && !d_rgb) return RT_ERR_UNSUPPORTED;
+        st = launch_bands(s, cam, depth, spp, seed, band_rows, rank, world, o, hs);
+    } else {
+        if (use_megakernel()) return RT_ERR_UNSUPPORTED;
+        st = wave_pipeline(s, s->ws, cam, depth, band_rows, rank, world, o, hs, nullptr, nullptr, 1, 0, 0, n_frames,
+                           cams);
+    }
+    if (st != RT_OK) return st;
+    HIP_TRY(hipEventRecord(s->ev_last, hs));
+    s->ev_last_set = true;
+    return RT_OK;
+}
+
 rt_status rt_render_bands_spp_async(const rt_scene* scene, const rt_camera* cam, uint32_t depth, uint32_t spp,
                                     uint32_t seed, uint32_t band_rows, uint32_t rank, uint32_t world, float* d_rgb,
                                     uint64_t* d_counters, void* stream) {
-    rt_scene* s = const_cast<rt_scene*>(scene);
-    if (!s) return RT_ERR_INVALID_ARG;
-    HIP_TRY(hipSetDevice(s->device));
-    return launch_bands(s, cam, depth, spp, seed, band_rows, rank, world, d_rgb,
-                        reinterpret_cast<unsigned long long*>(d_counters), (hipStream_t)stream);
+    if (!d_rgb) return RT_ERR_INVALID_ARG;
+    return rt_render_bands_ex_async(scene, cam, 1, depth, spp, seed, band_rows, rank, world, d_rgb, nullptr,
+                                    d_counters, stream);
 }
 
 rt_status rt_render_bands_batch_async(const rt_scene* scene, const rt_camera* cams, uint32_t n_frames,
                                       uint32_t depth, uint32_t band_rows, uint32_t rank, uint32_t world,
                                       float* d_rgb, uint64_t* d_counters, void* stream) {
-    rt_scene* s = const_cast<rt_scene*>(scene);
-    if (!s || !cams || n_frames == 0 || n_frames > RT_MAX_FRAMES) return RT_ERR_INVALID_ARG;
-    if (n_frames == 1)
-        return rt_render_bands_spp_async(scene, cams, depth, 1, 0, band_rows, rank, world, d_rgb, d_counters, stream);
-    const rt_camera* cam = cams;
-    if (!d_rgb || band_rows == 0 || world == 0 || rank >= world) return RT_ERR_INVALID_ARG;
-    if (cam->x_res == 0 || cam->y_res == 0) return RT_ERR_INVALID_ARG;
-    if (depth > RT_MAX_DEPTH) return RT_ERR_UNSUPPORTED;
-    if (use_megakernel()) return RT_ERR_UNSUPPORTED;
-    HIP_TRY(hipSetDevice(s->device));
-    rt_status st = ensure_ws(s, 0, 0);
-    if (st != RT_OK) return st;
-    return wave_pipeline(s, s->ws, cam, depth, band_rows, rank, world, d_rgb,
-                         reinterpret_cast<unsigned long long*>(d_counters), (hipStream_t)stream, nullptr, nullptr, 1,
-                         0, 0, n_frames, cams);
+    if (!d_rgb) return RT_ERR_INVALID_ARG;
+    return rt_render_bands_ex_async(scene, cams, n_frames, depth, 1, 0, band_rows, rank, world, d_rgb, nullptr,
+                                    d_counters, stream);
 }
 
 rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* cam, uint32_t depth,
@@ -1750,12 +1809,72 @@ rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* cam, uin
     return rt_render_bands_spp_async(scene, cam, depth, 1, 0, band_rows, rank, world, d_rgb, d_counters, stream);
 }
 
+rt_status rt_scene_sync_status(rt_scene* s) {
+    if (!s) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(s->device));
+    if (s->ev_last_set) HIP_TRY(hipEventSynchronize(s->ev_last));
+    if (!s->ws.overflow) return RT_OK;
+    uint32_t v = 0;
+    HIP_TRY(hipMemcpy(&v, s->ws.overflow + 1, sizeof(v), hipMemcpyDeviceToHost));
+    if (!v) return RT_OK;
+    HIP_TRY(hipMemset(s->ws.overflow + 1, 0, sizeof(v)));
+    // the next pass on this scene gets a pool twice as large (up to the index limit)
+    s->pool_floor = (uint32_t)std::min<uint64_t>(2ull * s->ws.capacity, pool_cap_limit(s));
+    return RT_ERR_CAPACITY;
+}
+
+rt_status rt_scene_clone(const rt_scene* src, int32_t device, rt_scene** out) {
+    if (!src || !out) return RT_ERR_INVALID_ARG;
+    std::unique_ptr<rt_scene> sc(new (std::nothrow) rt_scene());
+    if (!sc) return RT_ERR_OUT_OF_MEMORY;
+    rt_status st = select_device(device, &sc->device);
+    if (st != RT_OK) return st;
+    HIP_TRY(hipMalloc(&sc->dmem, src->dbytes));
+    sc->dbytes = src->dbytes;
+    if (sc->device == src->device)
+        HIP_TRY(hipMemcpy(sc->dmem, src->dmem, src->dbytes, hipMemcpyDeviceToDevice));
+    else
+        HIP_TRY(hipMemcpyPeer(sc->dmem, sc->device, src->dmem, src->device, src->dbytes));
+    HIP_TRY(hipMemset((uint8_t*)sc->dmem + ((const uint8_t*)src->S.scan_ops - (const uint8_t*)src->dmem), 0,
+                      RT_OPS_SLOTS * RT_OPS_STRIDE * sizeof(unsigned long long)));
+    // the same DevScene, every pointer rebased into the new allocation
+    sc->S = src->S;
+    const uint8_t* from = (const uint8_t*)src->dmem;
+    uint8_t* to = (uint8_t*)sc->dmem;
+    auto rebase = [&](auto& ptr) {
+        if (ptr) ptr = reinterpret_cast<std::remove_reference_t<decltype(ptr)>>(to + ((const uint8_t*)ptr - from));
+    };
+    DevScene& S = sc->S;
+    rebase(S.dsph); rebase(S.gsph); rebase(S.tri); rebase(S.cube); rebase(S.plane); rebase(S.cubetri);
+    rebase(S.shapes); rebase(S.mats); rebase(S.lights); rebase(S.bvh_nodes); rebase(S.bvh_leaves);
+    rebase(S.graze_blk); rebase(S.graze_tri); rebase(S.graze_pn); rebase(S.graze_mask); rebase(S.scan_ops);
+    sc->flops_per_scan = src->flops_per_scan;
+    sc->n_point_lights = src->n_point_lights;
+    sc->num_cus = g_num_cus(sc->device);
+    sc->count_ops = src->count_ops;
+    HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&sc->ev0));
+    HIP_TRY(hipEventCreate(&sc->ev1));
+    HIP_TRY(hipEventCreateWithFlags(&sc->ev_last, hipEventDisableTiming));
+    *out = sc.release();
+    return RT_OK;
+}
+
 rt_status rt_unpermute_bands_async(const float* d_gathered, uint32_t x_res, uint32_t y_res,
                                    uint32_t band_rows, uint32_t world, float* d_frame, void* stream) {
     if (!d_gathered || !d_frame || band_rows == 0 || world == 0 || x_res == 0 || y_res == 0)
         return RT_ERR_INVALID_ARG;
     uint32_t rpr = rt_band_rows_per_rank(y_res, band_rows, world);
     HIP_TRY(launch_unpermute(d_gathered, x_res, y_res, band_rows, world, rpr, d_frame, (hipStream_t)stream));
+    return RT_OK;
+}
+
+rt_status rt_unpermute_bands_u8_async(const uint8_t* d_gathered, uint32_t x_res, uint32_t y_res,
+                                      uint32_t band_rows, uint32_t world, uint8_t* d_frame, void* stream) {
+    if (!d_gathered || !d_frame || band_rows == 0 || world == 0 || x_res == 0 || y_res == 0)
+        return RT_ERR_INVALID_ARG;
+    uint32_t rpr = rt_band_rows_per_rank(y_res, band_rows, world);
+    HIP_TRY(launch_unpermute_u8(d_gathered, x_res, y_res, band_rows, world, rpr, d_frame, (hipStream_t)stream));
     return RT_OK;
 }
 
@@ -1776,29 +1895,36 @@ rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t de
     rt_scene* s = const_cast<rt_scene*>(scene);
     if (!s || !cam || !rgb || spp == 0) return RT_ERR_INVALID_ARG;
     if (opts && opts->device >= 0 && opts->device != s->device) return RT_ERR_INVALID_ARG;
+    if (s->multi) return rt_multi_render(s, cam, depth, spp, seed, opts, rgb, rgb8);
     HIP_TRY(hipSetDevice(s->device));
     size_t n = (size_t)cam->x_res * cam->y_res * 3;
-    rt_status st = ensure_ws(s, n, rgb8 ? n : 0);
+    // one band share holding every row: its buffer has the padded row count (the pass
+    // zero-fills rows y_res .. rows_local - 1); the first y_res rows are the frame
+    const size_t n_pad = (size_t)cam->x_res * rt_band_rows_per_rank(cam->y_res, 8, 1) * 3;
+    rt_status st = ensure_ws(s, n_pad, rgb8 ? n_pad : 0);
     if (st != RT_OK) return st;
     hipStream_t stream = s->stream;
+    const bool mega = use_megakernel();
     for (int attempt = 0;; attempt++) {
         HIP_TRY(hipMemsetAsync(s->ws.counters, 0, 4 * sizeof(unsigned long long), stream));
         HIP_TRY(hipEventRecord(s->ev0, stream));
-        // single device: one "band" holding every row
-        st = launch_bands(s, cam, depth, spp, seed, 8, 0, 1, s->ws.out, s->ws.counters, stream);
+        // single device: one "band" holding every row; as_u8 fused into the level-0 combine
+        const PassOut o{s->ws.out, (rgb8 && !mega) ? s->ws.out8 : nullptr, s->ws.counters, false};
+        st = launch_bands(s, cam, depth, spp, seed, 8, 0, 1, o, stream);
         if (st != RT_OK) return st;
         HIP_TRY(hipEventRecord(s->ev1, stream));
-        if (use_megakernel() || !s->ws.overflow) break;
+        if (mega || !s->ws.overflow) break;
         uint32_t ovf = 0;
         HIP_TRY(hipMemcpyAsync(&ovf, s->ws.overflow, sizeof(ovf), hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
         if (!ovf) break;
         // node pool too small for this scene's ray trees: grow it and render again
-        if (attempt >= 6 || s->ws.capacity >= 0x40000000u) return RT_ERR_OUT_OF_MEMORY;
-        rt_status st = grow_node_pool(s->ws, s->ws.capacity * 2u);
-        if (st != RT_OK) return st;
+        const uint64_t lim = pool_cap_limit(s);
+        if (attempt >= 8 || s->ws.capacity >= lim) return RT_ERR_CAPACITY;
+        rt_status g = grow_node_pool(s->ws, (uint32_t)std::min<uint64_t>(2ull * s->ws.capacity, lim));
+        if (g != RT_OK) return g;
     }
-    if (rgb8) HIP_TRY(launch_quantize(s->ws.out, n, s->ws.out8, stream));
+    if (rgb8 && mega) HIP_TRY(launch_quantize(s->ws.out, n, s->ws.out8, stream));
     HIP_TRY(hipMemcpyAsync(rgb, s->ws.out, n * sizeof(float), hipMemcpyDeviceToHost, stream));
     if (rgb8) HIP_TRY(hipMemcpyAsync(rgb8, s->ws.out8, n, hipMemcpyDeviceToHost, stream));
     unsigned long long cnt[4] = {0, 0, 0, 0};
@@ -1873,7 +1999,7 @@ rt_status forest_mark(rt_forest* f, const int32_t* ids, uint32_t n_ids, bool siz
         mask = f->key_mask;
     }
     if (sizes) HIP_TRY(hipMemsetAsync(f->sizes, 0, px * sizeof(uint32_t), st));
-    HIP_TRY(launch_forest_mark(f->ws.node_key, f->ws.node_pixel, f->ws.nodes, f->n_nodes, mask, f->n_keys, f->mark,
+    HIP_TRY(launch_forest_mark(f->ws.node_key, f->ws.node_pixel, f->ws.node_flags, f->n_nodes, mask, f->n_keys, f->mark,
                                sizes ? f->sizes : nullptr, st));
     return RT_OK;
 }
@@ -1914,14 +2040,16 @@ rt_status rt_forest_create(rt_scene* s, const rt_camera* cam, uint32_t depth, rt
     const uint32_t band_rows = 8;
     for (int attempt = 0;; attempt++) {
         HIP_TRY(hipMemsetAsync(f->counters, 0, 4 * sizeof(unsigned long long), st));
-        rt_status r = wave_pipeline(s, f->ws, cam, depth, band_rows, 0, 1, nullptr, f->counters, st, &f->p, f->levels);
+        const PassOut o{nullptr, nullptr, f->counters, false};
+        rt_status r = wave_pipeline(s, f->ws, cam, depth, band_rows, 0, 1, o, st, &f->p, f->levels);
         if (r != RT_OK) return r;
         uint32_t ovf = 0;
         HIP_TRY(hipMemcpyAsync(&ovf, f->ws.overflow, sizeof(ovf), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         if (!ovf) break;
-        if (attempt >= 6 || f->ws.capacity >= 0x40000000u) return RT_ERR_OUT_OF_MEMORY;
-        rt_status g = grow_node_pool(f->ws, f->ws.capacity * 2u);
+        const uint64_t lim = pool_cap_limit(s);
+        if (attempt >= 8 || f->ws.capacity >= lim) return RT_ERR_CAPACITY;
+        rt_status g = grow_node_pool(f->ws, (uint32_t)std::min<uint64_t>(2ull * f->ws.capacity, lim));
         if (g != RT_OK) return g;
     }
     uint32_t used = f->levels[2 * (RT_MAX_DEPTH + 1)];
@@ -2015,6 +2143,7 @@ rt_status rt_scene_set_material(rt_scene* s, uint32_t index, const rt_material* 
     rt_status r = mat_rec(*m, M);
     if (r != RT_OK) return r;
     HIP_TRY(hipMemcpy(const_cast<MatRec*>(s->S.mats) + index, &M, sizeof(M), hipMemcpyHostToDevice));
+    if (s->multi) return rt_multi_each(s->multi, [&](rt_scene* c) { return rt_scene_set_material(c, index, m); });
     return RT_OK;
 }
 

@@ -227,6 +227,14 @@ __device__ __forceinline__ int32_t sat_i32(float x) {
     return (int32_t)x;
 }
 
+// Color::as_u8 (color.rs:43-46): (255 * c) as u8 -- truncating, saturating, NaN -> 0
+__device__ __forceinline__ uint8_t as_u8(float c) {
+    const float x = 255.f * c;
+    uint8_t q = 0;
+    if (x > 0.f) q = (x >= 255.f) ? (uint8_t)255 : (uint8_t)x;
+    return q;
+}
+
 // texture programs: CONST colour, or my_scene.rs:26-43 checkerboard
 __device__ __forceinline__ V3 tex_eval(const TexRec& t, float tu, float tv) {
     if (t.kind == RT_TEX_CHECKERBOARD) {
@@ -283,6 +291,50 @@ enum : uint32_t {
     F_WAIT_REFR = 32u, // waiting for (or about to trace) the refraction child
     F_PEND_REFR = 64u  // refraction child still to be traced after the reflection child
 };
+
+// reflect_ray's direction (render.rs:105-110, Vector3::reflect vector3.rs:113-115)
+__device__ __forceinline__ V3 reflect_dir(V3 rd, V3 n) { return neg(norm(sub(mul(n, 2.f * dot(rd, n)), rd))); }
+
+// refract_ray's direction (render.rs:112-125; not re-normalised); false = total internal
+// reflection (None)
+__device__ __forceinline__ bool refract_dir(V3 rd, V3 n, float n1, float n2, V3& trd) {
+    float ratio = n1 / n2;
+    float m_dot_r = -dot(rd, n);
+    float cos2 = 1.f - ratio * ratio * (1.f - m_dot_r * m_dot_r);
+    if (!(cos2 > 0.f)) return false;
+    float ct = sqrtf(cos2);
+    trd = add(mul(rd, ratio), mul(n, ratio * m_dot_r - ct));
+    return true;
+}
+
+// The child weights of a hit node (render.rs:70-98), from what the trace pass stores
+// (ray direction, normal) and the material: the same expressions the trace pass uses for
+// the child rays, so the combine pass re-evaluates them bit for bit.  f.flags gets F_REFL
+// / F_SPEC / F_REFR / F_TIR; the caller fills the ambient + lights and kd / ks.
+__device__ __forceinline__ void node_weights(const MatRec& M, V3 rd, V3 n, V3 eye, float n1, float n2, Frame& f) {
+    f.flags = 0u;
+    f.fr = f.dr = f.pw = f.ft = 0.f;
+    if (M.reflectivity > RT_EPS) {
+        f.flags |= F_REFL;
+        const V3 rrd = reflect_dir(rd, n);
+        f.fr = fresnel_reflection(rrd, n, n1, n2);
+        f.dr = dot(rrd, n);
+        const V3 hv = norm(add(norm(eye), norm(rrd)));
+        const float mh = dot(n, hv);
+        if (!(mh < 0.f)) {
+            f.flags |= F_SPEC;
+            f.pw = powf(mh, M.power);
+        }
+    }
+    if (M.refraction_index > RT_EPS) {
+        f.flags |= F_REFR;
+        V3 trd;
+        if (refract_dir(rd, n, n1, n2, trd))
+            f.ft = 1.f - fresnel_reflection(trd, neg(n), n1, n2);
+        else
+            f.flags |= F_TIR;
+    }
+}
 
 // ((ambient + lights) + reflected) + refracted, render.rs:100
 __device__ __forceinline__ V3 combine(const Frame& f, V3 er, V3 et) {

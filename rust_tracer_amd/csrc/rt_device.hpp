@@ -154,25 +154,28 @@ struct Task {
     uint32_t pixel;    // y * width + x of the tree's pixel (ray forest)
 };
 
-// One traced tree node: the shading inputs of render.rs:57-68 (lights are summed later,
-// once the shadow scans have run), the child weights of render.rs:70-98, the colours its
-// children report, and where to report its own colour: 8 float4 chunks (128 B),
-//   NC_AMB {ambient (tex) * scene ambient, flags}   NC_N   {hit normal, parent}
-//   NC_EYE {eye_dir, power}                         NC_KD  {kd, n1}     NC_KS {ks, n2}
-//   NC_W   {fresnel_r, rdir.n, (m.h)^power, 1 - fresnel_t}
-//   NC_ER  {colour of the reflected child, -}       NC_ET  {... of the refracted child, -}
-// stored AoSoA: blocks of 64 nodes, chunk-major inside a block (rt_wavefront.hip
-// node_c), so a wave's load or store of one chunk is one contiguous 1 KB access.  The
-// shadow-ray origin lives in the compact `node_ps` array and the shadow results in
-// `node_lit` (bit l: point light l is NOT shadowed): the shadow pass's randomly ordered
-// accesses touch 16 + 4 bytes per entry.  (Ray forest: NC_KD / NC_KS hold the children's
-// directions instead, render_tree.rs:214-255.)
-enum : int { NC_AMB = 0, NC_N = 1, NC_EYE = 2, NC_KD = 3, NC_KS = 4, NC_W = 5, NC_ER = 6, NC_ET = 7, NC_CHUNKS = 8 };
-struct NodeRec {
-    float4 c[NC_CHUNKS];  // allocation unit only; element n lives at node_c(base, n, chunk)
+// One traced tree node, in structure-of-arrays form (index n = the node's slot in its
+// level's queue, so a wave's accesses to one array are one contiguous 1 KB run):
+//   node_flags[n]  NODE_HIT / NODE_MISS / NODE_NONE | F_HAS_R / F_HAS_T (a reflected /
+//                  refracted child was queued) | F_ENTER | material index << F_MAT_SHIFT
+//   node_ps[n]     {shadow-ray origin p + 0.0002 n (render.rs:147), texture u}
+//   node_n[n]      {hit normal, texture v}
+//   node_d[n]      {the ray's direction, parent = (parent node << 1) | slot}
+//   node_lit[n]    bit l: point light l is NOT shadowed
+//   node_ec[2n+s]  colour the node's child in slot s (0 reflected, 1 refracted) reports
+// That is 52 B written per hit node.  Everything else render.rs:57-100 needs (eye_dir,
+// n1 / n2, the material's textures at (u, v), the reflected direction, Schlick weights,
+// (m.h)^power, the refracted direction) is a pure function of these and the material,
+// and the combine pass re-evaluates it with the trace kernel's own expressions
+// (rt_common.hpp node_weights), bit for bit.  The shadow pass reads node_ps at random
+// (16 B per entry).  Ray forest (render_tree.rs): node_dc[2n+s] holds the direction the
+// child reports (render_tree.rs:252), node_key / node_pixel the shape id and pixel.
+enum : uint32_t {
+    NODE_HIT = 1u << 8, NODE_MISS = 1u << 9, NODE_NONE = 1u << 10,
+    F_HAS_R = 1u << 11, F_HAS_T = 1u << 12, F_ENTER = 1u << 13,
+    F_MAT_SHIFT = 14u   // material index: up to 2^18 materials
 };
-// nodes to allocate for `cap` slots (whole 64-node blocks)
-inline size_t node_alloc_count(uint32_t cap) { return ((size_t)cap + 63u) & ~(size_t)63u; }
+#define RT_MAX_MATERIALS (1u << 18)
 
 // frame batches (rt_render_bands_batch_async): up to RT_MAX_FRAMES frames of one
 // resolution in one pipeline pass; a task carries its frame in Task.pixel's top bits
@@ -183,8 +186,6 @@ struct FrameCam {
 };
 struct WaveParams {
     DevScene S;
-    float cam_ox, cam_oy, cam_oz;
-    float x_min, y_max, x_delta, y_delta;
     uint32_t frames;                   // frames in this pass (1: rt_render_bands_async)
     uint32_t frame_items;              // level-0 items per frame (total_items / frames)
     uint32_t task_frame_shift;         // task key |= frame << this (frames > 1)
@@ -197,15 +198,21 @@ struct WaveParams {
     uint32_t capacity;                 // node / task slots
     uint32_t shadow_capacity;          // shadow-queue slots
     Task* tasks;                       // [capacity]
-    NodeRec* nodes;                    // [capacity]
-    float4* node_ps;                   // [capacity]: shadow-ray origin (w unused)
+    uint32_t* node_flags;              // [capacity] (node layout above)
+    float4* node_ps;                   // [capacity]
+    float4* node_n;                    // [capacity]
+    float4* node_d;                    // [capacity]
     uint32_t* node_lit;                // [capacity]: unshadowed-light bits
-    uint32_t* shadow;                  // [shadow_capacity]: (node << 5) | light
+    float4* node_ec;                   // [2 x capacity]: children's colours
+    uint32_t* shadow;                  // [shadow_capacity]: (node << light_bits) | light
+    uint32_t light_bits;               // bits of the light index in a shadow entry
     uint32_t* levels;                  // [RT_LEVEL_TABLE_WORDS]: offset, count per level;
                                        // levels[2 * (RT_MAX_DEPTH + 1)] = shadow-queue count;
                                        // then the work counters (RT_WORK_WORD)
-    uint32_t* overflow;                // set when an append would exceed a capacity
+    uint32_t* overflow;                // set when an append would exceed a capacity (this pass)
+    uint32_t* overflow_sticky;         // ORed with `overflow` at the end of every pass (rt_scene_sync_status)
     float* out;
+    uint8_t* out8;                     // optional: Color::as_u8 of `out`, written by the level-0 combine
     unsigned long long* ray_counters;  // [node, shadow, pixels], added to
     // ray-queue ordering (rt_order.hip): the producer writes a 16-bit key per task /
     // shadow entry; the sort writes the order; the consumer reads through `perm` (tasks)
@@ -220,7 +227,7 @@ struct WaveParams {
     uint32_t light_shift;              // shadow key = (light << light_shift) | (Morton >> (15 - light_shift))
     uint32_t count_mask;               // bit 0: trace kernels add to scan_ops, bit 1: shadow kernel
     // ray forest (render_tree.rs; set only when building an rt_forest): per node
-    float4* node_aux;                  // {material index bits, tex u, tex v, entering bits}
+    float4* node_dc;                   // [2 x capacity]: directions the children report
     uint32_t* node_key;                // shape id as the reference records it (cube: inner triangle)
     uint32_t* node_pixel;              // y * width + x of the tree's pixel
     const uint8_t* dirty;              // forest shade: per-pixel mask (null: every pixel)

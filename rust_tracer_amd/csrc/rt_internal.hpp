@@ -1,0 +1,19 @@
+// rt_internal.hpp -- what rt_multi.cpp (the multi-device render behind rt_scene_create_multi)
+// needs from rt_api.cpp's scene handle.  Not part of the C ABI.
+#pragma once
+#include <functional>
+
+#include "../../include/rt_api.h"
+
+struct rt_multi_state;
+
+// The multi-device state a primary scene handle carries (null: a one-device scene).
+rt_multi_state*& rt_scene_multi(rt_scene* s);
+int rt_scene_device_of(const rt_scene* s);
+
+// rt_render_spp on a multi-device scene (rt_multi.cpp).
+rt_status rt_multi_render(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
+                          const rt_render_opts* opts, float* rgb, uint8_t* rgb8);
+// Applies `f` to every clone (devices[1..]) of a multi-device scene; first error wins.
+rt_status rt_multi_each(rt_multi_state* m, const std::function<rt_status(rt_scene*)>& f);
+void rt_multi_free(rt_multi_state* m);

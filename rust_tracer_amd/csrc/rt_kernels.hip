@@ -284,17 +284,19 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
     cnt_flush(cnt, ops_slot(S));
 }
 
-// Scatter gathered per-rank band buffers into the row-major frame (one block row per frame row).
-__global__ void unpermute_kernel(const float* __restrict__ in, uint32_t row_floats, uint32_t height,
+// Scatter gathered per-rank band buffers into the row-major frame (one block row per frame
+// row); T = float (RGB f32) or uint8_t (RGB8, Color::as_u8 values).
+template <class T>
+__global__ void unpermute_kernel(const T* __restrict__ in, uint32_t row_floats, uint32_t height,
                                  uint32_t band_rows, uint32_t world, uint32_t rows_per_rank,
-                                 float* __restrict__ out) {
+                                 T* __restrict__ out) {
     uint32_t v = blockIdx.y;
     if (v >= height) return;
     uint32_t band = v / band_rows;
     uint32_t rank = band % world;
     uint32_t lr = (band / world) * band_rows + (v - band * band_rows);
-    const float* src = in + ((size_t)rank * rows_per_rank + lr) * row_floats;
-    float* dst = out + (size_t)v * row_floats;
+    const T* src = in + ((size_t)rank * rows_per_rank + lr) * row_floats;
+    T* dst = out + (size_t)v * row_floats;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < row_floats; i += gridDim.x * blockDim.x)
         dst[i] = src[i];
 }
@@ -303,12 +305,7 @@ __global__ void unpermute_kernel(const float* __restrict__ in, uint32_t row_floa
 __global__ void quantize_kernel(const float* __restrict__ in, size_t n, uint8_t* __restrict__ out) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (; i < n; i += stride) {
-        float x = 255.f * in[i];
-        uint8_t q = 0;
-        if (x > 0.f) q = (x >= 255.f) ? (uint8_t)255 : (uint8_t)x;
-        out[i] = q;
-    }
+    for (; i < n; i += stride) out[i] = as_u8(in[i]);
 }
 
 }  // namespace rtdev
@@ -360,7 +357,16 @@ hipError_t launch_unpermute(const float* in, uint32_t x_res, uint32_t y_res, uin
                             uint32_t world, uint32_t rows_per_rank, float* out, hipStream_t stream) {
     uint32_t row_floats = x_res * 3u;
     dim3 grid((row_floats + 255) / 256, y_res);
-    hipLaunchKernelGGL(unpermute_kernel, grid, dim3(256), 0, stream, in, row_floats, y_res, band_rows, world,
+    hipLaunchKernelGGL(unpermute_kernel<float>, grid, dim3(256), 0, stream, in, row_floats, y_res, band_rows, world,
+                       rows_per_rank, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpermute_u8(const uint8_t* in, uint32_t x_res, uint32_t y_res, uint32_t band_rows,
+                               uint32_t world, uint32_t rows_per_rank, uint8_t* out, hipStream_t stream) {
+    uint32_t row_bytes = x_res * 3u;
+    dim3 grid((row_bytes + 255) / 256, y_res);
+    hipLaunchKernelGGL(unpermute_kernel<uint8_t>, grid, dim3(256), 0, stream, in, row_bytes, y_res, band_rows, world,
                        rows_per_rank, out);
     return hipGetLastError();
 }

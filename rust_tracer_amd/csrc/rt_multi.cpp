@@ -1,0 +1,342 @@
+// rt_multi.cpp -- the multi-GPU render inside the C ABI.
+//
+// The reference renders one frame on one core (src/render.rs:31-38); its pixels are
+// independent, so a frame tiles across devices with a single exchange step.  A scene made
+// by rt_scene_create_multi(desc, devices, n) is built once on the host, uploaded to
+// devices[0] and cloned device-to-device to the others (rt_scene_clone: one workspace and
+// stream per device).  rt_render / rt_render_spp on it, from ONE host thread:
+//
+//   rank r (device devices[r]):  rows dealt in block-cyclic bands of 8 (band b -> rank
+//                                b % n), rendered into the rank's band buffer
+//                                (rt_render_bands_ex_async, f32 + optional fused RGB8)
+//   exchange:                    ncclGather of every band buffer to rank 0 (RCCL over xGMI;
+//                                one communicator per device from ncclCommInitAll, all
+//                                gathers in one ncclGroupStart / ncclGroupEnd)
+//   rank 0:                      un-permute kernel -> row-major frame -> caller's buffers
+//
+// RCCL is loaded at rt_scene_create_multi time (dlopen of librccl.so.1): a process that
+// already holds PyTorch's RCCL (same soname) shares it, and single-device use never loads
+// it.  A device listed more than once shares one GPU between band shares; RCCL cannot put
+// two ranks on one device, so such a scene exchanges bands with device copies instead (a
+// test configuration: it runs the multi-device band logic on a one-GPU machine).
+#include <hip/hip_runtime.h>
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/rt_api.h"
+#include "rt_internal.hpp"
+
+namespace {
+
+#define MHIP(x)                                                                                      \
+    do {                                                                                             \
+        hipError_t e_ = (x);                                                                         \
+        if (e_ != hipSuccess) {                                                                      \
+            std::fprintf(stderr, "rt_multi.cpp:%d: %s: %s\n", __LINE__, #x, hipGetErrorString(e_)); \
+            return e_ == hipErrorOutOfMemory ? RT_ERR_OUT_OF_MEMORY : RT_ERR_HIP;                    \
+        }                                                                                            \
+    } while (0)
+
+struct Rccl {
+    void* h = nullptr;
+    ncclResult_t (*init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+bool load_rccl(Rccl& r) {
+    r.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!r.h) r.h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!r.h) return false;
+    r.init_all = (decltype(r.init_all))dlsym(r.h, "ncclCommInitAll");
+    r.gather = (decltype(r.gather))dlsym(r.h, "ncclGather");
+    r.group_start = (decltype(r.group_start))dlsym(r.h, "ncclGroupStart");
+    r.group_end = (decltype(r.group_end))dlsym(r.h, "ncclGroupEnd");
+    r.destroy = (decltype(r.destroy))dlsym(r.h, "ncclCommDestroy");
+    r.error_string = (decltype(r.error_string))dlsym(r.h, "ncclGetErrorString");
+    return r.init_all && r.gather && r.group_start && r.group_end && r.destroy && r.error_string;
+}
+
+}  // namespace
+
+struct rt_multi_state {
+    std::vector<int> devices;
+    std::vector<rt_scene*> ranks;            // ranks[0] = the primary handle (not owned here)
+    std::vector<hipStream_t> streams;        // one per rank, on its device
+    std::vector<hipEvent_t> done;            // per rank: its band is rendered (copy exchange)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr; // device 0: the render's span
+    std::vector<float*> band;                // per rank: rows_per_rank x x_res x 3 floats
+    std::vector<uint8_t*> band8;             // per rank: ... bytes (when RGB8 is asked for)
+    std::vector<unsigned long long*> counters;  // per rank: node, shadow, pixel rays
+    size_t band_floats = 0;
+    bool have8 = false;
+    float* gathered = nullptr;               // device 0: world band buffers, rank-major
+    uint8_t* gathered8 = nullptr;
+    float* frame = nullptr;                  // device 0: the row-major frame
+    uint8_t* frame8 = nullptr;
+    size_t frame_floats = 0;
+    bool rccl = false;
+    Rccl lib;
+    std::vector<ncclComm_t> comms;
+};
+
+rt_status rt_multi_each(rt_multi_state* m, const std::function<rt_status(rt_scene*)>& f) {
+    for (size_t r = 1; r < m->ranks.size(); r++) {
+        rt_status st = f(m->ranks[r]);
+        if (st != RT_OK) return st;
+    }
+    return RT_OK;
+}
+
+static void free_buffers(rt_multi_state* m) {
+    for (size_t r = 0; r < m->band.size(); r++) {
+        (void)hipSetDevice(m->devices[r]);
+        if (m->band[r]) (void)hipFree(m->band[r]);
+        if (m->band8[r]) (void)hipFree(m->band8[r]);
+        m->band[r] = nullptr;
+        m->band8[r] = nullptr;
+    }
+    (void)hipSetDevice(m->devices[0]);
+    for (void* b : {(void*)m->gathered, (void*)m->gathered8, (void*)m->frame, (void*)m->frame8})
+        if (b) (void)hipFree(b);
+    m->gathered = m->frame = nullptr;
+    m->gathered8 = m->frame8 = nullptr;
+    m->band_floats = m->frame_floats = 0;
+    m->have8 = false;
+}
+
+void rt_multi_free(rt_multi_state* m) {
+    if (!m) return;
+    for (size_t r = 0; r < m->streams.size(); r++) {
+        (void)hipSetDevice(m->devices[r]);
+        if (m->streams[r]) (void)hipStreamSynchronize(m->streams[r]);
+    }
+    free_buffers(m);
+    for (size_t r = 0; r < m->ranks.size(); r++) {
+        (void)hipSetDevice(m->devices[r]);
+        if (r < m->counters.size() && m->counters[r]) (void)hipFree(m->counters[r]);
+        if (r < m->done.size() && m->done[r]) (void)hipEventDestroy(m->done[r]);
+        if (r < m->streams.size() && m->streams[r]) (void)hipStreamDestroy(m->streams[r]);
+        if (r > 0 && m->ranks[r]) (void)rt_scene_destroy(m->ranks[r]);
+    }
+    for (ncclComm_t c : m->comms)
+        if (c) (void)m->lib.destroy(c);
+    (void)hipSetDevice(m->devices[0]);
+    if (m->ev0) (void)hipEventDestroy(m->ev0);
+    if (m->ev1) (void)hipEventDestroy(m->ev1);
+    delete m;  // the RCCL library stays loaded (another communicator may use it)
+}
+
+static rt_status ensure_buffers(rt_multi_state* m, size_t band_floats, size_t frame_floats, bool want8) {
+    if (band_floats <= m->band_floats && frame_floats <= m->frame_floats && (!want8 || m->have8)) return RT_OK;
+    free_buffers(m);
+    const size_t world = m->ranks.size();
+    for (size_t r = 0; r < world; r++) {
+        MHIP(hipSetDevice(m->devices[r]));
+        MHIP(hipMalloc(&m->band[r], band_floats * sizeof(float)));
+        if (want8) MHIP(hipMalloc(&m->band8[r], band_floats));
+    }
+    MHIP(hipSetDevice(m->devices[0]));
+    MHIP(hipMalloc(&m->gathered, world * band_floats * sizeof(float)));
+    MHIP(hipMalloc(&m->frame, frame_floats * sizeof(float)));
+    if (want8) {
+        MHIP(hipMalloc(&m->gathered8, world * band_floats));
+        MHIP(hipMalloc(&m->frame8, frame_floats));
+    }
+    m->band_floats = band_floats;
+    m->frame_floats = frame_floats;
+    m->have8 = want8;
+    return RT_OK;
+}
+
+rt_status rt_multi_render(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
+                          const rt_render_opts* opts, float* rgb, uint8_t* rgb8) {
+    rt_multi_state* m = rt_scene_multi(s);
+    if (!cam || cam->x_res == 0 || cam->y_res == 0) return RT_ERR_INVALID_ARG;
+    const uint32_t world = (uint32_t)m->ranks.size(), band_rows = 8;
+    const uint32_t rpr = rt_band_rows_per_rank(cam->y_res, band_rows, world);
+    const size_t bf = (size_t)rpr * cam->x_res * 3u, ff = (size_t)cam->y_res * cam->x_res * 3u;
+    rt_status st = ensure_buffers(m, bf, ff, rgb8 != nullptr);
+    if (st != RT_OK) return st;
+    hipStream_t s0 = m->streams[0];
+    for (int attempt = 0;; attempt++) {
+        for (uint32_t r = 0; r < world; r++) {
+            MHIP(hipSetDevice(m->devices[r]));
+            MHIP(hipMemsetAsync(m->counters[r], 0, 3 * sizeof(unsigned long long), m->streams[r]));
+        }
+        MHIP(hipSetDevice(m->devices[0]));
+        MHIP(hipEventRecord(m->ev0, s0));
+        for (uint32_t r = 0; r < world; r++) {
+            st = rt_render_bands_ex_async(m->ranks[r], cam, 1, depth, spp, seed, band_rows, r, world, m->band[r],
+                                          rgb8 ? m->band8[r] : nullptr, (uint64_t*)m->counters[r], m->streams[r]);
+            if (st != RT_OK) return st;
+        }
+        // the one exchange step: every band buffer to rank 0
+        if (m->rccl) {
+            if (m->lib.group_start() != ncclSuccess) return RT_ERR_HIP;
+            for (uint32_t r = 0; r < world; r++) {
+                ncclResult_t e = m->lib.gather(m->band[r], r == 0 ? m->gathered : nullptr, bf, ncclFloat32, 0,
+                                               m->comms[r], m->streams[r]);
+                if (e == ncclSuccess && rgb8)
+                    e = m->lib.gather(m->band8[r], r == 0 ? m->gathered8 : nullptr, bf, ncclUint8, 0, m->comms[r],
+                                      m->streams[r]);
+                if (e != ncclSuccess) {
+                    std::fprintf(stderr, "rt_multi.cpp: ncclGather: %s\n", m->lib.error_string(e));
+                    (void)m->lib.group_end();
+                    return RT_ERR_HIP;
+                }
+            }
+            ncclResult_t e = m->lib.group_end();
+            if (e != ncclSuccess) {
+                std::fprintf(stderr, "rt_multi.cpp: ncclGroupEnd: %s\n", m->lib.error_string(e));
+                return RT_ERR_HIP;
+            }
+        } else {  // every rank on one device: device copies
+            for (uint32_t r = 0; r < world; r++) {
+                MHIP(hipSetDevice(m->devices[r]));
+                MHIP(hipEventRecord(m->done[r], m->streams[r]));
+            }
+            MHIP(hipSetDevice(m->devices[0]));
+            for (uint32_t r = 0; r < world; r++) {
+                MHIP(hipStreamWaitEvent(s0, m->done[r], 0));
+                MHIP(hipMemcpyAsync(m->gathered + r * bf, m->band[r], bf * sizeof(float), hipMemcpyDeviceToDevice,
+                                    s0));
+                if (rgb8)
+                    MHIP(hipMemcpyAsync(m->gathered8 + r * bf, m->band8[r], bf, hipMemcpyDeviceToDevice, s0));
+            }
+        }
+        MHIP(hipSetDevice(m->devices[0]));
+        st = rt_unpermute_bands_async(m->gathered, cam->x_res, cam->y_res, band_rows, world, m->frame, s0);
+        if (st != RT_OK) return st;
+        if (rgb8) {
+            st = rt_unpermute_bands_u8_async(m->gathered8, cam->x_res, cam->y_res, band_rows, world, m->frame8, s0);
+            if (st != RT_OK) return st;
+        }
+        MHIP(hipEventRecord(m->ev1, s0));
+        MHIP(hipStreamSynchronize(s0));
+        // a rank whose ray queues overflowed re-renders with a grown pool (rt_scene_sync_status)
+        bool overflow = false;
+        for (uint32_t r = 0; r < world; r++) {
+            st = rt_scene_sync_status(m->ranks[r]);
+            if (st == RT_ERR_CAPACITY)
+                overflow = true;
+            else if (st != RT_OK)
+                return st;
+        }
+        if (!overflow) break;
+        if (attempt >= 8) return RT_ERR_CAPACITY;
+    }
+    MHIP(hipSetDevice(m->devices[0]));
+    MHIP(hipMemcpyAsync(rgb, m->frame, ff * sizeof(float), hipMemcpyDeviceToHost, s0));
+    if (rgb8) MHIP(hipMemcpyAsync(rgb8, m->frame8, ff, hipMemcpyDeviceToHost, s0));
+    MHIP(hipStreamSynchronize(s0));
+    if (opts && opts->counters) {
+        rt_counters c{0, 0, 0, 0};
+        for (uint32_t r = 0; r < world; r++) {
+            unsigned long long h[3] = {0, 0, 0};
+            MHIP(hipSetDevice(m->devices[r]));
+            MHIP(hipMemcpy(h, m->counters[r], sizeof(h), hipMemcpyDeviceToHost));
+            c.node_rays += h[0];
+            c.shadow_rays += h[1];
+            c.pixels += h[2];
+        }
+        *opts->counters = c;
+    }
+    if (opts && opts->kernel_ms) {
+        float ms = 0.f;
+        MHIP(hipSetDevice(m->devices[0]));
+        MHIP(hipEventElapsedTime(&ms, m->ev0, m->ev1));
+        *opts->kernel_ms = ms;
+    }
+    MHIP(hipSetDevice(m->devices[0]));
+    return RT_OK;
+}
+
+extern "C" {
+
+rt_status rt_scene_create_multi(const rt_scene_desc* desc, const int32_t* devices, uint32_t n_devices,
+                                rt_scene** out) {
+    if (!desc || !devices || !out || n_devices == 0) return RT_ERR_INVALID_ARG;
+    int n_visible = 0;
+    if (hipGetDeviceCount(&n_visible) != hipSuccess || n_visible <= 0) return RT_ERR_NO_DEVICE;
+    for (uint32_t r = 0; r < n_devices; r++)
+        if (devices[r] < 0 || devices[r] >= n_visible) return RT_ERR_INVALID_ARG;
+    rt_scene* s0 = nullptr;
+    rt_status st = rt_scene_create(desc, devices[0], &s0);
+    if (st != RT_OK || n_devices == 1) {
+        *out = s0;
+        return st;
+    }
+    rt_multi_state* m = new (std::nothrow) rt_multi_state();
+    if (!m) {
+        rt_scene_destroy(s0);
+        return RT_ERR_OUT_OF_MEMORY;
+    }
+    rt_scene_multi(s0) = m;  // rt_scene_destroy(s0) frees m from here on
+    m->devices.assign(devices, devices + n_devices);
+    m->ranks.assign(n_devices, nullptr);
+    m->ranks[0] = s0;
+    m->streams.assign(n_devices, nullptr);
+    m->done.assign(n_devices, nullptr);
+    m->band.assign(n_devices, nullptr);
+    m->band8.assign(n_devices, nullptr);
+    m->counters.assign(n_devices, nullptr);
+    auto fail = [&](rt_status e) {
+        rt_scene_destroy(s0);
+        return e;
+    };
+    for (uint32_t r = 0; r < n_devices; r++) {
+        if (r > 0 && (st = rt_scene_clone(s0, devices[r], &m->ranks[r])) != RT_OK) return fail(st);
+        if (hipSetDevice(devices[r]) != hipSuccess ||
+            hipStreamCreateWithFlags(&m->streams[r], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&m->done[r], hipEventDisableTiming) != hipSuccess ||
+            hipMalloc(&m->counters[r], 3 * sizeof(unsigned long long)) != hipSuccess)
+            return fail(RT_ERR_HIP);
+    }
+    if (hipSetDevice(devices[0]) != hipSuccess || hipEventCreate(&m->ev0) != hipSuccess ||
+        hipEventCreate(&m->ev1) != hipSuccess)
+        return fail(RT_ERR_HIP);
+    std::vector<int> sorted(m->devices);
+    std::sort(sorted.begin(), sorted.end());
+    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    if (distinct) {
+        if (!load_rccl(m->lib)) {
+            std::fprintf(stderr, "rt_multi.cpp: librccl.so.1 not loadable: %s\n", dlerror());
+            return fail(RT_ERR_UNSUPPORTED);
+        }
+        m->comms.assign(n_devices, nullptr);
+        ncclResult_t e = m->lib.init_all(m->comms.data(), (int)n_devices, m->devices.data());
+        if (e != ncclSuccess) {
+            std::fprintf(stderr, "rt_multi.cpp: ncclCommInitAll: %s\n", m->lib.error_string(e));
+            m->comms.clear();
+            return fail(RT_ERR_HIP);
+        }
+        m->rccl = true;
+    }
+    (void)hipSetDevice(devices[0]);
+    *out = s0;
+    return RT_OK;
+}
+
+int32_t rt_scene_device_count(const rt_scene* s) {
+    if (!s) return 0;
+    rt_multi_state* m = rt_scene_multi(const_cast<rt_scene*>(s));
+    return m ? (int32_t)m->ranks.size() : 1;
+}
+
+int32_t rt_scene_uses_rccl(const rt_scene* s) {
+    if (!s) return 0;
+    rt_multi_state* m = rt_scene_multi(const_cast<rt_scene*>(s));
+    return (m && m->rccl) ? 1 : 0;
+}
+
+}  // extern "C"

@@ -29,20 +29,7 @@
 
 namespace rtdev {
 
-enum : uint32_t { NODE_HIT = 1u << 8, NODE_MISS = 1u << 9, NODE_NONE = 1u << 10 };
-
 #define RT_SHADOW_COUNT(P) ((P).levels[2 * (RT_MAX_DEPTH + 1)])
-
-// chunk `c` of node n (NodeRec layout, rt_device.hpp)
-__device__ __forceinline__ float4* node_c(NodeRec* nodes, uint32_t n, int c) {
-    return reinterpret_cast<float4*>(nodes) + ((((size_t)(n >> 6) * NC_CHUNKS + (size_t)c) << 6) + (n & 63u));
-}
-__device__ __forceinline__ const float4* node_c(const NodeRec* nodes, uint32_t n, int c) {
-    return reinterpret_cast<const float4*>(nodes) + ((((size_t)(n >> 6) * NC_CHUNKS + (size_t)c) << 6) + (n & 63u));
-}
-__device__ __forceinline__ void node_flags(NodeRec* nodes, uint32_t n, uint32_t f) {
-    node_c(nodes, n, NC_AMB)->w = __uint_as_float(f);
-}
 
 struct PixelRef {
     bool valid;
@@ -365,13 +352,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 const uint32_t fr = P.frames > 1 ? t / P.frame_items : 0u;
                 PixelRef px = pixel_of(P, t - fr * P.frame_items);
                 if (!px.valid) {
-                    node_flags(P.nodes, n, NODE_NONE);
+                    P.node_flags[n] = NODE_NONE;
                     active = false;
                 } else {
                     n_pix++;
                     pix = px.v * P.width + px.u;
                     if (P.depth == 0) {  // trace_ray(.., 0) == BLACK, no scan
-                        node_flags(P.nodes, n, NODE_MISS);
+                        P.node_flags[n] = NODE_MISS;
                         active = false;
                     } else {
                         float fu = (float)px.u, fv = (float)px.v;
@@ -399,6 +386,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
             }
         }
         bool want_refl = false, want_refr = false, hit = false;
+        uint32_t hit_flags = 0;  // node_flags of a hit, F_HAS_R / F_HAS_T added once queued
         uint32_t decided = 0;  // point lights whose shadow ray the own-shape test settled
         uint32_t mort = 0;  // Morton code of the shadow-ray origin (queue ordering key)
         V3 rro = v3(0, 0, 0), rrd = v3(0, 0, 0), tro = v3(0, 0, 0), trd = v3(0, 0, 0);
@@ -419,7 +407,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
             uint32_t bk;
             scan<LDS>(S, ro, rd, bt, bk, cnt, lnodes);
             if (bk == 0xFFFFFFFFu) {
-                node_flags(P.nodes, n, NODE_MISS);  // trace_ray -> BLACK; the parent slot stays 0
+                // trace_ray -> BLACK: the parent's child slot gets BLACK (forest: direction 0)
+                P.node_flags[n] = NODE_MISS;
+                if (level > 0) {
+                    P.node_ec[parent] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (P.node_dc) P.node_dc[parent] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
             } else {
                 hit = true;
                 const MatRec& M = S.mats[S.shapes[bk >> 4].mat];
@@ -427,9 +420,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 float ri = M.refraction_index;
                 float n1 = h.entering ? 1.f : ri;
                 float n2 = h.entering ? ri : 1.f;
-                V3 ka = tex_eval(M.ambient, h.tu, h.tv);
-                V3 kd = tex_eval(M.diffuse, h.tu, h.tv);
-                V3 ks = tex_eval(M.specular, h.tu, h.tv);
                 V3 ps = add(h.p, mul(h.n, 0.0002f));  // render.rs:147
                 if (P.shadow_keys)
                     mort = P.shadow_fine == 21u ? morton21(S, ps) : (P.shadow_fine ? morton18(S, ps) : morton15(S, ps));
@@ -441,9 +431,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                     if (level == 0) atomicAdd(&rt_scan_stats[13 + (out ? 1 : 0)], 1ull);
                 }
 #endif
-                uint32_t flags = NODE_HIT;
-                float fr = 0.f, dr = 0.f, pw = 0.f, ft = 0.f;
-                P.node_ps[n] = make_float4(ps.x, ps.y, ps.z, 0.f);
                 // PointLight::get_energy (mod.rs:189-206) decided here when the planes and
                 // the shape just hit settle it: a plane's t < 0 is the nearest hit; else any
                 // hit nearer than the light means the nearest one is too (shadow_scan)
@@ -451,69 +438,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 sh_n = h.n;
                 sh_entering = h.entering;
                 sh_key = bk;
-                if (P.node_aux) {  // ray forest: what render_ray_tree re-reads at shade time
-                    P.node_aux[n] = make_float4(__uint_as_float((uint32_t)h.mat), h.tu, h.tv,
-                                                __uint_as_float(h.entering ? 1u : 0u));
+                if (P.node_dc) {  // ray forest: the shape id as the reference records it, the pixel
                     uint32_t shape = bk >> 4;
                     P.node_key[n] = (S.shapes[shape].kind == RT_SHAPE_CUBE) ? (bk & 15u) : shape;
                     P.node_pixel[n] = pix;
                 }
-                bool child_ok = level + 1 < P.depth;
-                if (M.reflectivity > RT_EPS) {  // render.rs:70-84, reflect_ray :105-110
-                    flags |= F_REFL;
-                    V3 rv = sub(mul(h.n, 2.f * dot(rd, h.n)), rd);
-                    rrd = neg(norm(rv));
+                const bool child_ok = level + 1 < P.depth;
+                if (M.reflectivity > RT_EPS && child_ok) {  // render.rs:70-84, reflect_ray :105-110
+                    rrd = reflect_dir(rd, h.n);
                     rro = add(h.p, mul(rrd, 0.0002f));
-                    fr = fresnel_reflection(rrd, h.n, n1, n2);
-                    dr = dot(rrd, h.n);
-                    V3 hv = norm(add(norm(h.eye), norm(rrd)));
-                    float mh = dot(h.n, hv);
-                    if (!(mh < 0.f)) {
-                        flags |= F_SPEC;
-                        pw = powf(mh, M.power);
-                    }
-                    want_refl = child_ok;
+                    want_refl = true;
                 }
-                if (ri > RT_EPS) {  // render.rs:86-98, refract_ray :112-125
-                    flags |= F_REFR;
-                    float ratio = n1 / n2;
-                    float m_dot_r = -dot(rd, h.n);
-                    float cos2 = 1.f - ratio * ratio * (1.f - m_dot_r * m_dot_r);
-                    if (cos2 > 0.f) {
-                        float ct = sqrtf(cos2);
-                        trd = add(mul(rd, ratio), mul(h.n, ratio * m_dot_r - ct));
-                        tro = add(h.p, mul(trd, 0.0002f));
-                        ft = 1.f - fresnel_reflection(trd, neg(h.n), n1, n2);
-                        want_refr = child_ok;
-                    } else {
-                        flags |= F_TIR;
-                    }
+                if (ri > RT_EPS && child_ok && refract_dir(rd, h.n, n1, n2, trd)) {  // render.rs:86-98, :112-125
+                    tro = add(h.p, mul(trd, 0.0002f));
+                    want_refr = true;
                 }
-                if (P.node_aux) {  // children's directions arrive here (0: no / missed child)
-                    kd = v3(0.f, 0.f, 0.f);
-                    ks = v3(0.f, 0.f, 0.f);
-                }
-                *node_c(P.nodes, n, NC_AMB) = make_float4(ka.x * S.amb_r, ka.y * S.amb_g, ka.z * S.amb_b,
-                                                          __uint_as_float(flags));
-                *node_c(P.nodes, n, NC_N) = make_float4(h.n.x, h.n.y, h.n.z, __uint_as_float(parent));
-                *node_c(P.nodes, n, NC_EYE) = make_float4(h.eye.x, h.eye.y, h.eye.z, M.power);
-                *node_c(P.nodes, n, NC_KD) = make_float4(kd.x, kd.y, kd.z, n1);
-                *node_c(P.nodes, n, NC_KS) = make_float4(ks.x, ks.y, ks.z, n2);
-                *node_c(P.nodes, n, NC_W) = make_float4(fr, dr, pw, ft);
-                *node_c(P.nodes, n, NC_ER) = make_float4(0.f, 0.f, 0.f, 0.f);
-                *node_c(P.nodes, n, NC_ET) = make_float4(0.f, 0.f, 0.f, 0.f);
+                // the node record: what the combine pass cannot re-derive (rt_device.hpp)
+                hit_flags = NODE_HIT | (h.entering ? F_ENTER : 0u) | ((uint32_t)h.mat << F_MAT_SHIFT);
+                P.node_ps[n] = make_float4(ps.x, ps.y, ps.z, h.tu);
+                P.node_n[n] = make_float4(h.n.x, h.n.y, h.n.z, h.tv);
+                P.node_d[n] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(parent));
             }
         }
         // ---- children -> level k+1 queue
         uint32_t nc = (want_refl ? 1u : 0u) + (want_refr ? 1u : 0u);
         uint32_t my = wave_append(&P.levels[2 * (level + 1) + 1], nc, lane);
+        const uint32_t fkey = P.frames > 1 ? ((pix >> RT_FRAME_SHIFT) << P.task_frame_shift) : 0u;
         if (want_refl) {
             uint32_t slot = next_off + my;
             if (slot < P.capacity) {
                 Task T = {rro.x, rro.y, rro.z, rrd.x, rrd.y, rrd.z, (n << 1) | 0u, pix};
                 P.tasks[slot] = T;
-                if (P.task_keys)
-                    P.task_keys[slot] = task_key(P, rro, rrd) | ((pix >> RT_FRAME_SHIFT) << P.task_frame_shift);
+                if (P.task_keys) P.task_keys[slot] = task_key(P, rro, rrd) | fkey;
+                hit_flags |= F_HAS_R;
             } else {
                 atomicOr(P.overflow, 1u);
             }
@@ -524,12 +481,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
             if (slot < P.capacity) {
                 Task T = {tro.x, tro.y, tro.z, trd.x, trd.y, trd.z, (n << 1) | 1u, pix};
                 P.tasks[slot] = T;
-                if (P.task_keys)
-                    P.task_keys[slot] = task_key(P, tro, trd) | ((pix >> RT_FRAME_SHIFT) << P.task_frame_shift);
+                if (P.task_keys) P.task_keys[slot] = task_key(P, tro, trd) | fkey;
+                hit_flags |= F_HAS_T;
             } else {
                 atomicOr(P.overflow, 1u);
             }
         }
+        if (hit) P.node_flags[n] = hit_flags;
         // ---- shadow rays the own shape decides, and (levels < inline_levels) the rest:
         // after the node record and the children are out, so that little stays live
         // across the shadow scans
@@ -600,11 +558,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 group += (uint32_t)__builtin_popcountll(m);
                 if (want) {
                     if (slot < P.shadow_capacity) {
-                        P.shadow[slot] = (n << 5) | (uint32_t)li;
+                        P.shadow[slot] = (n << P.light_bits) | (uint32_t)li;
                         if (P.shadow_keys)
                             P.shadow_keys[slot] = (P.shadow_fine ? (((uint32_t)li << P.shadow_fine) | mort)
                                                                    : ((uint32_t)li << P.light_shift) | (mort >> (15u - P.light_shift)))
-                                                  | ((pix >> RT_FRAME_SHIFT) << P.shadow_frame_shift);
+                                                  | (P.frames > 1 ? ((pix >> RT_FRAME_SHIFT) << P.shadow_frame_shift) : 0u);
                     } else
                         atomicOr(P.overflow, 2u);
                 }
@@ -657,7 +615,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
         const uint32_t t = base + lane;
         if (t < count) {
             uint32_t e = P.shadow_in[t];
-            uint32_t n = e >> 5, li = e & 31u;
+            uint32_t n = e >> P.light_bits, li = e & ((1u << P.light_bits) - 1u);
             const float4 q = P.node_ps[n];
             V3 ps = v3(q.x, q.y, q.z);
             const LightRec& L = S.lights[li];
@@ -675,84 +633,135 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
     bc_flush(ops_slot(S), P.ray_counters);
 }
 
+// The stored part of a hit node (rt_device.hpp) and what the shading passes derive from it:
+// eye_dir = -norm(ray direction) (the Intersection's eye_dir, sphere.rs:81 etc.), n1 / n2
+// from `entering` (render.rs:51-55), the material's textures at (u, v).
+struct NodeIn {
+    Hit h;
+    V3 ps, rd;
+    float n1, n2;
+    uint32_t parent;
+};
+__device__ __forceinline__ NodeIn node_in(const WaveParams& P, uint32_t n, uint32_t flags, const MatRec& M) {
+    NodeIn q;
+    const float4 a = P.node_ps[n], b = P.node_n[n], c = P.node_d[n];
+    q.ps = xyz(a);
+    q.h.n = xyz(b);
+    q.rd = xyz(c);
+    q.h.tu = a.w;
+    q.h.tv = b.w;
+    q.parent = __float_as_uint(c.w);
+    q.h.eye = neg(norm(q.rd));
+    const bool entering = (flags & F_ENTER) != 0u;
+    const float ri = M.refraction_index;
+    q.n1 = entering ? 1.f : ri;
+    q.n2 = entering ? ri : 1.f;
+    return q;
+}
+
+// sum over the lights of fresnel(ldir) * get_reflected_energy(E, ldir) (render.rs:59-68,
+// get_light_energy :142-153), the shadow decisions taken from `litmask`; Sum starts at
+// BLACK (color.rs:164-167)
+__device__ __forceinline__ V3 light_sum(const DevScene& S, const NodeIn& q, uint32_t litmask, V3 kd, V3 ks,
+                                        float power) {
+    V3 lsum = v3(0.f, 0.f, 0.f);
+    for (int li = 0; li < S.n_lights; ++li) {
+        const LightRec& L = S.lights[li];
+        V3 ldir = v3(0.f, 0.f, 0.f);
+        V3 E = v3(L.r, L.g, L.b);
+        if (L.kind == RT_LIGHT_POINT) {
+            ldir = norm(sub(v3(L.px, L.py, L.pz), q.ps));
+            if (!((litmask >> li) & 1u)) E = v3(0.f, 0.f, 0.f);
+        }
+        float f = fresnel_reflection(ldir, q.h.n, q.n1, q.n2);
+        V3 g = reflected_energy(E, ldir, q.h, kd, ks, power);
+        lsum = add(lsum, v3(f * g.x, f * g.y, f * g.z));
+    }
+    return lsum;
+}
+
 // render.rs:57-68 + :100 for every node of `level`; children (level + 1) already reported.
 __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32_t level) {
     const DevScene& S = P.S;
     const uint32_t off = P.levels[2 * level];
     const uint32_t count = min(P.levels[2 * level + 1], off < P.capacity ? P.capacity - off : 0u);
     const uint32_t stride = gridDim.x * blockDim.x;
+    // the last launch of a pass: latch this pass's queue overflows into the sticky word
+    // rt_scene_sync_status reads (every producer of the pass ran before this launch)
+    if (level == 0 && blockIdx.x == 0 && threadIdx.x == 0 && P.overflow_sticky && *P.overflow)
+        atomicOr(P.overflow_sticky, *P.overflow);
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < count; t += stride) {
         const uint32_t n = off + t;
-        const float4 c0 = *node_c(P.nodes, n, NC_AMB);
-        const uint32_t flags = __float_as_uint(c0.w);
+        const uint32_t flags = P.node_flags[n];
         // frame batches: level-0 node t belongs to frame t / frame_items
         const uint32_t fr = (level == 0 && P.frames > 1) ? t / P.frame_items : 0u;
-        float* const out = P.out + (size_t)fr * P.frame_floats;
         if (flags & NODE_NONE) {  // padding of the band buffer: defined as 0
             PixelRef px = pixel_of(P, t - fr * P.frame_items);
             if (level == 0 && px.u < P.width && px.lr < P.rows_local) {
-                float* o = out + ((size_t)px.lr * P.width + px.u) * 3u;
-                o[0] = 0.f;
-                o[1] = 0.f;
-                o[2] = 0.f;
+                const size_t i = (size_t)px.lr * P.width + px.u;
+                if (P.out) {
+                    float* o = P.out + (size_t)fr * P.frame_floats + i * 3u;
+                    o[0] = 0.f;
+                    o[1] = 0.f;
+                    o[2] = 0.f;
+                }
+                if (P.out8) {
+                    uint8_t* o8 = P.out8 + (size_t)fr * P.frame_floats + i * 3u;
+                    o8[0] = o8[1] = o8[2] = 0;
+                }
             }
             continue;
         }
         V3 c = v3(0.f, 0.f, 0.f);
         uint32_t parent = 0;
         if (flags & NODE_HIT) {
-            const float4 cn = *node_c(P.nodes, n, NC_N), ce = *node_c(P.nodes, n, NC_EYE);
-            const float4 ckd = *node_c(P.nodes, n, NC_KD), cks = *node_c(P.nodes, n, NC_KS);
-            const float4 cw = *node_c(P.nodes, n, NC_W);
-            const float4 cer = *node_c(P.nodes, n, NC_ER), cet = *node_c(P.nodes, n, NC_ET);
-            const float4 q = P.node_ps[n];
-            parent = __float_as_uint(cn.w);
-            Hit h;
-            h.n = v3(cn.x, cn.y, cn.z);
-            h.eye = v3(ce.x, ce.y, ce.z);
-            const float power = ce.w, n1 = ckd.w, n2 = cks.w;
-            V3 ps = v3(q.x, q.y, q.z);
-            V3 kd = v3(ckd.x, ckd.y, ckd.z), ks = v3(cks.x, cks.y, cks.z);
-            V3 lsum = v3(0.f, 0.f, 0.f);  // Sum starts at BLACK (color.rs:164-167)
-            const uint32_t litmask = P.node_lit[n];
-            for (int li = 0; li < S.n_lights; ++li) {
-                const LightRec& L = S.lights[li];
-                V3 ldir = v3(0.f, 0.f, 0.f);
-                V3 E = v3(L.r, L.g, L.b);
-                if (L.kind == RT_LIGHT_POINT) {
-                    ldir = norm(sub(v3(L.px, L.py, L.pz), ps));
-                    if (!((litmask >> li) & 1u)) E = v3(0.f, 0.f, 0.f);
-                }
-                float f = fresnel_reflection(ldir, h.n, n1, n2);
-                V3 g = reflected_energy(E, ldir, h, kd, ks, power);
-                lsum = add(lsum, v3(f * g.x, f * g.y, f * g.z));
-            }
-            V3 loc = add(v3(c0.x, c0.y, c0.z), lsum);
+            const MatRec& M = S.mats[flags >> F_MAT_SHIFT];
+            const NodeIn q = node_in(P, n, flags, M);
+            parent = q.parent;
+            const V3 ka = tex_eval(M.ambient, q.h.tu, q.h.tv);
+            const V3 kd = tex_eval(M.diffuse, q.h.tu, q.h.tv);
+            const V3 ks = tex_eval(M.specular, q.h.tu, q.h.tv);
+            const V3 lsum = light_sum(S, q, P.node_lit[n], kd, ks, M.power);
+            // ambient = mat.ambient(tex) * scene.ambient (render.rs:57), then + lights
+            const V3 loc = add(v3(ka.x * S.amb_r, ka.y * S.amb_g, ka.z * S.amb_b), lsum);
             Frame f;
+            node_weights(M, q.rd, q.h.n, q.h.eye, q.n1, q.n2, f);
             f.ax = loc.x; f.ay = loc.y; f.az = loc.z;
-            f.fr = cw.x; f.dr = cw.y; f.pw = cw.z; f.ft = cw.w;
             f.kdx = kd.x; f.kdy = kd.y; f.kdz = kd.z;
             f.ksx = ks.x; f.ksy = ks.y; f.ksz = ks.z;
-            f.flags = flags;
-            c = combine(f, v3(cer.x, cer.y, cer.z), v3(cet.x, cet.y, cet.z));
+            // a child that was never queued (depth limit: trace_ray(.., 0)) reports BLACK
+            const float4 er = (flags & F_HAS_R) ? P.node_ec[2u * n] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 et = (flags & F_HAS_T) ? P.node_ec[2u * n + 1u] : make_float4(0.f, 0.f, 0.f, 0.f);
+            c = combine(f, xyz(er), xyz(et));
         } else if (level > 0) {
-            continue;  // a missed child reports BLACK: the parent's slot already holds 0
+            continue;  // a missed child: the trace pass wrote BLACK to its parent's slot
         }
         if (level == 0) {
             PixelRef px = pixel_of(P, t - fr * P.frame_items);
-            float* o = out + ((size_t)px.lr * P.width + px.u) * 3u;
-            if (P.spp > 1) {  // the f32 sum of the samples in sample order, then / spp
-                if (P.sample > 0) c = v3(o[0] + c.x, o[1] + c.y, o[2] + c.z);
-                if (P.sample + 1 == P.spp) {
-                    const float fs = (float)P.spp;
-                    c = v3(c.x / fs, c.y / fs, c.z / fs);
+            const size_t i = (size_t)px.lr * P.width + px.u;
+            bool last = true;
+            if (P.out) {  // (null: an RGB8-only pass, spp == 1)
+                float* o = P.out + (size_t)fr * P.frame_floats + i * 3u;
+                if (P.spp > 1) {  // the f32 sum of the samples in sample order, then / spp
+                    if (P.sample > 0) c = v3(o[0] + c.x, o[1] + c.y, o[2] + c.z);
+                    last = P.sample + 1 == P.spp;
+                    if (last) {
+                        const float fs = (float)P.spp;
+                        c = v3(c.x / fs, c.y / fs, c.z / fs);
+                    }
                 }
+                o[0] = c.x;
+                o[1] = c.y;
+                o[2] = c.z;
             }
-            o[0] = c.x;
-            o[1] = c.y;
-            o[2] = c.z;
+            if (P.out8 && last) {  // Color::as_u8 (color.rs:43-46) fused into the epilogue
+                uint8_t* o8 = P.out8 + (size_t)fr * P.frame_floats + i * 3u;
+                o8[0] = as_u8(c.x);
+                o8[1] = as_u8(c.y);
+                o8[2] = as_u8(c.z);
+            }
         } else {
-            *node_c(P.nodes, parent >> 1, (parent & 1u) ? NC_ET : NC_ER) = make_float4(c.x, c.y, c.z, 0.f);
+            P.node_ec[parent] = make_float4(c.x, c.y, c.z, 0.f);
         }
     }
 }
@@ -766,7 +775,7 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
 //   reflected     fresnel(dir_r) * reflected_energy(E_r, eye_dir)   -- eye_dir as light dir
 //   refracted     (1 - fresnel(dir_t, -n)) * E_t                     -- no diffuse factor
 //   colour        ((ambient + lights) + reflected) + refracted, reported with dir = -eye_dir
-// (E, dir) of a missing or missed child = (BLACK, 0): its slots were zeroed at build time.
+// (E, dir) of a missing child = (BLACK, 0); a missed child wrote (BLACK, 0) at build time.
 // dirty != null: only nodes of marked pixels are shaded (render_forest_filter).
 __global__ __launch_bounds__(256) void forest_shade_level_kernel(WaveParams P, uint32_t level, float* frame) {
     const DevScene& S = P.S;
@@ -775,7 +784,7 @@ __global__ __launch_bounds__(256) void forest_shade_level_kernel(WaveParams P, u
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < count; t += stride) {
         const uint32_t n = off + t;
-        const uint32_t flags = __float_as_uint(node_c(P.nodes, n, NC_AMB)->w);
+        const uint32_t flags = P.node_flags[n];
         if (flags & NODE_NONE) continue;
         if (!(flags & NODE_HIT)) {  // RayTreeNode::None: (BLACK, 0)
             if (level == 0) {
@@ -792,46 +801,20 @@ __global__ __launch_bounds__(256) void forest_shade_level_kernel(WaveParams P, u
         }
         const uint32_t pix = P.node_pixel[n];
         if (P.dirty && !P.dirty[pix]) continue;
-        const float4 aux = P.node_aux[n];
-        const MatRec& M = S.mats[__float_as_uint(aux.x)];
-        const float4 cn = *node_c(P.nodes, n, NC_N), ce = *node_c(P.nodes, n, NC_EYE);
-        const float4 ckd = *node_c(P.nodes, n, NC_KD), cks = *node_c(P.nodes, n, NC_KS);
-        const float4 cer = *node_c(P.nodes, n, NC_ER), cet = *node_c(P.nodes, n, NC_ET);
-        const float4 q = P.node_ps[n];
-        const uint32_t parent = __float_as_uint(cn.w);
-        Hit h;
-        h.n = v3(cn.x, cn.y, cn.z);
-        h.eye = v3(ce.x, ce.y, ce.z);
-        h.tu = aux.y;
-        h.tv = aux.z;
-        const bool entering = __float_as_uint(aux.w) != 0u;
-        const float ri = M.refraction_index;
-        const float n1 = entering ? 1.f : ri;
-        const float n2 = entering ? ri : 1.f;
-        const V3 kd = tex_eval(M.diffuse, h.tu, h.tv), ks = tex_eval(M.specular, h.tu, h.tv);
-        V3 ps = v3(q.x, q.y, q.z);
-        V3 lsum = v3(0.f, 0.f, 0.f);
-        const uint32_t litmask = P.node_lit[n];
-        for (int li = 0; li < S.n_lights; ++li) {
-            const LightRec& L = S.lights[li];
-            V3 ldir = v3(0.f, 0.f, 0.f);
-            V3 E = v3(L.r, L.g, L.b);
-            if (L.kind == RT_LIGHT_POINT) {
-                ldir = norm(sub(v3(L.px, L.py, L.pz), ps));
-                if (!((litmask >> li) & 1u)) E = v3(0.f, 0.f, 0.f);
-            }
-            float f = fresnel_reflection(ldir, h.n, n1, n2);
-            V3 g = reflected_energy(E, ldir, h, kd, ks, M.power);
-            lsum = add(lsum, v3(f * g.x, f * g.y, f * g.z));
-        }
-        const V3 er = v3(cer.x, cer.y, cer.z), dr = v3(ckd.x, ckd.y, ckd.z);
-        const V3 et = v3(cet.x, cet.y, cet.z), dt = v3(cks.x, cks.y, cks.z);
-        float fr = fresnel_reflection(dr, h.n, n1, n2);
-        V3 gr = reflected_energy(er, h.eye, h, kd, ks, M.power);
+        const MatRec& M = S.mats[flags >> F_MAT_SHIFT];
+        const NodeIn q = node_in(P, n, flags, M);
+        const V3 kd = tex_eval(M.diffuse, q.h.tu, q.h.tv), ks = tex_eval(M.specular, q.h.tu, q.h.tv);
+        const V3 lsum = light_sum(S, q, P.node_lit[n], kd, ks, M.power);
+        const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool has_r = (flags & F_HAS_R) != 0u, has_t = (flags & F_HAS_T) != 0u;
+        const V3 er = xyz(has_r ? P.node_ec[2u * n] : zero), dr = xyz(has_r ? P.node_dc[2u * n] : zero);
+        const V3 et = xyz(has_t ? P.node_ec[2u * n + 1u] : zero), dt = xyz(has_t ? P.node_dc[2u * n + 1u] : zero);
+        float fr = fresnel_reflection(dr, q.h.n, q.n1, q.n2);
+        V3 gr = reflected_energy(er, q.h.eye, q.h, kd, ks, M.power);
         V3 refl = v3(fr * gr.x, fr * gr.y, fr * gr.z);
-        float ft = 1.f - fresnel_reflection(dt, neg(h.n), n1, n2);
+        float ft = 1.f - fresnel_reflection(dt, neg(q.h.n), q.n1, q.n2);
         V3 refr = v3(ft * et.x, ft * et.y, ft * et.z);
-        V3 ka = tex_eval(M.ambient, h.tu, h.tv);
+        V3 ka = tex_eval(M.ambient, q.h.tu, q.h.tv);
         V3 amb = v3(ka.x * S.amb_r, ka.y * S.amb_g, ka.z * S.amb_b);
         V3 c = add(add(add(amb, lsum), refl), refr);
         if (level == 0) {
@@ -839,11 +822,10 @@ __global__ __launch_bounds__(256) void forest_shade_level_kernel(WaveParams P, u
             o[0] = c.x;
             o[1] = c.y;
             o[2] = c.z;
-        } else {  // the parent's slot: colour, and the direction in its kd / ks chunk (n1 / n2 unused here)
-            const V3 d = neg(h.eye);
-            const bool refr = (parent & 1u) != 0;
-            *node_c(P.nodes, parent >> 1, refr ? NC_ET : NC_ER) = make_float4(c.x, c.y, c.z, 0.f);
-            *node_c(P.nodes, parent >> 1, refr ? NC_KS : NC_KD) = make_float4(d.x, d.y, d.z, 0.f);
+        } else {  // the parent's slot: colour and the direction -eye_dir (render_tree.rs:252)
+            const V3 d = neg(q.h.eye);
+            P.node_ec[q.parent] = make_float4(c.x, c.y, c.z, 0.f);
+            P.node_dc[q.parent] = make_float4(d.x, d.y, d.z, 0.f);
         }
     }
 }
@@ -851,11 +833,11 @@ __global__ __launch_bounds__(256) void forest_shade_level_kernel(WaveParams P, u
 // mark[pixel] = 1 for every pixel whose tree holds a node with key_mask[id] set
 // (render_forest_filter's shapes ∩ mutated, render_tree.rs:138-140); also counts the
 // hit nodes per pixel when sizes != null (RayTree::size, :39-48)
-__global__ void forest_mark_kernel(const uint32_t* node_key, const uint32_t* node_pixel, const NodeRec* nodes,
+__global__ void forest_mark_kernel(const uint32_t* node_key, const uint32_t* node_pixel, const uint32_t* node_flags,
                                    uint32_t n_nodes, const uint8_t* key_mask, uint32_t n_keys, uint8_t* mark,
                                    uint32_t* sizes) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_nodes; i += gridDim.x * blockDim.x) {
-        if (!(__float_as_uint(node_c(nodes, i, NC_AMB)->w) & NODE_HIT)) continue;
+        if (!(node_flags[i] & NODE_HIT)) continue;
         uint32_t pix = node_pixel[i];
         if (sizes) atomicAdd(&sizes[pix], 1u);
         if (key_mask) {
@@ -934,12 +916,12 @@ hipError_t launch_forest_shade(const WaveParams& p, uint32_t level, int blocks, 
     return hipGetLastError();
 }
 
-hipError_t launch_forest_mark(const uint32_t* node_key, const uint32_t* node_pixel, const NodeRec* nodes,
+hipError_t launch_forest_mark(const uint32_t* node_key, const uint32_t* node_pixel, const uint32_t* node_flags,
                               uint32_t n_nodes, const uint8_t* key_mask, uint32_t n_keys, uint8_t* mark,
                               uint32_t* sizes, hipStream_t stream) {
     if (n_nodes == 0) return hipSuccess;
     uint32_t blocks = std::min<uint32_t>((n_nodes + 255) / 256, 4096u);
-    hipLaunchKernelGGL(forest_mark_kernel, dim3(blocks), dim3(256), 0, stream, node_key, node_pixel, nodes, n_nodes,
+    hipLaunchKernelGGL(forest_mark_kernel, dim3(blocks), dim3(256), 0, stream, node_key, node_pixel, node_flags, n_nodes,
                        key_mask, n_keys, mark, sizes);
     return hipGetLastError();
 }

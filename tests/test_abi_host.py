@@ -128,3 +128,20 @@ def test_bands_partition_the_frame(h, band, world):
         assert len(rows) == rpr
         seen += [v for v in rows if v >= 0]
     assert sorted(seen) == list(range(h))
+
+
+def test_multi_device_scene_needs_devices():
+    """rt_scene_create_multi validates its device list; without a HIP device it reports
+    RT_ERR_NO_DEVICE like rt_scene_create (no CPU fallback)."""
+    from tests.conftest import gpu_available
+    L = abi.lib()
+    h = C.c_void_p()
+    desc = rt.SceneDesc.my_scene()
+    assert L.rt_scene_create_multi(desc.ptr(), None, 1, C.byref(h)) == 1  # RT_ERR_INVALID_ARG
+    devs = (C.c_int32 * 2)(0, 1)
+    assert L.rt_scene_create_multi(desc.ptr(), devs, 0, C.byref(h)) == 1
+    if not gpu_available():
+        assert L.rt_scene_create_multi(desc.ptr(), devs, 2, C.byref(h)) == 4  # RT_ERR_NO_DEVICE
+    assert L.rt_scene_device_count(None) == 0
+    assert L.rt_status_str(abi.RT_ERR_CAPACITY) == b"RT_ERR_CAPACITY"
+    assert L.rt_scene_sync_status(None) == 1

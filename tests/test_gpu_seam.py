@@ -1,0 +1,213 @@
+"""GPU tests of the drop-in seam beyond one device and one float frame:
+
+- multi-device scenes (rt_scene_create_multi): the frame tiled over ranks, gathered and
+  un-permuted, equals the one-device rt_render bit for bit -- with one device (the RCCL
+  communicator of one rank) and with one GPU listed 2 / 3 times (band shares exchanged by
+  device copies: the multi-rank band logic on a one-GPU box);
+- queue overflow is never a silent RT_OK: the stream-ordered entry points latch it and
+  rt_scene_sync_status raises RT_ERR_CAPACITY; rt_render grows its pool and renders the
+  full frame (render.rs:40-103 traces every ray);
+- Color::as_u8 fused into the level-0 combine (color.rs:43-46): RGB8 equals as_u8 of the
+  float frame on every path (rt_render, band renders, RGB8-only band renders, multi-device);
+- BASELINE config 4 (3840x2160, depth 8, 1 spp) against the oracle on sampled rows.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.oracle import OracleScene, as_u8
+from rust_tracer_amd import DeviceScene, RtError, SceneDesc, abi, band_rows_per_rank
+from rust_tracer_amd.dist import local_rows
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def same_bits(a, b):
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def compare(gpu, ref, tol=TOL):
+    diff = np.abs(gpu.astype(np.float64) - ref.astype(np.float64))
+    diff[np.isnan(gpu) & np.isnan(ref)] = 0.0
+    assert not np.isnan(diff).any(), "NaN in one image only"
+    assert float(diff.max()) <= tol
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_multi_device_scene_equals_single(devices):
+    """rt_scene_create_multi: same frame, counters and RGB8 as the one-device render."""
+    desc = SceneDesc.synth_config(3)
+    w, h, depth = 320, 180, 8
+    single = DeviceScene(desc, device=0)
+    ref, rcnt, _, ref8 = single.render(w, h, depth, want_u8=True)
+    single.close()
+    multi = DeviceScene(desc, devices=devices)
+    assert multi.device_count == len(devices)
+    # RCCL is used only when every listed device is distinct and there is more than one
+    assert not multi.uses_rccl
+    img, cnt, ms, img8 = multi.render(w, h, depth, want_u8=True)
+    img2, cnt2, _, _ = multi.render(w, h, depth)  # buffers reused
+    multi.close()
+    assert same_bits(img, ref) and same_bits(img2, ref)
+    assert np.array_equal(img8, ref8)
+    assert cnt == rcnt and cnt2 == rcnt
+    assert ms > 0
+
+
+def test_multi_device_ragged_and_spp():
+    """Frames whose rows do not fill the last bands, and jittered supersampling, tiled."""
+    desc = SceneDesc.my_scene()
+    single = DeviceScene(desc, device=0)
+    multi = DeviceScene(desc, devices=[0, 0, 0])
+    for (w, h, spp) in [(67, 45, 1), (8, 3, 1), (96, 61, 4)]:
+        ref, rcnt, _, _ = single.render(w, h, 6, spp=spp, seed=7)
+        img, cnt, _, _ = multi.render(w, h, 6, spp=spp, seed=7)
+        assert same_bits(img, ref), (w, h, spp)
+        assert cnt == rcnt
+    single.close()
+    multi.close()
+
+
+def test_scene_clone_renders_identically():
+    desc = SceneDesc.synth_config(2)
+    a = DeviceScene(desc, device=0)
+    b = a.clone(0)
+    ra, ca, _, _ = a.render(200, 120, 4)
+    rb, cb, _, _ = b.render(200, 120, 4)
+    assert same_bits(ra, rb) and ca == cb
+    b.close()
+    ra2, _, _, _ = a.render(200, 120, 4)  # the source outlives its clone
+    assert same_bits(ra, ra2)
+    a.close()
+
+
+def _band_render(scene, w, h, depth, rank, world, rgb=True, rgb8=False, band_rows=8):
+    dev = torch.device("cuda", 0)
+    rpr = band_rows_per_rank(h, band_rows, world)
+    out = torch.full((rpr, w, 3), -1.0, dtype=torch.float32, device=dev) if rgb else None
+    out8 = torch.zeros((rpr, w, 3), dtype=torch.uint8, device=dev) if rgb8 else None
+    cnt = torch.zeros(3, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    scene.render_bands_ex_async([abi.camera(w, h)], depth, band_rows, rank, world,
+                                out.data_ptr() if rgb else 0, out8.data_ptr() if rgb8 else 0, cnt.data_ptr(),
+                                stream)
+    torch.cuda.synchronize()
+    return (out.cpu().numpy() if rgb else None), (out8.cpu().numpy() if rgb8 else None), cnt.cpu().numpy()
+
+
+def test_overflow_is_reported_not_truncated(monkeypatch):
+    """A node pool far too small for the ray trees: the stream-ordered render still returns
+    RT_OK (it cannot know yet), rt_scene_sync_status then raises RT_ERR_CAPACITY; the next
+    pass gets a grown pool.  rt_render retries internally and returns the full frame."""
+    desc = SceneDesc.synth_config(3)
+    w, h, depth = 256, 144, 8
+    full = DeviceScene(desc, device=0)
+    ref, rcnt, _, _ = full.render(w, h, depth)
+    full.close()
+    monkeypatch.setenv("RT_NODE_CAP", str(w * h + 4096))  # level 0 plus a sliver
+    s = DeviceScene(desc, device=0)
+    _band_render(s, w, h, depth, 0, 1)
+    with pytest.raises(RtError) as e:
+        s.sync_status()
+    assert e.value.status == abi.RT_ERR_CAPACITY
+    s.sync_status()  # cleared once reported
+    # rt_render grows the pool until every ray fits
+    img, cnt, _, _ = s.render(w, h, depth)
+    assert same_bits(img, ref) and cnt == rcnt
+    s.close()
+    monkeypatch.delenv("RT_NODE_CAP")
+    s = DeviceScene(desc, device=0)
+    _band_render(s, w, h, depth, 0, 1)
+    s.sync_status()  # default pool: no overflow
+    s.close()
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_fused_rgb8_bands(world):
+    """RGB8 written by the level-0 combine equals as_u8 of the float bands; RGB8-only bands
+    (no float frame written) are the same bytes."""
+    desc = SceneDesc.my_scene()
+    w, h, depth = 130, 77, 8
+    s = DeviceScene(desc, device=0)
+    for rank in range(world):
+        f, b8, c = _band_render(s, w, h, depth, rank, world, rgb=True, rgb8=True)
+        assert np.array_equal(b8, as_u8(f))
+        _, only8, c2 = _band_render(s, w, h, depth, rank, world, rgb=False, rgb8=True)
+        assert np.array_equal(only8, b8)
+        assert np.array_equal(c, c2)
+    s.sync_status()
+    s.close()
+
+
+def test_u8_unpermute_matches_float_unpermute():
+    from rust_tracer_amd import unpermute_bands_async, unpermute_bands_u8_async
+    dev = torch.device("cuda", 0)
+    w, h, br, world = 37, 53, 8, 3
+    rpr = band_rows_per_rank(h, br, world)
+    g = torch.rand((world, rpr, w, 3), device=dev)
+    g8 = (g * 255).to(torch.uint8)
+    f = torch.zeros((h, w, 3), device=dev)
+    f8 = torch.zeros((h, w, 3), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    unpermute_bands_async(g.data_ptr(), w, h, br, world, f.data_ptr(), st)
+    unpermute_bands_u8_async(g8.data_ptr(), w, h, br, world, f8.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert torch.equal((f * 255).to(torch.uint8), f8)
+    for r in range(world):
+        for lr, v in enumerate(local_rows(h, br, r, world)):
+            if v >= 0:
+                assert torch.equal(f8[v], g8[r, lr])
+
+
+def test_config4_sampled_rows():
+    """BASELINE config 4: 3840x2160, depth 8, 1 spp, the config-3 scene; rows sampled across
+    the frame (every 270th) against the oracle, and the whole frame run-to-run identical."""
+    desc = SceneDesc.synth_config(4)
+    s = DeviceScene(desc, device=0)
+    img, cnt, _, img8 = s.render(3840, 2160, 8, want_u8=True)
+    img2, cnt2, _, _ = s.render(3840, 2160, 8)
+    s.close()
+    assert cnt["pixels"] == 3840 * 2160 and cnt == cnt2
+    assert same_bits(img, img2)
+    assert np.array_equal(img8, as_u8(img))
+    rows = np.arange(13, 2160, 270)
+    ref, _ = OracleScene(desc).render(3840, 2160, 8, rows=(13, 2160, 270), threads=16)
+    compare(img[rows], ref[rows])
+
+
+def test_config4_tiled_two_ways():
+    """Config 4 tiled over ranks through the C ABI (one GPU listed twice) equals the whole
+    frame rendered on one device."""
+    desc = SceneDesc.synth_config(4)
+    s = DeviceScene(desc, device=0)
+    ref, rcnt, _, _ = s.render(3840, 2160, 8)
+    s.close()
+    m = DeviceScene(desc, devices=[0, 0])
+    img, cnt, _, _ = m.render(3840, 2160, 8)
+    m.close()
+    assert same_bits(img, ref) and cnt == rcnt
+
+
+def test_torchrun_two_ranks_render_and_gather():
+    """bench.py under torchrun with two ranks (gloo exchange on one GPU): every rank renders
+    its bands of config 3, rank 0 gathers and un-permutes, and the assembled frames equal a
+    single-launch render bit for bit (frame_check)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29611", "bench.py", "--backend", "gloo", "--check", "1",
+           "--steps", "2", "--warmup", "1", "--inflight", "2", "--cpu-baseline", "0", "--count-frame", "0",
+           "--seam-stats", "0"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 2
+    assert out["frame_check"] is True
