@@ -146,6 +146,26 @@ void cube_triangles(std::vector<float>& out) {
 
 // rt_material -> device record (material.rs: Phong / TexturePhong with a closed set of
 // texture programs)
+// The combine pass skips a shadowed point light of a node (rt_wavefront.hip light_sum)
+// only when its term f * ((l.n * 0) * kd + (pw * 0) * ks) is exactly +-0: the Schlick r0
+// and the fresnel factor finite for either side of the surface (n1 + n2 = 1 + ri != 0,
+// |1 - r0| x (1 + |n|)^5 finite for |n| <= 1e3), (m.h)^power finite (power in [0, 1e6],
+// m.h <= 1 + eps), finite diffuse / specular colours.
+bool dark_zero(const rt_material& m) {
+    auto finite_tex = [](const rt_texture& t) {
+        return t.kind == RT_TEX_CHECKERBOARD ||
+               (std::isfinite(t.color.r) && std::isfinite(t.color.g) && std::isfinite(t.color.b));
+    };
+    const float ri = m.refraction_index;
+    if (!(std::isfinite(m.power) && m.power >= 0.f && m.power <= 1e6f && std::isfinite(ri))) return false;
+    for (int entering = 0; entering < 2; entering++) {
+        const float n1 = entering ? 1.f : ri, n2 = entering ? ri : 1.f;
+        const float q = (n1 - n2) / (n1 + n2), r0 = q * q;
+        if (!std::isfinite(q) || !std::isfinite(r0) || !(std::fabs(1.0 - (double)r0) * 1.01e15 < 1e37)) return false;
+    }
+    return finite_tex(m.diffuse) && finite_tex(m.specular);
+}
+
 rt_status mat_rec(const rt_material& m, MatRec& M) {
     if (m.kind != RT_MAT_PHONG && m.kind != RT_MAT_TEXTURE_PHONG) return RT_ERR_INVALID_ARG;
     const rt_texture* tx[3] = {&m.ambient, &m.diffuse, &m.specular};
@@ -156,6 +176,7 @@ rt_status mat_rec(const rt_material& m, MatRec& M) {
     }
     std::memset(&M, 0, sizeof(M));
     M.kind = m.kind;
+    M.dark_zero = dark_zero(m) ? 1 : 0;
     M.power = m.power;
     M.reflectivity = m.reflectivity;
     M.refraction_index = m.refraction_index;
@@ -1153,6 +1174,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     std::vector<TriIn> tri_in;
     std::vector<CubeIn> cube_in;
     uint64_t flops = 0;
+    bool normals_ok = true;  // DevScene::dark_skip: every hit normal finite with |n| <= 1e3
     for (uint32_t i = 0; i < d->n_shapes; i++) {
         const rt_shape& s = d->shapes[i];
         if (s.material < 0 || (uint32_t)s.material >= d->n_materials) return RT_ERR_BAD_MATERIAL;
@@ -1163,7 +1185,10 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
         M4 inv;
         if (!gj_inverse(s.transform, inv)) return RT_ERR_SINGULAR_MATRIX;  // set_transform
         for (int r = 0; r < 3; r++)
-            for (int c = 0; c < 4; c++) R.inv[r * 4 + c] = inv.m[r][c];
+            for (int c = 0; c < 4; c++) {
+                R.inv[r * 4 + c] = inv.m[r][c];
+                if (!(std::fabs(inv.m[r][c]) < 1e18f)) normals_ok = false;  // sphere / cube normals
+            }
         float key = keyf(i << 4);
         switch (s.kind) {
             case RT_SHAPE_SPHERE: {
@@ -1184,6 +1209,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
                 F3 u = fnorm(fcross(n, w));
                 F3 v = fnorm(fcross(n, u));
                 F3 tn = vec3_mul(s.transform, n);  // `self.transform * self.normal` (plane.rs:79)
+                if (!(std::fabs(tn.x) <= 1e3f && std::fabs(tn.y) <= 1e3f && std::fabs(tn.z) <= 1e3f)) normals_ok = false;
                 const float a[15] = {n.x, n.y, n.z, o.x, o.y, o.z, tn.x, tn.y, tn.z, u.x, u.y, u.z, v.x, v.y, v.z};
                 std::memcpy(R.a, a, sizeof(a));
                 for (int r = 0; r < 3; r++) put4(plane, inv.m[r][0], inv.m[r][1], inv.m[r][2], inv.m[r][3]);
@@ -1201,6 +1227,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
                 q.e2 = fsub(q.v[2], q.v[0]);
                 q.key = key;
                 F3 nn = tri_normal(q.v[0], q.v[1], q.v[2]);
+                if (!(std::isfinite(nn.x) && std::isfinite(nn.y) && std::isfinite(nn.z))) normals_ok = false;
                 const float a[12] = {q.v[0].x, q.v[0].y, q.v[0].z, q.e1.x, q.e1.y, q.e1.z,
                                      q.e2.x, q.e2.y, q.e2.z, nn.x, nn.y, nn.z};
                 std::memcpy(R.a, a, sizeof(a));
@@ -1335,6 +1362,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     S.bvh_m1 = lay.m1;
     S.bvh_m0 = lay.m0;
     S.graze_s2 = 1.0201f;  // normals pre-divided by sin(phi_T): checked at 1.01 sin(phi_T)
+    S.dark_skip = (normals_ok && !std::getenv("RT_NO_DARK_SKIP")) ? 1 : 0;  // env: A/B
     S.amb_r = d->ambient.r;
     S.amb_g = d->ambient.g;
     S.amb_b = d->ambient.b;

@@ -261,16 +261,21 @@ __device__ __forceinline__ float fresnel_reflection(V3 l, V3 n, float n1, float 
 
 // Phong::get_reflected_energy (material.rs:77-93): lambert + phong, per channel
 //   ((l.n * E) * Kd) + ((m.h ^ power * E) * Ks)   (phong term BLACK when m.h < 0)
-__device__ __forceinline__ V3 reflected_energy(V3 E, V3 l, const Hit& h, V3 kd, V3 ks, float power) {
-    float ln = dot(l, h.n);
-    V3 hv = norm(add(norm(h.eye), norm(l)));
-    float mh = dot(h.n, hv);
+// with h = norm(norm(eye) + norm(l)); ne = norm(eye), the same for every light of a node,
+// is evaluated once by the caller (reflected_energy_ne).
+__device__ __forceinline__ V3 reflected_energy_ne(V3 E, V3 l, V3 n, V3 ne, V3 kd, V3 ks, float power) {
+    float ln = dot(l, n);
+    V3 hv = norm(add(ne, norm(l)));
+    float mh = dot(n, hv);
     V3 spec = v3(0.f, 0.f, 0.f);
     if (!(mh < 0.f)) {
         float pw = powf(mh, power);
         spec = v3((pw * E.x) * ks.x, (pw * E.y) * ks.y, (pw * E.z) * ks.z);
     }
     return v3((ln * E.x) * kd.x + spec.x, (ln * E.y) * kd.y + spec.y, (ln * E.z) * kd.z + spec.z);
+}
+__device__ __forceinline__ V3 reflected_energy(V3 E, V3 l, const Hit& h, V3 kd, V3 ks, float power) {
+    return reflected_energy_ne(E, l, h.n, norm(h.eye), kd, ks, power);
 }
 
 // Continuation frame of a tree node whose children are still being traced.
@@ -311,7 +316,7 @@ __device__ __forceinline__ bool refract_dir(V3 rd, V3 n, float n1, float n2, V3&
 // (ray direction, normal) and the material: the same expressions the trace pass uses for
 // the child rays, so the combine pass re-evaluates them bit for bit.  f.flags gets F_REFL
 // / F_SPEC / F_REFR / F_TIR; the caller fills the ambient + lights and kd / ks.
-__device__ __forceinline__ void node_weights(const MatRec& M, V3 rd, V3 n, V3 eye, float n1, float n2, Frame& f) {
+__device__ __forceinline__ void node_weights(const MatRec& M, V3 rd, V3 n, V3 ne, float n1, float n2, Frame& f) {
     f.flags = 0u;
     f.fr = f.dr = f.pw = f.ft = 0.f;
     if (M.reflectivity > RT_EPS) {
@@ -319,7 +324,7 @@ __device__ __forceinline__ void node_weights(const MatRec& M, V3 rd, V3 n, V3 ey
         const V3 rrd = reflect_dir(rd, n);
         f.fr = fresnel_reflection(rrd, n, n1, n2);
         f.dr = dot(rrd, n);
-        const V3 hv = norm(add(norm(eye), norm(rrd)));
+        const V3 hv = norm(add(ne, norm(rrd)));  // ne = norm(eye_dir)
         const float mh = dot(n, hv);
         if (!(mh < 0.f)) {
             f.flags |= F_SPEC;

@@ -41,7 +41,8 @@ struct TexRec {
 };
 
 struct MatRec {
-    int32_t kind, pad;
+    int32_t kind;
+    int32_t dark_zero;   // 1: an unlit point light's term is exactly +-0 for this material (rt_api.cpp mat_rec)
     float power, reflectivity;
     float refraction_index, pad1, pad2, pad3;
     TexRec ambient, diffuse, specular;
@@ -92,6 +93,7 @@ struct DevScene {
     // 6 x lb_res x lb_res cells, each a leaf of bvh_leaves (LightRec::lb_base + cell)
     uint32_t lb_res;           // 0: no light buffers
     float lb_dmax;             // origins with D above it walk the hierarchy
+    int32_t dark_skip;         // 1: every hit normal is finite with |n| <= 1e3 (shadowed-light skip, light_sum)
 };
 #define RT_LB_LMAX 45.f        // ... and so do origins farther than this from the light
 

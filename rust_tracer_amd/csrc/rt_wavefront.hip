@@ -661,20 +661,37 @@ __device__ __forceinline__ NodeIn node_in(const WaveParams& P, uint32_t n, uint3
 
 // sum over the lights of fresnel(ldir) * get_reflected_energy(E, ldir) (render.rs:59-68,
 // get_light_energy :142-153), the shadow decisions taken from `litmask`; Sum starts at
-// BLACK (color.rs:164-167)
-__device__ __forceinline__ V3 light_sum(const DevScene& S, const NodeIn& q, uint32_t litmask, V3 kd, V3 ks,
-                                        float power) {
+// BLACK (color.rs:164-167).  ne = norm(eye_dir).
+// A shadowed point light (E = BLACK) adds f * ((l.n * 0) * kd + (pw * 0) * ks), which is
+// +-0 in every channel whenever f, l.n, kd, ks and (m.h)^power are finite -- and adding a
+// +-0 to the running sum changes nothing: the sum starts at +0 and can never become -0
+// under round-to-nearest (x + (-0) = x, +0 + (-0) = +0).  So such a light is skipped when
+// the material guarantees finite terms (MatRec::dark_zero: power in [0, 1e6], n1 + n2 != 0,
+// finite colours), the scene's normals are finite and bounded (DevScene::dark_skip), and the
+// half vector norm(ne + norm(ldir)) cannot degenerate (ldir not within ~8 degrees of -ne;
+// exactly opposite vectors give 0 / 0 = NaN, which the reference propagates).  A shadowed
+// light's direction is finite: a NaN direction hits nothing, so it is never shadowed.
+__device__ __forceinline__ V3 light_sum(const DevScene& S, const MatRec& M, const NodeIn& q, V3 ne, uint32_t litmask,
+                                        V3 kd, V3 ks, float power) {
     V3 lsum = v3(0.f, 0.f, 0.f);
+    const bool dark_ok = S.dark_skip && M.dark_zero;
     for (int li = 0; li < S.n_lights; ++li) {
         const LightRec& L = S.lights[li];
         V3 ldir = v3(0.f, 0.f, 0.f);
         V3 E = v3(L.r, L.g, L.b);
         if (L.kind == RT_LIGHT_POINT) {
-            ldir = norm(sub(v3(L.px, L.py, L.pz), q.ps));
-            if (!((litmask >> li) & 1u)) E = v3(0.f, 0.f, 0.f);
+            const V3 raw = sub(v3(L.px, L.py, L.pz), q.ps);
+            if (!((litmask >> li) & 1u)) {
+                if (dark_ok) {
+                    const float r2 = len2(raw), c = dot(raw, ne);
+                    if (r2 > 1e-30f && r2 < 1e30f && !(c < 0.f && c * c > 0.98f * r2)) continue;
+                }
+                E = v3(0.f, 0.f, 0.f);
+            }
+            ldir = norm(raw);
         }
         float f = fresnel_reflection(ldir, q.h.n, q.n1, q.n2);
-        V3 g = reflected_energy(E, ldir, q.h, kd, ks, power);
+        V3 g = reflected_energy_ne(E, ldir, q.h.n, ne, kd, ks, power);
         lsum = add(lsum, v3(f * g.x, f * g.y, f * g.z));
     }
     return lsum;
@@ -721,11 +738,12 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
             const V3 ka = tex_eval(M.ambient, q.h.tu, q.h.tv);
             const V3 kd = tex_eval(M.diffuse, q.h.tu, q.h.tv);
             const V3 ks = tex_eval(M.specular, q.h.tu, q.h.tv);
-            const V3 lsum = light_sum(S, q, P.node_lit[n], kd, ks, M.power);
+            const V3 ne = norm(q.h.eye);
+            const V3 lsum = light_sum(S, M, q, ne, P.node_lit[n], kd, ks, M.power);
             // ambient = mat.ambient(tex) * scene.ambient (render.rs:57), then + lights
             const V3 loc = add(v3(ka.x * S.amb_r, ka.y * S.amb_g, ka.z * S.amb_b), lsum);
             Frame f;
-            node_weights(M, q.rd, q.h.n, q.h.eye, q.n1, q.n2, f);
+            node_weights(M, q.rd, q.h.n, ne, q.n1, q.n2, f);
             f.ax = loc.x; f.ay = loc.y; f.az = loc.z;
             f.kdx = kd.x; f.kdy = kd.y; f.kdz = kd.z;
             f.ksx = ks.x; f.ksy = ks.y; f.ksz = ks.z;
@@ -804,13 +822,14 @@ __global__ __launch_bounds__(256) void forest_shade_level_kernel(WaveParams P, u
         const MatRec& M = S.mats[flags >> F_MAT_SHIFT];
         const NodeIn q = node_in(P, n, flags, M);
         const V3 kd = tex_eval(M.diffuse, q.h.tu, q.h.tv), ks = tex_eval(M.specular, q.h.tu, q.h.tv);
-        const V3 lsum = light_sum(S, q, P.node_lit[n], kd, ks, M.power);
+        const V3 ne = norm(q.h.eye);
+        const V3 lsum = light_sum(S, M, q, ne, P.node_lit[n], kd, ks, M.power);
         const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
         const bool has_r = (flags & F_HAS_R) != 0u, has_t = (flags & F_HAS_T) != 0u;
         const V3 er = xyz(has_r ? P.node_ec[2u * n] : zero), dr = xyz(has_r ? P.node_dc[2u * n] : zero);
         const V3 et = xyz(has_t ? P.node_ec[2u * n + 1u] : zero), dt = xyz(has_t ? P.node_dc[2u * n + 1u] : zero);
         float fr = fresnel_reflection(dr, q.h.n, q.n1, q.n2);
-        V3 gr = reflected_energy(er, q.h.eye, q.h, kd, ks, M.power);
+        V3 gr = reflected_energy_ne(er, q.h.eye, q.h.n, ne, kd, ks, M.power);
         V3 refl = v3(fr * gr.x, fr * gr.y, fr * gr.z);
         float ft = 1.f - fresnel_reflection(dt, neg(q.h.n), q.n1, q.n2);
         V3 refr = v3(ft * et.x, ft * et.y, ft * et.z);

@@ -211,3 +211,40 @@ def test_torchrun_two_ranks_render_and_gather():
     out = json.loads(line)
     assert out["n_gpus"] == 2
     assert out["frame_check"] is True
+
+
+def _axis_scene():
+    """A sphere on the camera axis with a point light straight behind it: the centre pixel's
+    eye direction and its (shadowed) light direction are exact opposites, so the reference's
+    half vector norm(eye + l) is 0 / 0 and the pixel is NaN (phong, material.rs:197-213)."""
+    from rust_tracer_amd import Matrix
+    d = SceneDesc()
+    red = d.phong((0.1, 0.0, 0.0), (1, 0, 0), (1, 1, 1), 60.0, 0.0, 0.0)
+    glass = d.phong((0, 0, 0), (1, 1, 1), (1, 1, 1), 60.0, 0.7, 1.333)
+    d.sphere(red, Matrix.identity())
+    d.sphere(glass, Matrix.translate(2.0, 1.0, 0.0) * Matrix.scale(0.5, 0.5, 0.5))
+    d.point_light((0.0, 0.0, 10.0), (1, 1, 1))
+    d.point_light((3.0, 4.0, -6.0), (0.5, 0.5, 0.5))
+    d.set_ambient((0.1, 0.1, 0.1))
+    return d
+
+
+@pytest.mark.parametrize("name", ["config3", "my_scene", "axis"])
+def test_shadowed_light_skip_is_exact(name, monkeypatch):
+    """The combine pass skips shadowed point lights (their term is exactly +-0, light_sum):
+    frames equal the full evaluation bit for bit (RT_NO_DARK_SKIP=1), NaNs included."""
+    desc = {"config3": lambda: SceneDesc.synth_config(3), "my_scene": SceneDesc.my_scene, "axis": _axis_scene}[name]()
+    w, h = (256, 144) if name == "config3" else (64, 64)
+    s = DeviceScene(desc, device=0)
+    img, cnt, _, _ = s.render(w, h, 8)
+    s.close()
+    monkeypatch.setenv("RT_NO_DARK_SKIP", "1")
+    s = DeviceScene(desc, device=0)
+    ref, rcnt, _, _ = s.render(w, h, 8)
+    s.close()
+    assert same_bits(img, ref) and cnt == rcnt
+    if name == "axis":
+        assert np.isnan(img[32, 32]).all()  # the reference's 0 / 0 half vector
+        oimg, ocnt = OracleScene(desc).render(w, h, 8)
+        compare(img, oimg)
+        assert cnt == ocnt

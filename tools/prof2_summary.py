@@ -1,0 +1,129 @@
+"""Summarise a tools/prof2.sh run: per-kernel ms per frame (frames in flight and one at a
+time), per-kernel HBM bytes per frame (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md's
+gfx950 correction) and SQ wave-cycle shares.  Copies the evidence to profiles/TAG/.
+
+usage: python tools/prof2_summary.py TAG [frames_in_pmc_runs]
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def fam(name):
+    n = name.split("(")[0].replace("void ", "").replace("rtdev::", "")
+    if n.startswith("trace_level_kernel<true") or "shadow_kernel<true, true>" in n or "shadow_kernel<false, true>" in n:
+        return "instrumented (counted frame)"
+    return n.split("<")[0]
+
+
+def one(pattern):
+    f = glob.glob(pattern, recursive=True)
+    return f[0] if f else None
+
+
+def trace_table(d, frames):
+    f = one(os.path.join(d, "**", "*kernel_trace.csv"))
+    if not f:
+        return {}, None, []
+    rows = list(csv.DictReader(open(f)))
+    tot = defaultdict(int)
+    n = defaultdict(int)
+    for r in rows:
+        k = fam(r["Kernel_Name"])
+        tot[k] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        n[k] += 1
+    return {k: v / 1e6 / frames for k, v in tot.items()}, f, rows
+
+
+def pmc_table(d, counter):
+    f = one(os.path.join(d, "**", "*counter_collection.csv"))
+    if not f:
+        return {}, None
+    tot = defaultdict(float)
+    for r in csv.DictReader(open(f)):
+        if r["Counter_Name"] == counter:
+            tot[fam(r["Kernel_Name"])] += float(r["Counter_Value"])
+    return tot, f
+
+
+def main():
+    tag = sys.argv[1]
+    src = os.path.join(ROOT, "gpurun_out", tag)
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    bench = json.load(open(os.path.join(src, "bench.json")))
+    bench1 = json.load(open(os.path.join(src, "bench1.json")))
+    for fn in ("bench.json", "bench1.json", "cpu_max.txt"):
+        if os.path.exists(os.path.join(src, fn)):
+            shutil.copy(os.path.join(src, fn), os.path.join(dst, fn))
+    out = [f"# Profile {tag}: {bench['config']['workload']}", ""]
+    out.append(f"bench.py: **{bench['value']} Mpixels/s** ({bench['ms_per_step']} ms/frame, "
+               f"{bench['config']['frames_in_flight']} frames in flight); one frame at a time (--inflight 1): "
+               f"{bench1['value']} Mpixels/s ({bench1['ms_per_step']} ms/frame).")
+    out.append("")
+    # trace runs: warmup + slot set-up + steps frames; divide by all frames rendered
+    f4 = bench["config"]["frames_in_flight"]
+    t4, f_t4, _ = trace_table(os.path.join(src, "trace"), 12 + 4 + f4)
+    t1, f_t1, _ = trace_table(os.path.join(src, "trace1"), 6 + 1 + 1)
+    out += ["## rocprofv3 --kernel-trace (ms of kernel time per frame)", "",
+            "| kernel | 4 frames in flight | one frame at a time |", "|---|---|---|"]
+    for k in sorted(set(t4) | set(t1), key=lambda k: -t1.get(k, 0)):
+        out.append(f"| {k} | {t4.get(k, 0):.3f} | {t1.get(k, 0):.3f} |")
+    out.append(f"| **sum** | {sum(t4.values()):.3f} | {sum(t1.values()):.3f} |")
+    for name, f in (("trace", f_t4), ("trace1", f_t1)):
+        if f:
+            shutil.copy(f, os.path.join(dst, f"kernel_trace_{name}.csv"))
+            st = one(os.path.join(src, name, "**", "*kernel_stats.csv"))
+            if st:
+                shutil.copy(st, os.path.join(dst, f"kernel_stats_{name}.csv"))
+    pmc_frames = 4 + 1  # steps + the slot's set-up frame (inflight 1, warmup 0)
+    fe, f_fe = pmc_table(os.path.join(src, "pmc_fetch"), "FETCH_SIZE")
+    wr, f_wr = pmc_table(os.path.join(src, "pmc_write"), "WRITE_SIZE")
+    out += ["", "## HBM bytes per frame (MB; FETCH_SIZE x 2 + WRITE_SIZE, KB counters)", "",
+            "| kernel | fetch x2 | write | total |", "|---|---|---|---|"]
+    tf = tw = 0.0
+    for k in sorted(set(fe) | set(wr), key=lambda k: -(2 * fe.get(k, 0) + wr.get(k, 0))):
+        a, b = 2 * fe.get(k, 0) / 1024 / pmc_frames, wr.get(k, 0) / 1024 / pmc_frames
+        tf += a
+        tw += b
+        out.append(f"| {k} | {a:.1f} | {b:.1f} | {a + b:.1f} |")
+    out.append(f"| **all** | {tf:.1f} | {tw:.1f} | {tf + tw:.1f} |")
+    for f, n in ((f_fe, "pmc_fetch.csv"), (f_wr, "pmc_write.csv")):
+        if f:
+            shutil.copy(f, os.path.join(dst, n))
+    sq = {}
+    f_sq = one(os.path.join(src, "pmc_sq", "**", "*counter_collection.csv"))
+    if f_sq:
+        shutil.copy(f_sq, os.path.join(dst, "pmc_sq.csv"))
+        tot = defaultdict(float)
+        for r in csv.DictReader(open(f_sq)):
+            tot[r["Counter_Name"]] += float(r["Counter_Value"])
+        sq = {k: v / pmc_frames for k, v in tot.items()}
+        wc = sq.get("SQ_WAVE_CYCLES", 0) or 1
+        out += ["", "## SQ (per frame, all render kernels)", "", "| counter | value |", "|---|---|"]
+        for k, v in sorted(sq.items()):
+            out.append(f"| {k} | {v:.4g} |")
+        out.append("")
+        out.append(f"Wave-cycle shares: VALU active {sq.get('SQ_ACTIVE_INST_VALU', 0) / wc:.3f}, "
+                   f"waiting (s_waitcnt) {sq.get('SQ_WAIT_ANY', 0) / wc:.3f}, "
+                   f"issue-stalled {sq.get('SQ_WAIT_INST_ANY', 0) / wc:.3f}.")
+    traffic = (tf + tw) * 1024 * 1024
+    json.dump({"workload": bench["config"]["workload"], "bytes_per_launch": traffic,
+               "launch": "one frame of the render pipeline (every kernel of the frame)",
+               "fetch_size_bytes_x2": tf * 1024 * 1024, "write_size_bytes": tw * 1024 * 1024,
+               "correction": "FETCH_SIZE x 2 per MI355X_MICROARCH.md (gfx950 tallies 128-B requests at 64 B); "
+                             "WRITE_SIZE as reported",
+               "source": f"profiles/{tag}/pmc_fetch.csv, pmc_write.csv"},
+              open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+    open(os.path.join(dst, "summary.md"), "w").write("\n".join(out) + "\n")
+    print("\n".join(out))
+
+
+if __name__ == "__main__":
+    main()
