@@ -107,12 +107,13 @@ class OracleScene:
         if self.h:
             self.L.oracle_scene_destroy(self.h)
 
-    def render(self, x_res, y_res, depth, rows=None, threads=1, spp=1, seed=0):
+    def render(self, x_res, y_res, depth, rows=None, threads=1, spp=1, seed=0, cam=None):
         """render.rs:31-38 -> (rgb float32 [y_res, x_res, 3], counters dict).
         rows = (begin, end, step) renders a subset (other rows stay 0).
-        spp > 1: jittered supersampling with rt_render_spp's hash (config 5)."""
+        spp > 1: jittered supersampling with rt_render_spp's hash (config 5).
+        cam: an abi.rt_camera (default Camera::new(x_res, y_res), render.rs:166-176)."""
         from rust_tracer_amd import abi
-        cam = abi.camera(x_res, y_res)
+        cam = cam if cam is not None else abi.camera(x_res, y_res)
         rgb = np.zeros((y_res, x_res, 3), np.float32)
         cnt = (C.c_uint64 * 3)()
         b, e, s = rows if rows is not None else (0, y_res, 1)

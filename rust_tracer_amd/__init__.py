@@ -315,10 +315,11 @@ class DeviceScene:
               "rt_scene_scan_ops")
         return dict(zip(self.SCAN_OPS, (int(v) for v in out)))
 
-    def render(self, x_res, y_res, depth, want_u8=False, device=-1, spp=1, seed=0):
+    def render(self, x_res, y_res, depth, want_u8=False, device=-1, spp=1, seed=0, cam=None):
         """render.rs:31-38 -> (rgb float32 [y_res, x_res, 3], counters dict, kernel_ms, rgb8).
-        spp > 1: jittered supersampling (rt_render_spp, BASELINE config 5)."""
-        cam = camera(x_res, y_res)
+        spp > 1: jittered supersampling (rt_render_spp, BASELINE config 5).  cam: an
+        abi.rt_camera (default Camera::new(x_res, y_res), render.rs:166-176)."""
+        cam = cam if cam is not None else camera(x_res, y_res)
         rgb = np.zeros((y_res, x_res, 3), np.float32)
         rgb8 = np.zeros((y_res, x_res, 3), np.uint8) if want_u8 else None
         cnt = abi.rt_counters()
