@@ -606,23 +606,55 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
     typename std::conditional<COUNT, ScanCnt, NoCnt>::type cnt;
     if constexpr (COUNT) cnt_init(cnt);
     bc_init();
-    for (uint32_t it = 0;; ++it) {
-        const uint32_t base = sched_base(P, &P.levels[RT_WORK_WORD(RT_MAX_DEPTH + 1)], count, it);
-        if (base >= count) {
-            if (P.sched == 2 && base != 0xFFFFFFFFu) continue;  // a block's tail past the queue end
-            break;
+    const uint32_t lmask = (1u << P.light_bits) - 1u;
+    if (P.sched == 0) {
+        // grid-stride, software-pipelined: the next iteration's entry is requested before this
+        // iteration's scan and its origin before this iteration's lit-bit atomic, so the next
+        // iteration waits neither for an HBM round trip nor for the atomic (vmcnt counts loads,
+        // stores and atomics in issue order)
+        const uint32_t stride = gridDim.x * (blockDim.x >> 6) * 64u;
+        uint32_t base = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64u;
+        uint32_t t = base + lane;
+        uint32_t e = t < count ? P.shadow_in[t] : 0u;
+        float4 q = t < count ? P.node_ps[e >> P.light_bits] : make_float4(0.f, 0.f, 0.f, 0.f);
+        while (base < count) {
+            const uint32_t tn = t + stride;
+            const uint32_t en = tn < count ? P.shadow_in[tn] : 0u;
+            bool lit = false;
+            const uint32_t n = e >> P.light_bits, li = e & lmask;
+            if (t < count) {
+                V3 ps = v3(q.x, q.y, q.z);
+                const LightRec& L = S.lights[li];
+                V3 lpos = v3(L.px, L.py, L.pz);
+                V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
+                n_shadow++;
+                lit = !shadow_scan<LDS>(S, ps, ldir, lpos, cnt, lnodes, L.lb_base);
+            }
+            q = tn < count ? P.node_ps[en >> P.light_bits] : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (lit) atomicOr(&P.node_lit[n], 1u << li);
+            base += stride;
+            t = tn;
+            e = en;
         }
-        const uint32_t t = base + lane;
-        if (t < count) {
-            uint32_t e = P.shadow_in[t];
-            uint32_t n = e >> P.light_bits, li = e & ((1u << P.light_bits) - 1u);
-            const float4 q = P.node_ps[n];
-            V3 ps = v3(q.x, q.y, q.z);
-            const LightRec& L = S.lights[li];
-            V3 lpos = v3(L.px, L.py, L.pz);
-            V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
-            n_shadow++;
-            if (!shadow_scan<LDS>(S, ps, ldir, lpos, cnt, lnodes, L.lb_base)) atomicOr(&P.node_lit[n], 1u << li);
+    } else {
+        for (uint32_t it = 0;; ++it) {
+            const uint32_t base = sched_base(P, &P.levels[RT_WORK_WORD(RT_MAX_DEPTH + 1)], count, it);
+            if (base >= count) {
+                if (P.sched == 2 && base != 0xFFFFFFFFu) continue;  // a block's tail past the queue end
+                break;
+            }
+            const uint32_t t = base + lane;
+            if (t < count) {
+                uint32_t e = P.shadow_in[t];
+                uint32_t n = e >> P.light_bits, li = e & lmask;
+                const float4 q = P.node_ps[n];
+                V3 ps = v3(q.x, q.y, q.z);
+                const LightRec& L = S.lights[li];
+                V3 lpos = v3(L.px, L.py, L.pz);
+                V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
+                n_shadow++;
+                if (!shadow_scan<LDS>(S, ps, ldir, lpos, cnt, lnodes, L.lb_base)) atomicOr(&P.node_lit[n], 1u << li);
+            }
         }
     }
     for (int o = 32; o > 0; o >>= 1) n_shadow += __shfl_xor(n_shadow, o);
