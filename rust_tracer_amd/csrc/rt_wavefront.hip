@@ -330,6 +330,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
     uint64_t clk0 = 0;
     uint32_t clk_base = 0;
 #endif
+    // sorted levels, grid-stride: this lane's next permutation entry is requested one
+    // iteration ahead, so a task costs one dependent load (the task), not two
+    const bool pf_on = level > 0 && P.perm && P.sched == 0;
+    const uint32_t pf_stride = gridDim.x * (blockDim.x >> 6) * W;
+    uint32_t pf_slot = 0;
+    bool pf_have = false;
     for (uint32_t it = 0;; ++it) {
         const uint32_t base = sched_base(P, &P.levels[RT_WORK_WORD(level)], count, it, W);
 #if RT_TASK_CLOCK_BUILD
@@ -342,6 +348,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         }
         const uint32_t t = base + lane;
         bool active = lane < W && t < count;
+        uint32_t pf_next = 0;
+        if (pf_on) {
+            const uint32_t tn = t + pf_stride;
+            pf_next = (lane < W && tn < count) ? P.perm[off + tn] : 0u;
+        }
         typedef decltype(cnt) CntT;
         RT_T0(CntT, t_load);
         V3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
@@ -378,7 +389,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                     }
                 }
             } else {
-                const Task& T = P.tasks[P.perm ? P.perm[n] : n];
+                const Task& T = P.tasks[P.perm ? (pf_have ? pf_slot : P.perm[n]) : n];
                 ro = v3(T.ox, T.oy, T.oz);
                 rd = v3(T.dx, T.dy, T.dz);
                 parent = T.parent;
@@ -571,6 +582,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         if constexpr (CntT::kCount)  // the rest of the iteration: attributes, records, children, entries
             cnt.cyc_post += (rt_clock() - t_load) - it_load - (cnt.cyc_scan - it_scan0 - it_scan_self) -
                             (cnt.cyc_self - it_self0);
+        pf_slot = pf_next;
+        pf_have = pf_on;
     }
     for (int o = 32; o > 0; o >>= 1) {
         n_node += __shfl_xor(n_node, o);
@@ -674,9 +687,8 @@ struct NodeIn {
     float n1, n2;
     uint32_t parent;
 };
-__device__ __forceinline__ NodeIn node_in(const WaveParams& P, uint32_t n, uint32_t flags, const MatRec& M) {
+__device__ __forceinline__ NodeIn node_in(float4 a, float4 b, float4 c, uint32_t flags, const MatRec& M) {
     NodeIn q;
-    const float4 a = P.node_ps[n], b = P.node_n[n], c = P.node_d[n];
     q.ps = xyz(a);
     q.h.n = xyz(b);
     q.rd = xyz(c);
@@ -742,6 +754,12 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < count; t += stride) {
         const uint32_t n = off + t;
         const uint32_t flags = P.node_flags[n];
+        // every input of the node requested at once (one memory round trip, not three: flags,
+        // then the record, then the children's colours); the slots of a miss, of padding or of
+        // an absent child hold stale values that are never used
+        const float4 qa = P.node_ps[n], qb = P.node_n[n], qc = P.node_d[n];
+        const uint32_t litmask = P.node_lit[n];
+        const float4 er = P.node_ec[2u * n], et = P.node_ec[2u * n + 1u];
         // frame batches: level-0 node t belongs to frame t / frame_items
         const uint32_t fr = (level == 0 && P.frames > 1) ? t / P.frame_items : 0u;
         if (flags & NODE_NONE) {  // padding of the band buffer: defined as 0
@@ -765,13 +783,13 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
         uint32_t parent = 0;
         if (flags & NODE_HIT) {
             const MatRec& M = S.mats[flags >> F_MAT_SHIFT];
-            const NodeIn q = node_in(P, n, flags, M);
+            const NodeIn q = node_in(qa, qb, qc, flags, M);
             parent = q.parent;
             const V3 ka = tex_eval(M.ambient, q.h.tu, q.h.tv);
             const V3 kd = tex_eval(M.diffuse, q.h.tu, q.h.tv);
             const V3 ks = tex_eval(M.specular, q.h.tu, q.h.tv);
             const V3 ne = norm(q.h.eye);
-            const V3 lsum = light_sum(S, M, q, ne, P.node_lit[n], kd, ks, M.power);
+            const V3 lsum = light_sum(S, M, q, ne, litmask, kd, ks, M.power);
             // ambient = mat.ambient(tex) * scene.ambient (render.rs:57), then + lights
             const V3 loc = add(v3(ka.x * S.amb_r, ka.y * S.amb_g, ka.z * S.amb_b), lsum);
             Frame f;
@@ -780,9 +798,8 @@ __global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32
             f.kdx = kd.x; f.kdy = kd.y; f.kdz = kd.z;
             f.ksx = ks.x; f.ksy = ks.y; f.ksz = ks.z;
             // a child that was never queued (depth limit: trace_ray(.., 0)) reports BLACK
-            const float4 er = (flags & F_HAS_R) ? P.node_ec[2u * n] : make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 et = (flags & F_HAS_T) ? P.node_ec[2u * n + 1u] : make_float4(0.f, 0.f, 0.f, 0.f);
-            c = combine(f, xyz(er), xyz(et));
+            const V3 zero = v3(0.f, 0.f, 0.f);
+            c = combine(f, (flags & F_HAS_R) ? xyz(er) : zero, (flags & F_HAS_T) ? xyz(et) : zero);
         } else if (level > 0) {
             continue;  // a missed child: the trace pass wrote BLACK to its parent's slot
         }
@@ -852,7 +869,7 @@ __global__ __launch_bounds__(256) void forest_shade_level_kernel(WaveParams P, u
         const uint32_t pix = P.node_pixel[n];
         if (P.dirty && !P.dirty[pix]) continue;
         const MatRec& M = S.mats[flags >> F_MAT_SHIFT];
-        const NodeIn q = node_in(P, n, flags, M);
+        const NodeIn q = node_in(P.node_ps[n], P.node_n[n], P.node_d[n], flags, M);
         const V3 kd = tex_eval(M.diffuse, q.h.tu, q.h.tv), ks = tex_eval(M.specular, q.h.tu, q.h.tv);
         const V3 ne = norm(q.h.eye);
         const V3 lsum = light_sum(S, M, q, ne, P.node_lit[n], kd, ks, M.power);

@@ -69,10 +69,12 @@ def main():
     out.append("")
     # trace runs: warmup + slot set-up + steps frames; divide by all frames rendered
     f4 = bench["config"]["frames_in_flight"]
+    # slot set-up (inflight x batch frames) + warm-up + timed frames
     t4, f_t4, _ = trace_table(os.path.join(src, "trace"), 12 + 4 + f4)
     t1, f_t1, _ = trace_table(os.path.join(src, "trace1"), 6 + 1 + 1)
     out += ["## rocprofv3 --kernel-trace (ms of kernel time per frame)", "",
-            "| kernel | 4 frames in flight | one frame at a time |", "|---|---|---|"]
+            f"| kernel | {f4} frames in flight ({bench['config']['passes_in_flight']} passes x "
+            f"{bench['config']['frames_per_pass']}) | one frame at a time |", "|---|---|---|"]
     for k in sorted(set(t4) | set(t1), key=lambda k: -t1.get(k, 0)):
         out.append(f"| {k} | {t4.get(k, 0):.3f} | {t1.get(k, 0):.3f} |")
     out.append(f"| **sum** | {sum(t4.values()):.3f} | {sum(t1.values()):.3f} |")

@@ -1,6 +1,5 @@
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_cull_stress.py -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/stress.log 2>&1
-echo "stress rc=$?"
-for b in 1 2 4; do timeout -k 10 200 python bench.py --steps 20 --warmup 4 --batch $b --cpu-baseline 0 --seam-stats 0 --count-frame 0 > gpurun_out/b$b.json 2>/dev/null || exit 3; done
-echo done
+export TMPDIR=/tmp
+mkdir -p gpurun_out/pmc_x
+timeout -s KILL 90 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_DCACHE_HITS SQC_DCACHE_MISSES SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d gpurun_out/pmc_x -o run -- python bench.py --steps 4 --warmup 0 --inflight 1 --cpu-baseline 0 --seam-stats 0 --count-frame 0 > gpurun_out/pmc_x.log 2>&1
+echo rc=$?
