@@ -974,9 +974,13 @@ bool sort_tasks_enabled() {
 // RT_TASK_KEY overrides (A/B): config 3 1080p frame 10.35 / 10.77 / 10.39 ms.
 uint32_t task_key_mode() {
     const char* e = std::getenv("RT_TASK_KEY");
-    return e ? (uint32_t)std::atoi(e) : 6u;
+    return e ? (uint32_t)std::atoi(e) : 7u;
 }
-// 5 / 6 (default 6): face x 2x2 direction cells | 11-bit Morton code of the point
+// 7 (default): a ray inside a sphere or cube (the refracted child of an entering hit, the
+// reflected child of a hit from inside) is keyed by that shape's centre (1 | 15-bit Morton
+// of the centre), so a wave holds the rays trapped in one or two shapes; every other ray by
+// face x 2x2 direction cells | 10-bit Morton code of a point ahead (mode 6 with one bit less).
+// 5 / 6: face x 2x2 direction cells | 11-bit Morton code of the point
 // RT_KEY_AHEAD x (scene radius) ahead on the ray (default 0.5 / 0.25): rays that cross
 // the same region next share a key.  Config 3 (same box): mode 1 4.90 ms, 6 at 0.10 /
 // 0.15 / 0.20 / 0.25 / 0.35: 4.88 / 4.86 / 4.88 / 4.81 / 4.94, mode 5 (0.5) +1.5%.
@@ -1263,6 +1267,25 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     // rest: the scan's run counts below exclude them)
     const int n_dsph_all = (int)(lay.dsph.size() / 16), n_gsph_all = (int)(lay.gsph.size() / 16);
     const int n_tri_all = (int)(lay.tri.size() / 24), n_cube_all = (int)(lay.cube.size() / 16);
+    // the Morton code (morton15, rt_wavefront.hip) of every sphere's and cube's centre -- the
+    // forward transform's translation: the task key of rays inside the shape
+    if (lay.use) {
+        const float sc = 16.f / lay.r;
+        auto cell = [&](float p, float c) { return (uint32_t)(int)std::fmin(std::fmax((p - c) * sc + 16.f, 0.f), 31.f); };
+        auto spread5 = [](uint32_t v) {
+            v = (v | (v << 8)) & 0x0300F00Fu;
+            v = (v | (v << 4)) & 0x030C30C3u;
+            v = (v | (v << 2)) & 0x09249249u;
+            return v;
+        };
+        for (uint32_t i = 0; i < d->n_shapes; i++) {
+            const rt_shape& sh = d->shapes[i];
+            if (sh.kind != RT_SHAPE_SPHERE && sh.kind != RT_SHAPE_CUBE) continue;
+            const uint32_t x = cell(sh.transform[3], lay.c[0]), y = cell(sh.transform[7], lay.c[1]),
+                           z = cell(sh.transform[11], lay.c[2]);
+            shapes[i].center_key = (spread5(x) << 2) | (spread5(y) << 1) | spread5(z);
+        }
+    }
     LightBuffers lbuf;
     build_light_buffers(lay, lights, lbuf);
     for (size_t i = 0; i < lights.size(); i++) lights[i].lb_base = lbuf.base[i];

@@ -30,7 +30,9 @@
 namespace rtdev {
 
 struct ShapeRec {
-    int32_t kind, mat, pad0, pad1;
+    int32_t kind, mat;
+    uint32_t center_key;  // sphere / cube: 15-bit Morton code of its centre (rt_wavefront.hip task_key)
+    int32_t pad1;
     float inv[12];   // rows 0..2 of the inverse transform (row 3 is never read)
     float a[16];     // plane: n(3) origin(3) Tn(3) u(3) v(3); triangle: v0 e1 e2 normal
 };

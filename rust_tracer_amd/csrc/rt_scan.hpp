@@ -779,14 +779,15 @@ __device__ __forceinline__ void linear_rest(const DevScene& S, V3 o, V3 d, float
     run_cube(S, S.n_cube_bvh, S.n_cube, o, d, bt, bk, c);
 }
 
-// Scene::intersect (scene/mod.rs:98-116): the nearest (t, key) over every shape.
+// Scene::intersect (scene/mod.rs:98-116): the nearest (t, key) over every shape, folded
+// into the (t, key) the lane already holds (scan_from: bt / bk may hold a shape tested
+// beforehand -- the lexicographic minimum does not depend on the order of the tests, and a
+// smaller starting t only lets the walk cull more).
 // LDS: the kernel staged the hierarchy's node records in LDS (lnodes).
 template <bool LDS = false, class C>
-__device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c,
-                                     lfloat4* lnodes = nullptr) {
+__device__ __forceinline__ void scan_from(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c,
+                                          lfloat4* lnodes = nullptr) {
     RT_T0(C, t_s);
-    bt = __builtin_huge_valf();
-    bk = 0xFFFFFFFFu;
     RT_STAT(0);
     const GrazePre gp = graze_prefetch(S, d);
     planes(S, o, d, bt, bk, c);
@@ -796,6 +797,13 @@ __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, u
     }
     linear_rest(S, o, d, bt, bk, c);
     RT_T1(C, c, cyc_scan, t_s);
+}
+template <bool LDS = false, class C>
+__device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c,
+                                     lfloat4* lnodes = nullptr) {
+    bt = __builtin_huge_valf();
+    bk = 0xFFFFFFFFu;
+    scan_from<LDS>(S, o, d, bt, bk, c, lnodes);
 }
 
 // ------------------------------------------------------------------ light buffers

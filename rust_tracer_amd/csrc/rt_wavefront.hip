@@ -30,6 +30,7 @@
 namespace rtdev {
 
 #define RT_SHADOW_COUNT(P) ((P).levels[2 * (RT_MAX_DEPTH + 1)])
+#define RT_INSIDE_MASK ((1u << RT_FRAME_SHIFT) - 1u)  // Task.pixel below the frame bits
 
 struct PixelRef {
     bool valid;
@@ -121,11 +122,12 @@ __device__ __forceinline__ uint32_t task_key(const WaveParams& P, V3 o, V3 d) {
     if (ax >= ay && ax >= az) { face = d.x < 0.f; u = d.y; v = d.z; m = ax; }
     else if (ay >= az) { face = 2u + (d.y < 0.f); u = d.x; v = d.z; m = ay; }
     else { face = 4u + (d.z < 0.f); u = d.x; v = d.y; m = az; }
-    if (P.key_mode == 5 || P.key_mode == 6) {  // Morton of a point ahead on the ray (A/B)
+    if (P.key_mode >= 5 && P.key_mode <= 7) {  // Morton of a point ahead on the ray
         const float ahead = P.key_ahead * P.S.bvh_r;
         const V3 q = add(o, mul(d, ahead));
         uint32_t cu = u > 0.f ? 1u : 0u, cv = v > 0.f ? 1u : 0u;
         uint32_t dir = (face << 2) | (cu << 1) | cv;
+        if (P.key_mode == 7) return (dir << 10) | (morton15(P.S, q) >> 5);  // 15 bits: bit 15 marks inside rays
         return (dir << 11) | (morton15(P.S, q) >> 4);
     }
     if (P.key_mode >= 3) {  // face x 8x8 cells (< 384) and the 15-bit Morton origin
@@ -330,6 +332,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
     uint64_t clk0 = 0;
     uint32_t clk_base = 0;
 #endif
+    // key mode 7 (not for ray forests, whose tasks carry the pixel itself): a task of a ray
+    // inside a sphere / cube carries that shape + 1 in the pixel word's low bits
+    const bool inside_keys = P.key_mode == 7 && !P.node_pixel;
     // sorted levels, grid-stride: this lane's next permutation entry is requested one
     // iteration ahead, so a task costs one dependent load (the task), not two
     const bool pf_on = level > 0 && P.perm && P.sched == 0;
@@ -356,7 +361,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         typedef decltype(cnt) CntT;
         RT_T0(CntT, t_load);
         V3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
-        uint32_t parent = 0, pix = 0;
+        uint32_t parent = 0, pix = 0, in_shape = 0;
         const uint32_t n = off + t;
         if (active) {
             if (level == 0) {
@@ -394,9 +399,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 rd = v3(T.dx, T.dy, T.dz);
                 parent = T.parent;
                 pix = T.pixel;
+                if (inside_keys) {  // a ray inside a sphere / cube: that shape + 1 below the frame bits
+                    in_shape = pix & RT_INSIDE_MASK;
+                    pix &= ~RT_INSIDE_MASK;
+                }
             }
         }
         bool want_refl = false, want_refr = false, hit = false;
+        bool refl_in = false, refr_in = false;  // the child starts inside the hit sphere / cube
         uint32_t hit_flags = 0;  // node_flags of a hit, F_HAS_R / F_HAS_T added once queued
         uint32_t decided = 0;  // point lights whose shadow ray the own-shape test settled
         uint32_t mort = 0;  // Morton code of the shadow-ray origin (queue ordering key)
@@ -414,9 +424,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         }
         if (active) {
             n_node++;
-            float bt;
-            uint32_t bk;
-            scan<LDS>(S, ro, rd, bt, bk, cnt, lnodes);
+            float bt = __builtin_huge_valf();
+            uint32_t bk = 0xFFFFFFFFu;
+            if (in_shape) {  // the enclosing sphere first: its exit point bounds the walk from the start
+                const ShapeRec& R = S.shapes[in_shape - 1u];
+                if (R.kind == RT_SHAPE_SPHERE) {
+                    RT_OPS(cnt, gsph);
+                    Rec16 q;
+                    q.r0 = ld4(R.inv);
+                    q.r1 = ld4(R.inv + 4);
+                    q.r2 = ld4(R.inv + 8);
+                    q.rk = make_float4(__uint_as_float((in_shape - 1u) << 4), 0.f, 0.f, 0.f);
+                    sph_general(q, ro, rd, bt, bk);
+                }
+            }
+            scan_from<LDS>(S, ro, rd, bt, bk, cnt, lnodes);
             if (bk == 0xFFFFFFFFu) {
                 // trace_ray -> BLACK: the parent's child slot gets BLACK (forest: direction 0)
                 P.node_flags[n] = NODE_MISS;
@@ -455,6 +477,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                     P.node_pixel[n] = pix;
                 }
                 const bool child_ok = level + 1 < P.depth;
+                if (inside_keys) {  // closed shapes: refraction enters from outside, reflection stays inside
+                    const int32_t kind = S.shapes[bk >> 4].kind;
+                    const bool closed = kind == RT_SHAPE_SPHERE || kind == RT_SHAPE_CUBE;
+                    refr_in = closed && h.entering;
+                    refl_in = closed && !h.entering;
+                }
                 if (M.reflectivity > RT_EPS && child_ok) {  // render.rs:70-84, reflect_ray :105-110
                     rrd = reflect_dir(rd, h.n);
                     rro = add(h.p, mul(rrd, 0.0002f));
@@ -475,12 +503,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         uint32_t nc = (want_refl ? 1u : 0u) + (want_refr ? 1u : 0u);
         uint32_t my = wave_append(&P.levels[2 * (level + 1) + 1], nc, lane);
         const uint32_t fkey = P.frames > 1 ? ((pix >> RT_FRAME_SHIFT) << P.task_frame_shift) : 0u;
+        // inside keys: the children carry the frame bits and the enclosing shape + 1
+        const uint32_t cpix = inside_keys ? (pix & ~RT_INSIDE_MASK) : pix, own = sh_key >> 4;
         if (want_refl) {
             uint32_t slot = next_off + my;
             if (slot < P.capacity) {
-                Task T = {rro.x, rro.y, rro.z, rrd.x, rrd.y, rrd.z, (n << 1) | 0u, pix};
+                Task T = {rro.x, rro.y, rro.z, rrd.x, rrd.y, rrd.z, (n << 1) | 0u, refl_in ? cpix | (own + 1u) : cpix};
                 P.tasks[slot] = T;
-                if (P.task_keys) P.task_keys[slot] = task_key(P, rro, rrd) | fkey;
+                if (P.task_keys)
+                    P.task_keys[slot] = (refl_in ? (1u << 15) | S.shapes[own].center_key : task_key(P, rro, rrd)) | fkey;
                 hit_flags |= F_HAS_R;
             } else {
                 atomicOr(P.overflow, 1u);
@@ -490,9 +521,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         if (want_refr) {
             uint32_t slot = next_off + my;
             if (slot < P.capacity) {
-                Task T = {tro.x, tro.y, tro.z, trd.x, trd.y, trd.z, (n << 1) | 1u, pix};
+                Task T = {tro.x, tro.y, tro.z, trd.x, trd.y, trd.z, (n << 1) | 1u, refr_in ? cpix | (own + 1u) : cpix};
                 P.tasks[slot] = T;
-                if (P.task_keys) P.task_keys[slot] = task_key(P, tro, trd) | fkey;
+                if (P.task_keys)
+                    P.task_keys[slot] = (refr_in ? (1u << 15) | S.shapes[own].center_key : task_key(P, tro, trd)) | fkey;
                 hit_flags |= F_HAS_T;
             } else {
                 atomicOr(P.overflow, 1u);
