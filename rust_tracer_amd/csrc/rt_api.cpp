@@ -207,6 +207,7 @@ enum : uint32_t { LB_DSPH = 0, LB_GSPH = 1, LB_TRI = 2, LB_CUBE = 3 };
 struct LbPrim {
     double c[3], r;
     uint32_t code;
+    uint32_t shape;  // insertion index of the primitive's shape (a pair record: this member's)
 };
 
 struct RunLayout {
@@ -689,6 +690,70 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
     }
 }
 
+// Shape buffers (rt_scan.hpp scan_buffered, key mode 7).  A ray inside a sphere S tests S
+// first; its exit t bounds the walk.  If the ray's segment [o, o + t d] lies in S's bounding
+// ball B(c, Rc) (the device checks both ends: the ball is convex), every hit nearer than the
+// exit lies on that segment, and a hierarchy primitive Q can only report such a hit if the
+// point lies within h(D) of Q (the hierarchy's own bound, D <= 3 R inside the scene ball;
+// grazing triangles: the grazing pass, which always runs) -- i.e. only if Q's ball, grown by
+// h(3 R), meets B(c, Rlist).  Rlist = Rc + 2e-5 (|c| + Rc) covers the f32 rounding of the
+// device's check (the ends' distances, o + t d, c); Rc is the ball's radius + 0.1 % (the
+// exit point lies on the surface, up to rounding).  S's buffer is a leaf record whose runs
+// are copies of the records of every such Q (S itself included); a lane whose check passes
+// tests it instead of walking the hierarchy.  Spheres whose list would exceed 96 records
+// get no buffer.
+void build_shape_buffers(RunLayout& L, std::vector<ShapeRec>& shapes) {
+    const char* e = std::getenv("RT_SHAPE_BUF");  // "0": off (A/B)
+    if ((e && e[0] == '0') || !L.use || L.lb_prims.empty()) return;
+    const double dmax = 3.0 * (double)L.r;
+    const double hmax = ((double)L.g2 * dmax + (double)L.g1) * dmax + (double)L.g0;
+    for (const LbPrim& P : L.lb_prims) {
+        const uint32_t type = P.code >> 30;
+        if (type != LB_DSPH && type != LB_GSPH) continue;
+        ShapeRec& R = shapes[P.shape];
+        if (R.kind != RT_SHAPE_SPHERE || R.pad1 != 0) continue;
+        const double cn = std::sqrt(P.c[0] * P.c[0] + P.c[1] * P.c[1] + P.c[2] * P.c[2]);
+        // 0.1 % over the ball: the exit point lies on the surface, up to rounding
+        const float rc = up_f(P.r * 1.001);
+        const double rlist = (double)rc + 2e-5 * (cn + (double)rc);
+        std::vector<uint32_t> by[4];
+        size_t n_rec = 0;
+        for (const LbPrim& Q : L.lb_prims) {
+            const double dx = Q.c[0] - P.c[0], dy = Q.c[1] - P.c[1], dz = Q.c[2] - P.c[2];
+            if (!(std::sqrt(dx * dx + dy * dy + dz * dz) <= (Q.r + rlist + hmax) * (1 + 1e-9))) continue;
+            auto& v = by[Q.code >> 30];
+            const uint32_t rec = Q.code & 0x3FFFFFFFu;
+            if (std::find(v.begin(), v.end(), rec) == v.end()) {
+                v.push_back(rec);
+                n_rec++;
+            }
+        }
+        if (std::getenv("RT_DEBUG_SHAPE_BUF"))
+            std::fprintf(stderr, "shape %u r %.4f rc %.4f hmax %.5f records %zu\n", P.shape, P.r, (double)rc, hmax, n_rec);
+        if (n_rec == 0 || n_rec > 96) continue;
+        uint32_t rec[8];
+        auto copy = [&](std::vector<float>& run, size_t width, const std::vector<uint32_t>& recs, uint32_t* range) {
+            range[0] = (uint32_t)(run.size() / width);
+            for (uint32_t r : recs) {
+                std::vector<float> t(run.begin() + width * (size_t)r, run.begin() + width * (size_t)r + width);
+                run.insert(run.end(), t.begin(), t.end());
+            }
+            range[1] = (uint32_t)(run.size() / width);
+        };
+        copy(L.dsph, 16, by[LB_DSPH], rec + 0);
+        copy(L.gsph, 16, by[LB_GSPH], rec + 2);
+        copy(L.tri, 24, by[LB_TRI], rec + 4);
+        copy(L.cube, 16, by[LB_CUBE], rec + 6);
+        const uint32_t leaf = (uint32_t)(L.leaves.size() / 8);
+        L.leaves.insert(L.leaves.end(), rec, rec + 8);
+        R.pad1 = (int32_t)(leaf + 1);
+        R.a[0] = (float)P.c[0];
+        R.a[1] = (float)P.c[1];
+        R.a[2] = (float)P.c[2];
+        R.a[3] = rc;
+    }
+}
+
 void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, const std::vector<CubeIn>& cubes,
                 bool enable, RunLayout& L) {
     using namespace rtbvh;
@@ -842,7 +907,11 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
         }
         auto lb_add = [&](uint32_t pi, uint32_t type, size_t rec) {
             const Geo& g = geo[pi];
-            L.lb_prims.push_back(LbPrim{{g.c[0], g.c[1], g.c[2]}, g.r, (type << 30) | (uint32_t)rec});
+            const Prim& p = prims[pi];
+            float key = p.kind == P_TRI ? tris[p.id].key : (p.kind == P_CUBE ? cubes[p.id].key : sph[p.id].key);
+            uint32_t kb;
+            std::memcpy(&kb, &key, 4);
+            L.lb_prims.push_back(LbPrim{{g.c[0], g.c[1], g.c[2]}, g.r, (type << 30) | (uint32_t)rec, kb >> 4});
         };
         for (const auto& leaf : T.leaves) {
             std::vector<const SphIn*> ds, gs;
@@ -1289,6 +1358,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     LightBuffers lbuf;
     build_light_buffers(lay, lights, lbuf);
     for (size_t i = 0; i < lights.size(); i++) lights[i].lb_base = lbuf.base[i];
+    build_shape_buffers(lay, shapes);
     dsph.swap(lay.dsph);
     gsph.swap(lay.gsph);
     tri.swap(lay.tri);

@@ -32,9 +32,10 @@ namespace rtdev {
 struct ShapeRec {
     int32_t kind, mat;
     uint32_t center_key;  // sphere / cube: 15-bit Morton code of its centre (rt_wavefront.hip task_key)
-    int32_t pad1;
+    int32_t pad1;         // sphere: its shape buffer's leaf + 1 (0: none; rt_api.cpp build_shape_buffers)
     float inv[12];   // rows 0..2 of the inverse transform (row 3 is never read)
-    float a[16];     // plane: n(3) origin(3) Tn(3) u(3) v(3); triangle: v0 e1 e2 normal
+    float a[16];     // plane: n(3) origin(3) Tn(3) u(3) v(3); triangle: v0 e1 e2 normal;
+                     // sphere with a shape buffer: its bounding ball's centre (3) and radius
 };
 
 struct TexRec {

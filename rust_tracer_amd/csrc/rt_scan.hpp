@@ -544,7 +544,7 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
     for (;;) {
         // the lane's limit: its best t (a plane's t < 0 beats everything: no votes), the
         // light for shadow rays, nothing once decided
-        float tmax = SHADOW ? (done ? -1.f : fminf(bt, tlim)) : bt;
+        float tmax = SHADOW ? (done ? -1.f : fminf(bt, tlim)) : (novote ? -1.f : bt);
         float tnode = (tmax < 0.f) ? -__builtin_huge_valf() : tmax + R.m;
         RT_T0(C, t_it);
         if (cur & BVH_LEAF) {
@@ -798,6 +798,39 @@ __device__ __forceinline__ void scan_from(const DevScene& S, V3 o, V3 d, float& 
     linear_rest(S, o, d, bt, bk, c);
     RT_T1(C, c, cyc_scan, t_s);
 }
+// scan_from for lanes that may hold a shape buffer (rt_api.cpp build_shape_buffers): a lane
+// with buf_ok (its segment to the enclosing sphere's exit lies in the sphere's ball, bt = that
+// exit) tests the buffer's records instead of walking the hierarchy; the wave takes its
+// lanes' buffers one after the other, each tested like a leaf by every lane (a record tested
+// for a lane that does not need it changes nothing), and walks the hierarchy for the other
+// lanes only (buffered lanes do not vote).
+template <bool LDS = false, class C>
+__device__ __forceinline__ void scan_buffered(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c,
+                                              lfloat4* lnodes, bool buf_ok, uint32_t buf_leaf) {
+    RT_T0(C, t_s);
+    RT_STAT(0);
+    const GrazePre gp = graze_prefetch(S, d);
+    planes(S, o, d, bt, bk, c);
+    if (S.use_bvh) {
+        bool want = buf_ok;
+        uint64_t pend;
+        if ((pend = __ballot(want)) != 0) {
+            const float on = sqrtf(len2(o));
+            do {
+                const uint32_t cur = (uint32_t)__builtin_amdgcn_readlane((int)buf_leaf, (int)__builtin_ctzll(pend));
+                want = want && buf_leaf != cur;
+                RT_T0(C, t_l);
+                bvh_leaf(S, cur, o, d, on, bt, bt, bk, c);
+                RT_T1(C, c, cyc_leaf, t_l);
+            } while ((pend = __ballot(want)) != 0);
+        }
+        if (__ballot(!buf_ok)) bvh_walk<false, LDS>(S, o, d, bt, bk, 0.f, 0.f, c, lnodes, buf_ok);
+        graze_pass(S, o, d, bt, bk, c, gp);
+    }
+    linear_rest(S, o, d, bt, bk, c);
+    RT_T1(C, c, cyc_scan, t_s);
+}
+
 template <bool LDS = false, class C>
 __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c,
                                      lfloat4* lnodes = nullptr) {

@@ -426,6 +426,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
             n_node++;
             float bt = __builtin_huge_valf();
             uint32_t bk = 0xFFFFFFFFu;
+            bool buf_ok = false;
+            uint32_t buf_leaf = 0;
             if (in_shape) {  // the enclosing sphere first: its exit point bounds the walk from the start
                 const ShapeRec& R = S.shapes[in_shape - 1u];
                 if (R.kind == RT_SHAPE_SPHERE) {
@@ -436,9 +438,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                     q.r2 = ld4(R.inv + 8);
                     q.rk = make_float4(__uint_as_float((in_shape - 1u) << 4), 0.f, 0.f, 0.f);
                     sph_general(q, ro, rd, bt, bk);
+                    if (R.pad1 && bt < __builtin_huge_valf()) {  // segment in the ball: its shape buffer
+                        const V3 c = v3(R.a[0], R.a[1], R.a[2]);
+                        const float rc2 = R.a[3] * R.a[3];
+                        buf_ok = len2(sub(ro, c)) <= rc2 && len2(sub(add(ro, mul(rd, bt)), c)) <= rc2;
+                        buf_leaf = (uint32_t)R.pad1 - 1u;
+                    }
                 }
             }
-            scan_from<LDS>(S, ro, rd, bt, bk, cnt, lnodes);
+            scan_buffered<LDS>(S, ro, rd, bt, bk, cnt, lnodes, buf_ok, buf_leaf);
             if (bk == 0xFFFFFFFFu) {
                 // trace_ray -> BLACK: the parent's child slot gets BLACK (forest: direction 0)
                 P.node_flags[n] = NODE_MISS;

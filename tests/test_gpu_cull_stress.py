@@ -138,3 +138,27 @@ def test_stress_scenes_match_oracle(seed, scale, cam_mode, near, slivers):
     diff[np.isnan(img) & np.isnan(ref)] = 0.0
     assert not np.isnan(diff).any()
     assert float(diff.max()) <= 1e-4  # north_star: every RGB channel within 1e-4
+
+
+@pytest.mark.parametrize("case", [None] + CASES[:3] + CASES[4:5])
+def test_shape_buffers_change_nothing(case, monkeypatch):
+    """Rays inside a sphere test its shape buffer instead of walking the hierarchy (rt_api.cpp
+    build_shape_buffers): frames and counters identical to the walk (RT_SHAPE_BUF=0) and to
+    the key mode without inside rays (RT_TASK_KEY=6)."""
+    if case is None:
+        desc, w, h, depth, cam = SceneDesc.synth_config(3), 480, 270, 8, None
+    else:
+        seed, scale, cam_mode, near, slivers = case
+        desc, w, h, depth = stress_scene(seed, scale, near, slivers), 160, 120, 8
+        cam = stress_camera(w, h, scale, cam_mode)
+    out = []
+    for env in ({}, {"RT_SHAPE_BUF": "0"}, {"RT_TASK_KEY": "6"}):
+        for k in ("RT_SHAPE_BUF", "RT_TASK_KEY"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        s = DeviceScene(desc, device=0)
+        out.append(s.render(w, h, depth, cam=cam)[:2])
+        s.close()
+    for img, cnt in out[1:]:
+        assert same_bits(img, out[0][0]) and cnt == out[0][1]
