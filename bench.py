@@ -123,20 +123,35 @@ def cpu_baseline(args, desc):
                   f"(C++ restatement of src/render.rs, g++ -O2 -ffp-contract=off); "
                   f"host: {os.cpu_count()} logical CPUs",
         "seconds": round(dt, 2),
-        "multicore": cpu_baseline_mt(args, o),
-        "per_gpu_share": cpu_baseline_mt(args, o, threads=min(16, cpu_threads(args)),
-                                         label="the box's CPU share per GPU"),
+        "multicore": cpu_baseline_mt(args, o, label=f"every core this process may use: affinity mask "
+                                                     f"{len(os.sched_getaffinity(0))} CPUs, cgroup CPU quota "
+                                                     f"{cpu_quota_cores() or 'none'}"),
     }
 
 
+def cpu_quota_cores():
+    """CPUs' worth of time the cgroup grants this process (cgroup v2 cpu.max), or None."""
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            return max(1, int(int(quota) // int(period)))
+    except Exception:
+        pass
+    return None
+
+
 def cpu_threads(args):
-    """Every host core this process may run on (OpenMP over all host cores)."""
+    """Every host core this process may run on (OpenMP over all host
+    cores): the affinity mask, capped by the cgroup's CPU quota (the GPU box shows 256 CPUs
+    in the mask but grants 16 CPUs of time; more threads than that only contend)."""
     if args.cpu_threads:
         return args.cpu_threads
-    return len(os.sched_getaffinity(0))
+    n = len(os.sched_getaffinity(0))
+    q = cpu_quota_cores()
+    return min(n, q) if q else n
 
 
-def cpu_baseline_mt(args, o, threads=None, label="every host core this process may use (sched_getaffinity)"):
+def cpu_baseline_mt(args, o, threads=None, label="every host core this process may use"):
     """The same oracle, rows dealt over T host threads (pixel-parallel over
     the host cores), on every k/T-th row: about the single-thread run's wall time."""
     threads = threads or cpu_threads(args)
