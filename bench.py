@@ -75,6 +75,9 @@ def parse():
     p.add_argument("--backend", default="nccl", help="nccl (RCCL) or gloo (CPU rehearsal)")
     p.add_argument("--check", type=int, default=0,
                    help="rank 0 compares the assembled frame with a single-launch render")
+    p.add_argument("--output", choices=("f32", "rgb8"), default="f32",
+                   help="f32 frames (the parity contract), or Color::as_u8 bytes only: fused into the "
+                        "render and gathered at 3 B per pixel (N > 1)")
     p.add_argument("--seam-stats", type=int, default=1,
                    help="N = 1: also time one frame at a time, rt_render with its host copy, the scene "
                         "build, and the depth-9 reading of 'primary+8 bounces' (untimed extras)")
@@ -208,6 +211,25 @@ def seam_stats(args, scene, pipe, tiler, dev):
     c = scene.clone(dev.index)
     out["scene_clone_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
     c.close()
+    if args.spp == 1:
+        # an animation: every frame its own camera (the origin moves 0.01 per frame along x),
+        # frames in flight and frames per pass as the headline -- the batches hold distinct views
+        from rust_tracer_amd import abi as _abi
+
+        def cam(i):
+            c = _abi.camera(args.width, args.height)
+            c.origin[0] = 0.01 * (i % 64)
+            return c
+        pipe.run(pipe.inflight * pipe.batch, cameras=cam)
+        torch.cuda.synchronize()
+        k = 12
+        e0.record(main)
+        pipe.run(k, cameras=cam)
+        e1.record(main)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / k
+        out["distinct_cameras_ms_per_frame"] = round(ms, 4)
+        out["distinct_cameras_mpixels_per_s"] = round(args.width * args.height / (ms / 1e3) / 1e6, 3)
     if args.spp == 1 and args.depth == 8:
         for t in pipe.tilers:
             t.depth = 9
@@ -274,7 +296,8 @@ def main():
         else:
             args.batch = max(1, min(4, (4 * 1920 * 1088) // share))
     pipe = FramePipeline(scene, desc, args.width, args.height, args.depth, args.band_rows, rank, world, dev,
-                         spp=args.spp, seed=args.seed, inflight=inflight, batch=args.batch)
+                         spp=args.spp, seed=args.seed, inflight=inflight, batch=args.batch,
+                         rgb8=args.output == "rgb8")
     batch = pipe.batch
     tilers = pipe.tilers
     tiler = tilers[0]
@@ -342,9 +365,12 @@ def main():
         torch.cuda.synchronize()
         if rank == 0:
             import numpy as np
-            ref, _, _, _ = scene.render(args.width, args.height, args.depth, device=dev.index, spp=args.spp,
-                                        seed=args.seed)
-            frame_check = all(bool(np.array_equal(f.view(np.uint32), ref.view(np.uint32))) for f in frames)
+            ref, _, _, ref8 = scene.render(args.width, args.height, args.depth, device=dev.index, spp=args.spp,
+                                           seed=args.seed, want_u8=args.output == "rgb8")
+            if args.output == "rgb8":
+                frame_check = all(bool(np.array_equal(f, ref8)) for f in frames)
+            else:
+                frame_check = all(bool(np.array_equal(f.view(np.uint32), ref.view(np.uint32))) for f in frames)
     seam = seam_stats(args, scene, pipe, tiler, dev) if (args.seam_stats and world == 1) else None
     for t in tilers:  # every stream-ordered pass of the run, incl. the timed ones, was complete
         t.scene.sync_status()
@@ -411,7 +437,7 @@ def main():
                 "leaf_primitives": 100 if args.config == 2 else 1000,
                 "spp": args.spp, "seed": args.seed, "band_rows": args.band_rows,
                 "frames_in_flight": inflight * batch, "passes_in_flight": inflight,
-                "frames_per_pass": batch, "pass_latency_ms": round(latency_ms, 4),
+                "frames_per_pass": batch, "pass_latency_ms": round(latency_ms, 4), "output": args.output,
                 "msamples_per_s": round(args.width * args.height * args.spp * steps / elapsed / 1e6, 3),
                 "parallelism": f"row-bands x{world}" + ((" + RCCL gather" if args.backend == "nccl"
                                                           else f" + {args.backend} gather (rehearsal)")

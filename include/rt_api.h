@@ -50,9 +50,10 @@ enum {
                                     returns a truncated frame as RT_OK) */
 };
 
-/* Largest `depth` the device path accepts (the DFS continuation stack has
- * RT_MAX_DEPTH-1 frames).  The reference recursion is unbounded. */
-#define RT_MAX_DEPTH 64
+/* Largest `depth` the device path accepts (the reference recursion is unbounded; its
+ * ray trees end where every branch missed, which the level-synchronous pipeline detects:
+ * rt_render stops enqueuing levels once one is empty). */
+#define RT_MAX_DEPTH 1024
 
 /* ---------------------------------------------------------------- scene description */
 

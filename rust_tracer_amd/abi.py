@@ -17,7 +17,7 @@ STATUS_NAMES = {
     6: "RT_ERR_OUT_OF_MEMORY", 7: "RT_ERR_BAD_MATERIAL", 8: "RT_ERR_CAPACITY",
 }
 RT_ERR_CAPACITY = 8
-RT_MAX_DEPTH = 64
+RT_MAX_DEPTH = 1024
 
 RT_TEX_CONST, RT_TEX_CHECKERBOARD = 0, 1
 RT_MAT_PHONG, RT_MAT_TEXTURE_PHONG = 0, 1

@@ -1528,6 +1528,7 @@ struct PassOut {
     uint8_t* rgb8;
     unsigned long long* counters;
     bool latch;
+    bool may_sync;  // the caller waits anyway (rt_render, forests): deep passes stop at the first empty level
 };
 
 static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
@@ -1547,7 +1548,8 @@ static rt_status launch_bands(rt_scene* s, const rt_camera* cam, uint32_t depth,
     rt_status st = ensure_ws(s, 0, 0);
     if (st != RT_OK) return st;
     if (!use_megakernel()) return launch_bands_wave(s, cam, depth, spp, seed, band_rows, rank, world, o, stream);
-    if (spp != 1 || o.rgb8 || !d_rgb) return RT_ERR_UNSUPPORTED;  // the per-pixel megakernel traces one sample, f32 out
+    // the per-pixel megakernel (A/B path): one sample, f32 out, a 63-frame continuation stack
+    if (spp != 1 || o.rgb8 || !d_rgb || depth > 64) return RT_ERR_UNSUPPORTED;  // the per-pixel megakernel traces one sample, f32 out
     RenderParams p;
     std::memset(&p, 0, sizeof(p));
     p.S = s->S;
@@ -1844,6 +1846,17 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     const char* sl = std::getenv("RT_SORT_LEVELS");
     const uint64_t sort_levels = sl ? std::strtoull(sl, nullptr, 0) : ~0ull;
     for (uint32_t k = 1; k < levels; k++) {
+        if (o.may_sync && levels > 16 && (k & 7u) == 0) {
+            // a deep pass the caller waits for anyway: stop at the first empty level (the
+            // levels after it would be no-op launches; the ray trees have ended)
+            uint32_t next = 0;
+            HIP_TRY(hipMemcpyAsync(&next, w.levels + 2 * k + 1, sizeof(next), hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+            if (next == 0) {
+                levels = k;
+                break;
+            }
+        }
         p.perm = nullptr;  // production order unless this level is sorted
         if (sort_tasks && ((sort_levels >> (k < 64 ? k : 63)) & 1ull)) {
             HIP_TRY(launch_sort(w.levels, (int32_t)k, w.capacity, task_bits, w.task_keys, nullptr, sort_scratch, w.perm,
@@ -1893,7 +1906,7 @@ rt_status rt_render_bands_ex_async(const rt_scene* scene, const rt_camera* cams,
     rt_status st = ensure_ws(s, 0, 0);
     if (st != RT_OK) return st;
     hipStream_t hs = (hipStream_t)stream;
-    const PassOut o{d_rgb, d_rgb8, reinterpret_cast<unsigned long long*>(d_counters), true};
+    const PassOut o{d_rgb, d_rgb8, reinterpret_cast<unsigned long long*>(d_counters), true, false};
     if (n_frames == 1) {
         if (use_megakernel() && !d_rgb) return RT_ERR_UNSUPPORTED;
         st = launch_bands(s, cam, depth, spp, seed, band_rows, rank, world, o, hs);
@@ -2030,7 +2043,7 @@ rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t de
         HIP_TRY(hipMemsetAsync(s->ws.counters, 0, 4 * sizeof(unsigned long long), stream));
         HIP_TRY(hipEventRecord(s->ev0, stream));
         // single device: one "band" holding every row; as_u8 fused into the level-0 combine
-        const PassOut o{s->ws.out, (rgb8 && !mega) ? s->ws.out8 : nullptr, s->ws.counters, false};
+        const PassOut o{s->ws.out, (rgb8 && !mega) ? s->ws.out8 : nullptr, s->ws.counters, false, true};
         st = launch_bands(s, cam, depth, spp, seed, 8, 0, 1, o, stream);
         if (st != RT_OK) return st;
         HIP_TRY(hipEventRecord(s->ev1, stream));
@@ -2161,7 +2174,7 @@ rt_status rt_forest_create(rt_scene* s, const rt_camera* cam, uint32_t depth, rt
     const uint32_t band_rows = 8;
     for (int attempt = 0;; attempt++) {
         HIP_TRY(hipMemsetAsync(f->counters, 0, 4 * sizeof(unsigned long long), st));
-        const PassOut o{nullptr, nullptr, f->counters, false};
+        const PassOut o{nullptr, nullptr, f->counters, false, true};
         rt_status r = wave_pipeline(s, f->ws, cam, depth, band_rows, 0, 1, o, st, &f->p, f->levels);
         if (r != RT_OK) return r;
         uint32_t ovf = 0;

@@ -14,7 +14,7 @@ independent, so the only exchange step is assembling the frame:
 import torch
 import torch.distributed as dist
 
-from . import DeviceScene, abi, band_rows_per_rank, unpermute_bands_async
+from . import DeviceScene, abi, band_rows_per_rank, unpermute_bands_async, unpermute_bands_u8_async
 
 
 def band_rows_per_rank_py(y_res, band_rows, world):
@@ -38,8 +38,11 @@ class FrameTiler:
     """Renders this rank's share of a frame and gathers the frame on rank 0."""
 
     def __init__(self, scene: DeviceScene, width, height, depth, band_rows=8, rank=0, world=1,
-                 device=None, spp=1, seed=0, batch=1):
+                 device=None, spp=1, seed=0, batch=1, rgb8=False):
+        """rgb8: render and gather only Color::as_u8 bytes (3 B per pixel instead of 12; the
+        level-0 combine writes them, rt_render_bands_ex_async with no float buffer)."""
         self.scene = scene
+        self.rgb8 = bool(rgb8) and spp == 1
         self.spp, self.seed = spp, seed
         self.w, self.h, self.depth = width, height, depth
         self.band_rows, self.rank, self.world = band_rows, rank, world
@@ -51,31 +54,36 @@ class FrameTiler:
         if spp > 1:
             self.batch = 1
         self.cam = abi.camera(width, height)
-        self.locals = torch.zeros((self.batch, self.rpr, width, 3), dtype=torch.float32, device=self.device)
+        dt = torch.uint8 if self.rgb8 else torch.float32
+        self.locals = torch.zeros((self.batch, self.rpr, width, 3), dtype=dt, device=self.device)
         self.local = self.locals[0]
         self.counters = torch.zeros(3, dtype=torch.int64, device=self.device)
         self.gathered = None
         self.frames = None          # [batch, H, W, 3]: the last pass's assembled frames (rank 0)
         if rank == 0 and world > 1:
-            self.gathered = torch.zeros((world, self.rpr, width, 3), dtype=torch.float32,
-                                        device=self.device)
-            self.frames = torch.zeros((self.batch, height, width, 3), dtype=torch.float32, device=self.device)
+            self.gathered = torch.zeros((world, self.rpr, width, 3), dtype=dt, device=self.device)
+            self.frames = torch.zeros((self.batch, height, width, 3), dtype=dt, device=self.device)
         elif world == 1:
             self.frames = self.locals[:, :height]
         self.frame = self.frames[0] if self.frames is not None else None
         self.last = 1               # frames in the last pass
 
-    def render_local(self, n=1):
-        """Render n (<= batch) frames of this rank's bands on the current stream."""
+    def render_local(self, n=1, cams=None):
+        """Render n (<= batch) frames of this rank's bands on the current stream; cams: their
+        cameras (default: Camera::new for every frame)."""
         stream = torch.cuda.current_stream(self.device).cuda_stream
         self.last = n
-        if n == 1:
-            self.scene.render_bands_async(self.cam, self.depth, self.band_rows, self.rank, self.world,
+        assert n <= self.batch
+        cams = list(cams) if cams is not None else [self.cam] * n
+        if self.rgb8:
+            self.scene.render_bands_ex_async(cams, self.depth, self.band_rows, self.rank, self.world, 0,
+                                             self.locals.data_ptr(), self.counters.data_ptr(), stream)
+        elif n == 1:
+            self.scene.render_bands_async(cams[0], self.depth, self.band_rows, self.rank, self.world,
                                           self.local.data_ptr(), self.counters.data_ptr(), stream,
                                           spp=self.spp, seed=self.seed)
         else:
-            assert n <= self.batch
-            self.scene.render_bands_batch_async([self.cam] * n, self.depth, self.band_rows, self.rank,
+            self.scene.render_bands_batch_async(cams, self.depth, self.band_rows, self.rank,
                                                 self.world, self.locals.data_ptr(), self.counters.data_ptr(),
                                                 stream)
 
@@ -99,8 +107,9 @@ class FrameTiler:
                 glist = list(self.gathered.unbind(0)) if self.rank == 0 else None
                 dist.gather(local, gather_list=glist, dst=0)
             if self.rank == 0:
-                unpermute_bands_async(self.gathered.data_ptr(), self.w, self.h, self.band_rows,
-                                      self.world, self.frames[b].data_ptr(), stream)
+                unpermute = unpermute_bands_u8_async if self.rgb8 else unpermute_bands_async
+                unpermute(self.gathered.data_ptr(), self.w, self.h, self.band_rows, self.world,
+                          self.frames[b].data_ptr(), stream)
         return self.frame
 
     def step(self):
@@ -111,21 +120,25 @@ class FrameTiler:
 class FramePipeline:
     """Consecutive frames with `inflight` frames in flight (DESIGN.md "Frames in flight").
 
-    Slot i = its own scene handle (rt_scene_create: its own workspace; one handle never
-    runs two renders at once, mirroring the reference's !Sync Scene) + its own HIP stream
-    + its own FrameTiler.  Frame k renders on slot k % inflight.  At world > 1 each frame's
+    Slot i = its own scene handle (slot 0 the caller's, the others rt_scene_clone: each its
+    own workspace; one handle never runs two renders at once, mirroring the reference's
+    !Sync Scene) + its own HIP stream + its own FrameTiler.  Frame k renders on slot k % inflight.  At world > 1 each frame's
     gather + un-permute runs on the caller's stream once its slot is done, and the slot's
     next render waits on an event recorded after that gather (the gather reads the slot's
     band buffer).  Every frame is rendered and gathered in full."""
 
     def __init__(self, scene: DeviceScene, desc, width, height, depth, band_rows=8, rank=0, world=1,
-                 device=None, spp=1, seed=0, inflight=4, batch=1):
+                 device=None, spp=1, seed=0, inflight=4, batch=1, rgb8=False):
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.inflight = max(1, int(inflight))
         self.world = world
-        self.tilers = [FrameTiler(scene if i == 0 else DeviceScene(desc, device=self.device.index), width, height,
-                                  depth, band_rows, rank, world, self.device, spp=spp, seed=seed, batch=batch)
+        # slot i > 0: a clone of the scene (device copy, own workspace and stream)
+        self.tilers = [FrameTiler(scene if i == 0 else scene.clone(self.device.index), width, height,
+                                  depth, band_rows, rank, world, self.device, spp=spp, seed=seed, batch=batch,
+                                  rgb8=rgb8)
                        for i in range(self.inflight)]
+        self.frame_index = 0        # frames enqueued so far (the `cameras` callback's argument)
+        self.pass_index = 0         # passes enqueued so far: pass k runs on slot k % inflight
         self.batch = self.tilers[0].batch
         self.streams = [torch.cuda.Stream(device=self.device) for _ in range(self.inflight)]
         self._reuse = [None] * self.inflight
@@ -139,19 +152,20 @@ class FramePipeline:
         for t in self.tilers:
             t.counters.zero_()
 
-    def run(self, n, latency_events=None):
-        """Enqueue n frames (asynchronous) in passes of up to `batch` frames, pass k on slot
-        k % inflight; the caller's stream waits for all of them.  latency_events: a list
-        that receives one (start, end) event pair per pass."""
+    def run(self, n, latency_events=None, cameras=None):
+        """Enqueue n frames (asynchronous) in passes of up to `batch` frames, pass k (counted
+        across calls) on slot k % inflight; the caller's stream waits for all of them.  latency_events: a list
+        that receives one (start, end) event pair per pass.  cameras: a callable giving the
+        rt_camera of frame i (frames numbered across calls; default Camera::new) -- an
+        animation, each frame its own view."""
         main = torch.cuda.current_stream(self.device)
         for s in self.streams:
             s.wait_stream(main)
-        k = 0
         while n > 0:
             b = min(self.batch, n)
             n -= b
-            i = k % self.inflight
-            k += 1
+            i = self.pass_index % self.inflight
+            self.pass_index += 1
             st = self.streams[i]
             with torch.cuda.stream(st):
                 if self._reuse[i] is not None:
@@ -159,7 +173,9 @@ class FramePipeline:
                 if latency_events is not None:
                     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                     ev[0].record(st)
-                self.tilers[i].render_local(b)
+                cams = [cameras(self.frame_index + j) for j in range(b)] if cameras is not None else None
+                self.tilers[i].render_local(b, cams)
+                self.frame_index += b
                 if latency_events is not None:
                     ev[1].record(st)
                     latency_events.append(ev)

@@ -248,3 +248,76 @@ def test_shadowed_light_skip_is_exact(name, monkeypatch):
         oimg, ocnt = OracleScene(desc).render(w, h, 8)
         compare(img, oimg)
         assert cnt == ocnt
+
+
+@pytest.mark.parametrize("depth", [65, 200])
+def test_depth_beyond_64(depth):
+    """The reference recursion is unbounded (render.rs:40-103); the device accepts depth up to
+    RT_MAX_DEPTH (1024) and rt_render stops enqueuing levels once one is empty.  my_scene's
+    glass and mirror spheres keep rays alive for many levels."""
+    desc = SceneDesc.my_scene()
+    s = DeviceScene(desc, device=0)
+    img, cnt, _, _ = s.render(48, 36, depth)
+    s.close()
+    ref, rcnt = OracleScene().render(48, 36, depth)
+    compare(img, ref)
+    assert cnt == rcnt
+
+
+def test_depth_limit_is_reported():
+    s = DeviceScene(SceneDesc.my_scene(), device=0)
+    with pytest.raises(RtError) as e:
+        s.render(8, 8, abi.RT_MAX_DEPTH + 1)
+    s.close()
+    assert e.value.status == 3  # RT_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("rgb8", [False, True])
+def test_frame_pipeline_distinct_cameras(rgb8):
+    """FramePipeline with a camera per frame (an animation) in batches of 2 on 2 slots: every
+    frame equals rt_render of its own camera (RGB8: its Color::as_u8 bytes)."""
+    from rust_tracer_amd.dist import FramePipeline
+    desc = SceneDesc.synth_config(3)
+    w, h, depth, n = 192, 108, 8, 4
+    s = DeviceScene(desc, device=0)
+
+    def cam(i):
+        c = abi.camera(w, h)
+        c.origin[0] = 0.05 * i
+        return c
+    refs = [s.render(w, h, depth, cam=cam(i), want_u8=True) for i in range(n)]
+    pipe = FramePipeline(s, desc, w, h, depth, inflight=2, batch=2, rgb8=rgb8)
+    seen = {}
+    for p in range(2):  # two passes of 2 frames: frames 0,1 on slot 0 and 2,3 on slot 1
+        pipe.run(2, cameras=cam)
+        torch.cuda.synchronize()
+        t = pipe.tilers[p]
+        for b in range(t.last):
+            seen[2 * p + b] = t.frames[b].cpu().numpy()
+    for i in range(n):
+        img, _, _, img8 = refs[i]
+        if rgb8:
+            assert np.array_equal(seen[i], img8)
+        else:
+            assert same_bits(seen[i], img)
+    assert not same_bits(refs[0][0], refs[1][0])  # the views really differ
+    pipe.close()
+    s.close()
+
+
+def test_torchrun_two_ranks_rgb8_gather():
+    """The N > 1 path with --output rgb8: RGB8-only bands gathered (3 B per pixel) and
+    un-permuted, equal to as_u8 of a single-launch render."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29612", "bench.py", "--backend", "gloo", "--check", "1",
+           "--steps", "2", "--warmup", "1", "--inflight", "2", "--cpu-baseline", "0", "--count-frame", "0",
+           "--seam-stats", "0", "--output", "rgb8"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["frame_check"] is True and out["config"]["output"] == "rgb8"
