@@ -1743,12 +1743,20 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     p.light_shift = lbits <= 1 ? 15u : (16u - lbits > 15u ? 15u : 16u - lbits);
     uint32_t task_bits = (p.key_mode == 3 || p.key_mode == 4) ? 24u : 16u, shadow_bits = 16u;
     {
-        // light | 18-bit Morton by default (config 3: 4.80 ms vs 4.93 with the 16-bit key);
-        // RT_SHADOW_KEY = 16 / 18 / 21 (A/B)
+        // light | light-buffer cell | 3-bit distance from the light by default ("cell2": a wave
+        // holds rays that test one cell's records, at similar reach; rays that walk the
+        // hierarchy: light | flag | 17-bit Morton): 790 / 789 Mpixels/s vs 784 / 775 for the
+        // cell alone ("cell") and 752 / 763 for light | 18-bit Morton ("18", round 1's
+        // default; round 1: 4.80 ms vs 4.93 with the 16-bit key "16"); RT_SHADOW_KEY (A/B)
         const char* e = std::getenv("RT_SHADOW_KEY");
-        const int v = e ? std::atoi(e) : 18;
+        const uint32_t cell = !e ? 2u : (std::strcmp(e, "cell") == 0 ? 1u : (std::strcmp(e, "cell2") == 0 ? 2u : 0u));
+        const int v = (e && !cell) ? std::atoi(e) : 18;
         p.shadow_fine = (p.key_mode == 3 || p.key_mode == 4 || v == 18) ? 18u : (v == 21 ? 21u : 0u);
         if (p.shadow_fine && p.shadow_fine + lbits > 32u) p.shadow_fine = 0u;
+        // cell keys: the light-buffer cell index (x 8 distance buckets for cell2) must fit
+        // below the flag bit
+        const uint64_t cells = 6ull * s->S.lb_res * s->S.lb_res * (cell == 2u ? 8u : 1u);
+        p.shadow_cell = (cell && p.shadow_fine == 18u && s->S.lb_res && cells < (1u << 17)) ? cell : 0u;
     }
     if (p.shadow_fine) shadow_bits = p.shadow_fine + lbits;
     if (frames > 1) {  // the frame index above every key bit: a wave never mixes frames

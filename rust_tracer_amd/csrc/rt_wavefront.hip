@@ -610,10 +610,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 if (want) {
                     if (slot < P.shadow_capacity) {
                         P.shadow[slot] = (n << P.light_bits) | (uint32_t)li;
-                        if (P.shadow_keys)
-                            P.shadow_keys[slot] = (P.shadow_fine ? (((uint32_t)li << P.shadow_fine) | mort)
+                        if (P.shadow_keys) {
+                            uint32_t low = mort;
+                            if (P.shadow_cell) {
+                                // the light-buffer cell this shadow ray will test (its direction
+                                // seen from the light), or flag | Morton for rays that walk
+                                const LightRec& L = S.lights[li];
+                                const V3 raw = sub(v3(L.px, L.py, L.pz), sh_ps);
+                                const float dx = sh_ps.x - S.bvh_cx, dy = sh_ps.y - S.bvh_cy, dz = sh_ps.z - S.bvh_cz;
+                                const float D = sqrtf(dx * dx + dy * dy + dz * dz) + S.bvh_r;
+                                const bool lb = L.lb_base != 0xFFFFFFFFu && D <= S.lb_dmax &&
+                                                len2(raw) <= RT_LB_LMAX * RT_LB_LMAX;
+                                if (!lb) {
+                                    low = (1u << 17) | (mort >> 1);
+                                } else if (P.shadow_cell == 2u) {  // cell | 3-bit distance from the light
+                                    const float dl = sqrtf(len2(raw)) * (8.f / RT_LB_LMAX);
+                                    low = (lb_cell(S.lb_res, neg(norm(raw))) << 3) | (uint32_t)fminf(dl, 7.f);
+                                } else {
+                                    low = lb_cell(S.lb_res, neg(norm(raw)));
+                                }
+                            }
+                            P.shadow_keys[slot] = (P.shadow_fine ? (((uint32_t)li << P.shadow_fine) | low)
                                                                    : ((uint32_t)li << P.light_shift) | (mort >> (15u - P.light_shift)))
                                                   | (P.frames > 1 ? ((pix >> RT_FRAME_SHIFT) << P.shadow_frame_shift) : 0u);
+                        }
                     } else
                         atomicOr(P.overflow, 2u);
                 }

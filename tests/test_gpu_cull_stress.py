@@ -162,3 +162,18 @@ def test_shape_buffers_change_nothing(case, monkeypatch):
         s.close()
     for img, cnt in out[1:]:
         assert same_bits(img, out[0][0]) and cnt == out[0][1]
+
+
+@pytest.mark.parametrize("key", ["18", "cell", "16"])
+def test_shadow_queue_order_changes_nothing(key, monkeypatch):
+    """The shadow queue's sort key (default: light | light-buffer cell | distance) only
+    orders the queue: frames and counters equal every other ordering bit for bit."""
+    desc = SceneDesc.synth_config(3)
+    s = DeviceScene(desc, device=0)
+    ref, rcnt, _, _ = s.render(320, 180, 8)
+    s.close()
+    monkeypatch.setenv("RT_SHADOW_KEY", key)
+    s = DeviceScene(desc, device=0)
+    img, cnt, _, _ = s.render(320, 180, 8)
+    s.close()
+    assert same_bits(img, ref) and cnt == rcnt
