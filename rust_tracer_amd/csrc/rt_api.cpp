@@ -45,8 +45,10 @@ hipError_t launch_forest_mark(const uint32_t* node_key, const uint32_t* node_pix
                               uint32_t* sizes, hipStream_t stream);
 hipError_t launch_sort(const uint32_t* levels, int32_t level, uint32_t cap, uint32_t bits, const uint32_t* keys,
                        const uint32_t* vals, uint32_t* tmp, uint32_t* vals_out,
-                         uint32_t* tile_counts, uint32_t* digit_totals, int blocks, hipStream_t stream);
+                         uint32_t* tile_counts, uint32_t* digit_totals, int blocks, hipStream_t stream,
+                         uint32_t max_digit);
 uint32_t sort_max_tiles(uint32_t cap);
+uint32_t sort_max_digits();
 }  // namespace rtdev
 
 using namespace rtdev;
@@ -1438,6 +1440,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     S.lb_res = lbuf.res;
     S.lb_dmax = lbuf.dmax;
     S.n_graze_blk = (int32_t)(lay.graze_blk.size() / 32);
+    if (std::getenv("RT_DEBUG_NO_GRAZE")) S.n_graze_blk = 0;  // measurement only: NOT exact (the grazing pass's cost)
     S.bvh_root = lay.root;
     S.n_bvh_nodes = (int32_t)(lay.nodes.size() / 16);
     S.use_bvh = lay.use ? 1 : 0;
@@ -1455,6 +1458,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     S.bvh_m1 = lay.m1;
     S.bvh_m0 = lay.m0;
     S.graze_s2 = 1.0201f;  // normals pre-divided by sin(phi_T): checked at 1.01 sin(phi_T)
+    if (const char* e = std::getenv("RT_DEBUG_GRAZE_S2")) S.graze_s2 = (float)std::atof(e);  // measurement only: NOT exact
     S.dark_skip = (normals_ok && !std::getenv("RT_NO_DARK_SKIP")) ? 1 : 0;  // env: A/B
     S.amb_r = d->ambient.r;
     S.amb_g = d->ambient.g;
@@ -1759,7 +1763,7 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         p.shadow_cell = (cell && p.shadow_fine == 18u && s->S.lb_res && cells < (1u << 17)) ? cell : 0u;
     }
     if (p.shadow_fine) shadow_bits = p.shadow_fine + lbits;
-    if (frames > 1) {  // the frame index above every key bit: a wave never mixes frames
+    if (frames > 1) {  // the frame index above every key bit: frames are contiguous in sorted queues (ordering only)
         uint32_t fbits = 0;
         while ((1u << fbits) < frames) fbits++;
         p.task_frame_shift = task_bits;
@@ -1789,7 +1793,8 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     }
     // sort scratch: keys + values for the larger queue, its tile counts, digit totals
     const uint32_t sort_cap = std::max(w.capacity, w.shadow_capacity);
-    const size_t sort_words = 4 * (size_t)sort_cap + 256 * (size_t)sort_max_tiles(sort_cap) + 256;
+    const size_t sort_words =
+        4 * (size_t)sort_cap + (size_t)sort_max_digits() * sort_max_tiles(sort_cap) + sort_max_digits();
     if ((sort_tasks || sort_shadow) && w.sort_tmp_words < sort_words) {
         if (w.sort_tmp) (void)hipFree(w.sort_tmp);
         w.sort_tmp = nullptr;
@@ -1799,7 +1804,14 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     }
     uint32_t* sort_scratch = w.sort_tmp;
     uint32_t* tile_counts = w.sort_tmp ? w.sort_tmp + 4 * (size_t)sort_cap : nullptr;
-    uint32_t* digit_totals = w.sort_tmp ? tile_counts + 256 * (size_t)sort_max_tiles(sort_cap) : nullptr;
+    uint32_t* digit_totals = w.sort_tmp ? tile_counts + (size_t)sort_max_digits() * sort_max_tiles(sort_cap) : nullptr;
+    // radix digits of up to RT_SORT_DIGIT (8..11) bits, the fewest passes for the key: 8 by
+    // default (byte digits: 3 passes for the 17-bit task keys of a 2-frame batch and the
+    // 21-bit shadow keys).  At 4 passes x 2 frames in flight: 9 (task keys in 2 passes)
+    // 788 / 795 vs 791 / 790 Mpixels/s, 11 (every key in 2 passes) 751 / 750 vs 789 / 785 --
+    // a wider digit's ranking and tile counts cost more than the pass it saves
+    const char* sd = std::getenv("RT_SORT_DIGIT");
+    const uint32_t sort_digit = sd ? (uint32_t)std::atoi(sd) : 8u;
     p.task_keys = sort_tasks ? w.task_keys : nullptr;
     p.perm = nullptr;
     p.shadow_keys = sort_shadow ? w.shadow_keys : nullptr;
@@ -1845,6 +1857,11 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         }
     }
     uint32_t levels = depth > 0 ? depth : 1;
+    // debug A/B (RT_DUP, letters s / h / c): launch every queue sort / the shadow pass / every
+    // combine twice -- each is idempotent -- to measure a stage's marginal cost in place
+    const char* dup = std::getenv("RT_DUP");
+    const int dup_sort = dup && std::strchr(dup, 's') ? 2 : 1, dup_shadow = dup && std::strchr(dup, 'h') ? 2 : 1,
+              dup_comb = dup && std::strchr(dup, 'c') ? 2 : 1;
     // Every launch sizes itself from the device-side level counts: the whole frame is
     // enqueued without a host round trip (levels past the deepest non-empty one are no-ops).
     HIP_TRY(launch_wave_init(w.levels, RT_LEVEL_TABLE_WORDS, p.total_items, sample == 0 ? w.overflow : nullptr,
@@ -1867,18 +1884,20 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         }
         p.perm = nullptr;  // production order unless this level is sorted
         if (sort_tasks && ((sort_levels >> (k < 64 ? k : 63)) & 1ull)) {
-            HIP_TRY(launch_sort(w.levels, (int32_t)k, w.capacity, task_bits, w.task_keys, nullptr, sort_scratch, w.perm,
-                                tile_counts, digit_totals, 4 * s->num_cus, stream));
+            for (int r = 0; r < dup_sort; r++)
+                HIP_TRY(launch_sort(w.levels, (int32_t)k, w.capacity, task_bits, w.task_keys, nullptr, sort_scratch,
+                                    w.perm, tile_counts, digit_totals, 4 * s->num_cus, stream, sort_digit));
             p.perm = w.perm;
         }
         HIP_TRY(launch_wave_trace(p, k, tb, stream));
     }
     if (sort_shadow) {
-        HIP_TRY(launch_sort(w.levels, -1, w.shadow_capacity, shadow_bits, w.shadow_keys, w.shadow, sort_scratch,
-                            w.shadow_sorted, tile_counts, digit_totals, 4 * s->num_cus, stream));
+        for (int r = 0; r < dup_sort; r++)
+            HIP_TRY(launch_sort(w.levels, -1, w.shadow_capacity, shadow_bits, w.shadow_keys, w.shadow, sort_scratch,
+                                w.shadow_sorted, tile_counts, digit_totals, 4 * s->num_cus, stream, sort_digit));
         p.shadow_in = w.shadow_sorted;
     }
-    HIP_TRY(launch_wave_shadow(p, sb, stream));
+    for (int r = 0; r < dup_shadow; r++) HIP_TRY(launch_wave_shadow(p, sb, stream));
     if (w.forest) {  // no combine: the forest is shaded later, any number of times
         HIP_TRY(hipMemcpyAsync(forest_levels, w.levels, 2 * (RT_MAX_DEPTH + 1) * sizeof(uint32_t),
                                hipMemcpyDeviceToHost, stream));
@@ -1894,7 +1913,8 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         forest_levels[2 * (RT_MAX_DEPTH + 1)] = used;
         return RT_OK;
     }
-    for (uint32_t k = levels; k-- > 0;) HIP_TRY(launch_wave_combine(p, k, cb, stream));
+    for (uint32_t k = levels; k-- > 0;)
+        for (int r = 0; r < dup_comb; r++) HIP_TRY(launch_wave_combine(p, k, cb, stream));
     return RT_OK;
 }
 
@@ -2300,4 +2320,40 @@ extern "C" int rt_debug_task_clock(uint32_t* out, uint32_t max_records) {
                    hipSuccess
                ? 0
                : 1;
+}
+
+// debug (tests/test_gpu_sort.py): the ray-queue radix sort on its own.  Sorts n device keys
+// (their low `bits` bits) with digits of up to max_digit bits, stably; the values (d_vals, or
+// the indices 0..n-1 when null) land in d_vals_out in key order.  Runs on the current device
+// and synchronises it.
+extern "C" int rt_debug_sort(const uint32_t* d_keys, const uint32_t* d_vals, uint32_t n, uint32_t bits,
+                             uint32_t max_digit, uint32_t* d_vals_out) {
+    if (!d_keys || !d_vals_out || bits == 0 || bits > 32) return RT_ERR_INVALID_ARG;
+    if (n == 0) return RT_OK;
+    uint32_t* levels = nullptr;
+    uint32_t* tmp = nullptr;
+    int rc = RT_OK;
+    const size_t words = 4 * (size_t)n + (size_t)sort_max_digits() * sort_max_tiles(n) + sort_max_digits();
+    if (hipMalloc(&levels, RT_LEVEL_TABLE_WORDS * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&tmp, words * sizeof(uint32_t)) != hipSuccess) {
+        rc = RT_ERR_HIP;
+    } else {
+        // the shadow queue's slot: count at levels[2 (RT_MAX_DEPTH + 1)], offset 0
+        std::vector<uint32_t> lv(RT_LEVEL_TABLE_WORDS, 0u);
+        lv[2 * (RT_MAX_DEPTH + 1)] = n;
+        uint32_t* tiles = tmp + 4 * (size_t)n;
+        uint32_t* totals = tiles + (size_t)sort_max_digits() * sort_max_tiles(n);
+        int cus = 0, dev = 0;
+        if (hipMemcpy(levels, lv.data(), lv.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess ||
+            hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            rc = RT_ERR_HIP;
+        else if (launch_sort(levels, -1, n, bits, d_keys, d_vals, tmp, d_vals_out, tiles, totals, 4 * cus, 0,
+                             max_digit) != hipSuccess ||
+                 hipDeviceSynchronize() != hipSuccess)  // d_vals == null: the values are the indices
+            rc = RT_ERR_HIP;
+    }
+    if (levels) (void)hipFree(levels);
+    if (tmp) (void)hipFree(tmp);
+    return rc;
 }

@@ -11,7 +11,8 @@
 // atomics-based counting sorts are slow here (same-bin atomics from many waves serialise
 // beyond the L2).  This sort reads its extent (offset, count) from the pipeline's level
 // counters, so a whole frame is enqueued without a host round trip, and uses no global
-// atomics.  One 8-bit pass per key byte (2 for 16-bit keys, 3 for 24), each reduce-then-scan:
+// atomics.  Passes of 8- to 11-bit digits, as few as the key needs (2 for keys of up to
+// 22 bits), each reduce-then-scan:
 //   count    per 4096-key tile, a digit histogram in LDS -> tile_counts[digit][tile]
 //   scan     per digit, exclusive scan over its tiles (one block per digit) + digit total
 //   scatter  per tile, stable block rank (rocprim::block_radix_rank, wave "match"
@@ -28,6 +29,7 @@
 namespace rtdev {
 
 constexpr uint32_t SORT_THREADS = 256, SORT_ITEMS = 16, SORT_TILE = SORT_THREADS * SORT_ITEMS;
+constexpr uint32_t SORT_MAX_DIGIT_BITS = 11, SORT_MAX_DIGITS = 1u << SORT_MAX_DIGIT_BITS;
 
 // the queue being ordered: a task level (offset / count in levels[2l], levels[2l + 1]) or
 // the shadow queue (count in levels[2 (RT_MAX_DEPTH + 1)], offset 0)
@@ -76,25 +78,28 @@ __device__ __forceinline__ void lds_digit_add(uint32_t* h, uint32_t d, bool vali
     }
 }
 
+// Digits of DB bits (2^DB digits, DB = 8..11): thread t owns digits t * DPT .. t * DPT + DPT - 1.
+template <uint32_t DB>
 __global__ __launch_bounds__(SORT_THREADS) void sort_count_kernel(SortRef r, const uint32_t* keys, int keys_abs,
-                                                                  uint32_t shift, uint32_t* tile_counts,
-                                                                  uint32_t max_tiles) {
-    __shared__ uint32_t h[256];
+                                                                  uint32_t shift, uint32_t dmask,
+                                                                  uint32_t* tile_counts, uint32_t max_tiles) {
+    constexpr uint32_t ND = 1u << DB, DPT = ND / SORT_THREADS;
+    __shared__ uint32_t h[ND];
     uint32_t off;
     const uint32_t n = sort_extent(r, off);
     const uint32_t tiles = (n + SORT_TILE - 1) / SORT_TILE;
     const uint32_t* kin = keys + (keys_abs ? off : 0u);
     const uint32_t t = threadIdx.x;
     for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-        h[t] = 0u;
+        for (uint32_t j = 0; j < DPT; j++) h[t * DPT + j] = 0u;
         __syncthreads();
         for (uint32_t i = 0; i < SORT_ITEMS; i++) {
             const uint32_t idx = tile * SORT_TILE + i * SORT_THREADS + t;
             const bool valid = idx < n;
-            lds_digit_add(h, valid ? (kin[idx] >> shift) & 255u : 0u, valid);
+            lds_digit_add(h, valid ? (kin[idx] >> shift) & dmask : 0u, valid);
         }
         __syncthreads();
-        tile_counts[t * max_tiles + tile] = h[t];
+        for (uint32_t j = 0; j < DPT; j++) tile_counts[(size_t)(t * DPT + j) * max_tiles + tile] = h[t * DPT + j];
         __syncthreads();
     }
 }
@@ -119,24 +124,34 @@ __global__ __launch_bounds__(SORT_THREADS) void sort_scan_kernel(SortRef r, uint
     if (threadIdx.x == 0) digit_totals[blockIdx.x] = running;
 }
 
-using SortRank = rocprim::block_radix_rank<SORT_THREADS, 8, rocprim::block_radix_rank_algorithm::match>;
-
 // vals == null: the value of entry i is off + i (a task's slot); keys_out == null: keys
 // are not written (last pass)
+template <uint32_t DB>
 __global__ __launch_bounds__(SORT_THREADS) void sort_scatter_kernel(SortRef r, const uint32_t* keys, const uint32_t* vals,
-                                                                    int in_abs, uint32_t shift,
+                                                                    int in_abs, uint32_t shift, uint32_t dmask,
                                                                     const uint32_t* tile_counts, uint32_t max_tiles,
                                                                     const uint32_t* digit_totals, uint32_t* keys_out,
                                                                     uint32_t* vals_out, int out_abs) {
-    __shared__ SortRank::storage_type rank_storage;
-    __shared__ uint32_t base[256];
+    constexpr uint32_t ND = 1u << DB, DPT = ND / SORT_THREADS;
+    using SortRank = rocprim::block_radix_rank<SORT_THREADS, DB, rocprim::block_radix_rank_algorithm::match>;
+    static_assert(SortRank::digits_per_thread == DPT, "digit ownership must match the ranker's");
+    __shared__ typename SortRank::storage_type rank_storage;
+    __shared__ uint32_t base[ND];
     __shared__ uint32_t lds4[4];
     uint32_t off;
     const uint32_t n = sort_extent(r, off);
     const uint32_t tiles = (n + SORT_TILE - 1) / SORT_TILE;
     const uint32_t t = threadIdx.x;
+    // thread t: digits t * DPT ..; their global bases (exclusive scan over every digit)
+    uint32_t dtot[DPT], dsum = 0;
+    for (uint32_t j = 0; j < DPT; j++) {
+        dtot[j] = digit_totals[t * DPT + j];
+        dsum += dtot[j];
+    }
     uint32_t all;
-    const uint32_t digit_base = block_exscan_256(digit_totals[t], all, lds4);  // thread t: digit t
+    uint32_t digit_base[DPT];
+    digit_base[0] = block_exscan_256(dsum, all, lds4);
+    for (uint32_t j = 1; j < DPT; j++) digit_base[j] = digit_base[j - 1] + dtot[j - 1];
     const uint32_t in_off = in_abs ? off : 0u, out_off = out_abs ? off : 0u;
     for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
         uint32_t k[SORT_ITEMS], v[SORT_ITEMS], rank[SORT_ITEMS];
@@ -145,18 +160,20 @@ __global__ __launch_bounds__(SORT_THREADS) void sort_scatter_kernel(SortRef r, c
         for (uint32_t i = 0; i < SORT_ITEMS; i++) {
             const uint32_t idx = first + i * 64u;
             const bool valid = idx < n;
-            // padding sorts last (digit 255, after every real entry) and is never written
+            // padding ranks after every real entry of its digit (it is last in the tile) and is
+            // never written
             k[i] = valid ? keys[in_off + idx] : 0xFFFFFFFFu;
             v[i] = valid ? (vals ? vals[in_off + idx] : off + idx) : 0u;
         }
-        unsigned int pre[1], cnt[1];
-        SortRank().rank_keys(k, rank, rank_storage, [shift](const uint32_t& key) { return (key >> shift) & 255u; },
+        unsigned int pre[DPT], cnt[DPT];
+        SortRank().rank_keys(k, rank, rank_storage, [shift, dmask](const uint32_t& key) { return (key >> shift) & dmask; },
                              pre, cnt);
-        base[t] = digit_base + tile_counts[(size_t)t * max_tiles + tile] - pre[0];
+        for (uint32_t j = 0; j < DPT; j++)
+            base[t * DPT + j] = digit_base[j] + tile_counts[(size_t)(t * DPT + j) * max_tiles + tile] - pre[j];
         __syncthreads();
         for (uint32_t i = 0; i < SORT_ITEMS; i++) {
             if (first + i * 64u < n) {
-                const uint32_t pos = base[(k[i] >> shift) & 255u] + rank[i];
+                const uint32_t pos = base[(k[i] >> shift) & dmask] + rank[i];
                 if (keys_out) keys_out[out_off + pos] = k[i];
                 vals_out[out_off + pos] = v[i];
             }
@@ -166,40 +183,54 @@ __global__ __launch_bounds__(SORT_THREADS) void sort_scatter_kernel(SortRef r, c
 }
 
 uint32_t sort_max_tiles(uint32_t cap) { return (cap + SORT_TILE - 1) / SORT_TILE; }
+uint32_t sort_max_digits() { return SORT_MAX_DIGITS; }
 
-// Sorts the queue `r` (keys at absolute slots) by `bits`-bit keys (8-bit digits, LSD);
-// its values (vals, or the slots themselves when vals == null) land in vals_out at the
-// same offset.  tmp: 2 x r.cap slots (keys, values) per intermediate buffer -- one for
-// two passes, two (ping-pong) for three or four; tile_counts: 256 x sort_max_tiles(r.cap);
-// digit_totals: 256.
+template <uint32_t DB>
+static void sort_pass(const SortRef& r, int nb, uint32_t mt, const uint32_t* kin, const uint32_t* vin, int in_abs,
+                      uint32_t shift, uint32_t dmask, uint32_t* tile_counts, uint32_t* digit_totals, uint32_t* kout,
+                      uint32_t* vout, int out_abs, hipStream_t stream) {
+    hipLaunchKernelGGL(sort_count_kernel<DB>, dim3(nb), dim3(SORT_THREADS), 0, stream, r, kin, in_abs, shift, dmask,
+                       tile_counts, mt);
+    hipLaunchKernelGGL(sort_scan_kernel, dim3(1u << DB), dim3(SORT_THREADS), 0, stream, r, tile_counts, mt,
+                       digit_totals);
+    hipLaunchKernelGGL(sort_scatter_kernel<DB>, dim3(nb), dim3(SORT_THREADS), 0, stream, r, kin, vin, in_abs, shift,
+                       dmask, (const uint32_t*)tile_counts, mt, (const uint32_t*)digit_totals, kout, vout, out_abs);
+}
+
+// Sorts the queue `r` (keys at absolute slots) by `bits`-bit keys, LSD, in as few passes
+// as digits of up to `max_digit` (8..11) bits allow, the bits split evenly over the passes
+// (16 bits: 2 x 8; 17: 2 x 9; 21: 2 x 11).  Its values (vals, or the slots themselves when
+// vals == null) land in vals_out at the same offset.  tmp: 2 x r.cap slots (keys, values)
+// per intermediate buffer -- one for two passes, two (ping-pong) for three or more;
+// tile_counts: sort_max_digits() x sort_max_tiles(r.cap); digit_totals: sort_max_digits().
 hipError_t launch_sort(const uint32_t* levels, int32_t level, uint32_t cap, uint32_t bits, const uint32_t* keys,
                        const uint32_t* vals, uint32_t* tmp, uint32_t* vals_out, uint32_t* tile_counts,
-                       uint32_t* digit_totals, int blocks, hipStream_t stream) {
+                       uint32_t* digit_totals, int blocks, hipStream_t stream, uint32_t max_digit) {
     const SortRef r{levels, level, cap};
     const uint32_t mt = sort_max_tiles(cap);
     const int nb = (int)std::min<uint32_t>((uint32_t)blocks, mt > 0 ? mt : 1u);
-    uint32_t passes = std::max(1u, std::min(4u, (bits + 7u) / 8u));
-    // RT_SORT_TOP=k (A/B): sort by the top k key bytes only (skip the low passes)
-    uint32_t skip = 0;
-    if (const char* e = getenv("RT_SORT_TOP")) {
-        const uint32_t k = (uint32_t)atoi(e);
-        if (k >= 1 && k < passes) skip = passes - k;
-    }
+    max_digit = std::max(8u, std::min(SORT_MAX_DIGIT_BITS, max_digit));
+    bits = std::max(1u, std::min(32u, bits));
+    const uint32_t passes = (bits + max_digit - 1u) / max_digit;
+    const uint32_t db = std::max(8u, (bits + passes - 1u) / passes);
     const uint32_t* kin = keys;
     const uint32_t* vin = vals;
     int in_abs = 1;
-    for (uint32_t p = skip; p < passes; p++) {
-        const uint32_t shift = 8u * p;
+    for (uint32_t p = 0; p < passes; p++) {
+        const uint32_t shift = db * p;
         const bool last = p + 1 == passes;
-        uint32_t* kout = last ? nullptr : tmp + (size_t)((p - skip) & 1u) * 2u * cap;
+        uint32_t* kout = last ? nullptr : tmp + (size_t)(p & 1u) * 2u * cap;
         uint32_t* vout = last ? vals_out : kout + cap;
-        hipLaunchKernelGGL(sort_count_kernel, dim3(nb), dim3(SORT_THREADS), 0, stream, r, kin, in_abs, shift,
-                           tile_counts, mt);
-        hipLaunchKernelGGL(sort_scan_kernel, dim3(256), dim3(SORT_THREADS), 0, stream, r, tile_counts, mt,
-                           digit_totals);
-        hipLaunchKernelGGL(sort_scatter_kernel, dim3(nb), dim3(SORT_THREADS), 0, stream, r, kin, vin, in_abs, shift,
-                           (const uint32_t*)tile_counts, mt, (const uint32_t*)digit_totals, kout, vout,
-                           last ? 1 : 0);
+        const int oa = last ? 1 : 0;
+        // the key's bits above `bits` are not sorted on: the last pass's digit may be narrower
+        const uint32_t w = std::min(db, bits - shift);
+        const uint32_t dm = (1u << w) - 1u;
+        switch (db) {
+            case 8: sort_pass<8>(r, nb, mt, kin, vin, in_abs, shift, dm, tile_counts, digit_totals, kout, vout, oa, stream); break;
+            case 9: sort_pass<9>(r, nb, mt, kin, vin, in_abs, shift, dm, tile_counts, digit_totals, kout, vout, oa, stream); break;
+            case 10: sort_pass<10>(r, nb, mt, kin, vin, in_abs, shift, dm, tile_counts, digit_totals, kout, vout, oa, stream); break;
+            default: sort_pass<11>(r, nb, mt, kin, vin, in_abs, shift, dm, tile_counts, digit_totals, kout, vout, oa, stream); break;
+        }
         kin = kout;
         vin = vout;
         in_abs = 0;  // scratch buffers are relative to the queue's offset
