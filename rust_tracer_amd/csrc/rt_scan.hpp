@@ -647,9 +647,6 @@ __device__ __forceinline__ uint32_t lb_cell(uint32_t res, V3 v) {
 // With direction cells (S.graze_res): the wave ORs the pair masks of its lanes' cells
 // (a superset of the pairs any lane grazes) and runs the per-triangle test on those.
 // The lane's first two mask words, loaded when its scan starts (latency hidden by the walk).
-#ifndef RT_GRAZE_PF
-#define RT_GRAZE_PF 0  // A/B: prefetch the next grazing pair's normals (measured: no gain, 2.97 vs 2.97 ms at F = 4, 4.54 vs 4.52 at F = 1)
-#endif
 struct GrazePre {
     uint32_t m0, m1;
 };
@@ -675,25 +672,23 @@ __device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float&
         cfloat4* tp = cptr(S.graze_tri);
         cfloat4* pn = cptr(S.graze_pn);
         for (uint32_t w = 0; w < S.graze_words; ++w) {
-            uint32_t m = w == 0 ? pre.m0 : (w == 1 ? pre.m1 : mp[w]);
-            for (int o2 = 32; o2 > 0; o2 >>= 1) m |= (uint32_t)__shfl_xor((int)m, o2);
-            m = (uint32_t)__builtin_amdgcn_readfirstlane((int)m);
+            // the pairs this lane's direction cell lists: a superset of the pairs it grazes
+            const uint32_t own = w == 0 ? pre.m0 : (w == 1 ? pre.m1 : mp[w]);
             RT_OPS(c, graze);
-#if RT_GRAZE_PF
-            // software-pipelined: the next pair's normals are requested before this pair's
-            // test (wave-uniform SMEM loads; the order of the tests is unchanged)
-            if (m) {
-                uint32_t pi = 32u * w + (uint32_t)__builtin_ctz(m);
-                m &= m - 1u;
-                float4 a = pn[2 * pi], b = pn[2 * pi + 1];
-                for (;;) {
-                    const bool more = m != 0u;
-                    uint32_t npi = pi;
-                    if (more) {
-                        npi = 32u * w + (uint32_t)__builtin_ctz(m);
-                        m &= m - 1u;
-                    }
-                    const float4 na = pn[2 * npi], nb = pn[2 * npi + 1];
+            // Every pair some active lane lists, each once: take the first lane that still
+            // lists an untested pair, test all of its untested pairs, repeat.  Ballots and
+            // readlane see exactly the active lanes, whatever they are (a butterfly of lane
+            // shuffles can lose a lane's bits when the lane it passes through is inactive);
+            // lanes of one direction cell share their list, so few rounds cover the wave.
+            uint32_t done = 0u;  // wave-uniform
+            uint64_t pend;
+            while ((pend = __ballot((own & ~done) != 0u)) != 0ull) {
+                uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)(own & ~done), (int)__builtin_ctzll(pend));
+                done |= m;
+                while (m) {
+                    const uint32_t pi = 32u * w + (uint32_t)__builtin_ctz(m);
+                    m &= m - 1u;
+                    const float4 a = pn[2 * pi], b = pn[2 * pi + 1];
                     f2 nn = (bc(d.x) * f2{a.x, a.y} + bc(d.y) * f2{a.z, a.w}) + bc(d.z) * f2{b.x, b.y};
                     nn *= nn;
                     RT_OPS(c, graze_n);
@@ -701,26 +696,8 @@ __device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float&
                         RT_OPS(c, tri);
                         tri_pair(ld_tri(tp + 6 * pi), o, d, bt, bk);
                     }
-                    if (!more) break;
-                    pi = npi;
-                    a = na;
-                    b = nb;
                 }
             }
-#else
-            while (m) {
-                const uint32_t pi = 32u * w + (uint32_t)__builtin_ctz(m);
-                m &= m - 1u;
-                const float4 a = pn[2 * pi], b = pn[2 * pi + 1];
-                f2 nn = (bc(d.x) * f2{a.x, a.y} + bc(d.y) * f2{a.z, a.w}) + bc(d.z) * f2{b.x, b.y};
-                nn *= nn;
-                RT_OPS(c, graze_n);
-                if (__ballot(nn.x < lim || nn.y < lim)) {
-                    RT_OPS(c, tri);
-                    tri_pair(ld_tri(tp + 6 * pi), o, d, bt, bk);
-                }
-            }
-#endif
         }
         RT_T1(C, c, cyc_graze, t_g);
         return;
@@ -842,9 +819,15 @@ __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, u
 // ------------------------------------------------------------------ light buffers
 // (rt_api.cpp build_light_buffers, DESIGN.md "Light buffers")
 
+// max of x over the active lanes (NaN lanes ignored unless the first lane's is NaN, which
+// only makes the caller's reach unbounded), wave-uniform: each round jumps to a lane above
+// the current max.  Exact for any set of active lanes, and no LDS round trips (a butterfly
+// of lane shuffles costs six and can lose a lane routed through an inactive one).
 __device__ __forceinline__ float wave_max(float x) {
-    for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
-    return x;
+    float m = rfl(x);
+    uint64_t b;
+    while ((b = __ballot(x > m)) != 0ull) m = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), (int)__builtin_ctzll(b)));
+    return m;
 }
 
 // The light-buffer pass of a shadow scan.  A lane with a buffer (lb) tests the records
