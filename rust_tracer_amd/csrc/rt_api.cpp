@@ -210,6 +210,8 @@ struct LbPrim {
     double c[3], r;
     uint32_t code;
     uint32_t shape;  // insertion index of the primitive's shape (a pair record: this member's)
+    double h3;       // this primitive's own bound h_P(D) at D = 3 R (+ the slab terms): how far
+                     // from it a hit it reports can lie, for any origin within 3 R of the centre
 };
 
 struct RunLayout {
@@ -601,7 +603,7 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
         for (const LbPrim& p : L.lb_prims) {
             double w[3] = {p.c[0] - lp[0], p.c[1] - lp[1], p.c[2] - lp[2]};
             const double dist = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-            const double rr = (p.r + hmax) * (1 + 1e-6);
+            const double rr = (p.r + std::min(p.h3, hmax)) * (1 + 1e-6);
             if (!(dist - rr >= LB_RHO)) {  // a primitive (nearly) at the light: no buffer
                 ok = false;
                 break;
@@ -722,7 +724,7 @@ void build_shape_buffers(RunLayout& L, std::vector<ShapeRec>& shapes) {
         size_t n_rec = 0;
         for (const LbPrim& Q : L.lb_prims) {
             const double dx = Q.c[0] - P.c[0], dy = Q.c[1] - P.c[1], dz = Q.c[2] - P.c[2];
-            if (!(std::sqrt(dx * dx + dy * dy + dz * dz) <= (Q.r + rlist + hmax) * (1 + 1e-9))) continue;
+            if (!(std::sqrt(dx * dx + dy * dy + dz * dz) <= (Q.r + rlist + std::min(Q.h3, hmax)) * (1 + 1e-9))) continue;
             auto& v = by[Q.code >> 30];
             const uint32_t rec = Q.code & 0x3FFFFFFFu;
             if (std::find(v.begin(), v.end(), rec) == v.end()) {
@@ -875,6 +877,25 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
         }
         R *= 1 + 1e-6;
         double g2 = 0, g1 = 0, g0 = 0, m1 = 0, m0 = 0;
+        if (const char* ss = std::getenv("RT_DEBUG_SPH_SCALE")) {  // measurement only: NOT conservative
+            const double k = std::atof(ss);
+            for (size_t i = 0; i < coef.size(); i++)
+                if (prims[i].kind == P_DSPH || prims[i].kind == P_GSPH) {
+                    coef[i].a2 *= k;
+                    coef[i].a1 *= k;
+                    coef[i].a0 *= k;
+                    coef[i].cC *= k;
+                }
+        }
+        if (const char* ts = std::getenv("RT_DEBUG_TRI_SCALE")) {  // measurement only: NOT conservative
+            const double k = std::atof(ts);
+            for (size_t i = 0; i < coef.size(); i++)
+                if (prims[i].kind == P_TRI) {
+                    coef[i].a1 *= k;
+                    coef[i].a0 *= k;
+                    coef[i].cC *= k;
+                }
+        }
         for (const Coef& c : coef) {
             g2 = std::max(g2, c.a2);
             g1 = std::max(g1, c.a1);
@@ -913,7 +934,13 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
             float key = p.kind == P_TRI ? tris[p.id].key : (p.kind == P_CUBE ? cubes[p.id].key : sph[p.id].key);
             uint32_t kb;
             std::memcpy(&kb, &key, 4);
-            L.lb_prims.push_back(LbPrim{{g.c[0], g.c[1], g.c[2]}, g.r, (type << 30) | (uint32_t)rec, kb >> 4});
+            // the primitive's own polynomial (the hierarchy grows boxes by the maximum over
+            // every primitive, which the smallest sphere sets), at D = 3 R, plus the slab terms
+            const Coef& q = coef[pi];
+            const double d3 = 3.0 * (double)L.r;  // the buffers' D_max
+            const double h3 = ((q.a2 * d3 + q.a1 + SAFETY_SLAB * 16.0 * FEPS) * d3 + q.a0 + q.cC * Cn +
+                               SAFETY_SLAB * 8.0 * FEPS * (3.0 * Cn + R)) * (1 + 1e-6);
+            L.lb_prims.push_back(LbPrim{{g.c[0], g.c[1], g.c[2]}, g.r, (type << 30) | (uint32_t)rec, kb >> 4, h3});
         };
         for (const auto& leaf : T.leaves) {
             std::vector<const SphIn*> ds, gs;
