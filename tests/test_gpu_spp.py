@@ -63,6 +63,20 @@ def test_config5_4k_sampled_rows():
     compare(img[r], ref[r])
 
 
+def test_config5_64spp_sampled_rows():
+    """Config 5 as benchmarked: 3840x2160, depth 8, 64 jittered samples per pixel, seed 3 --
+    two full rows (2 x 3840 pixels x 64 samples) against the oracle."""
+    desc = SceneDesc.synth_config(5)
+    s = DeviceScene(desc)
+    img, cnt, _, _ = s.render(3840, 2160, 8, spp=64, seed=3)
+    s.close()
+    assert cnt["pixels"] == 3840 * 2160 * 64
+    rows = (1080, 2160, 1000)
+    ref, _ = OracleScene(desc).render(3840, 2160, 8, rows=rows, threads=16, spp=64, seed=3)
+    r = np.arange(*rows)
+    compare(img[r], ref[r])
+
+
 def test_spp_bands_reassemble():
     """The multi-GPU band path with samples: per-rank bands + unpermute == one launch."""
     import torch
