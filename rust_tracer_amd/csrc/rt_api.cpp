@@ -1464,6 +1464,10 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     S.graze_mask = (const uint32_t*)at(15);
     S.graze_res = lay.graze_res;
     S.graze_words = lay.graze_words;
+    {  // RT_GRAZE_LANE=0: the wave-union grazing path (A/B)
+        const char* e = std::getenv("RT_GRAZE_LANE");
+        S.graze_lane = (e && e[0] == '0') ? 0u : 1u;
+    }
     S.lb_res = lbuf.res;
     S.lb_dmax = lbuf.dmax;
     S.n_graze_blk = (int32_t)(lay.graze_blk.size() / 32);

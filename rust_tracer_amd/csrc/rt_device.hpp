@@ -91,6 +91,7 @@ struct DevScene {
     const float4* graze_pn;    // per graze pair: {nAx nBx nAy nBy} {nAz nBz - -} (n / sin(phi_T))
     const uint32_t* graze_mask;  // per direction cell: graze_words words of pair bits
     uint32_t graze_res, graze_words;  // 0: the cone path (rt_scan.hpp graze_pass)
+    uint32_t graze_lane;       // 1: each lane tests its own cell's pairs first (per-lane grazing sets)
     unsigned long long* scan_ops;  // RT_OPS_* lane-weighted test counts
     // light buffers (shadow rays; rt_api.cpp build_light_buffers): per point light
     // 6 x lb_res x lb_res cells, each a leaf of bvh_leaves (LightRec::lb_base + cell)

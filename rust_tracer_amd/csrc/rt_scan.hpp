@@ -660,9 +660,15 @@ __device__ __forceinline__ GrazePre graze_prefetch(const DevScene& S, V3 d) {
     return g;
 }
 
-template <class C>
+// Per-lane sets (S.graze_lane): each lane first runs the per-triangle test on the pairs
+// its own cell lists (normals from LDS when the kernel staged them after the node
+// records, else per-lane loads); the wave then tests, by tri_pair, the union of the pairs
+// some lane really grazes -- the same pairs the union path below ends up testing, without
+// a round trip per candidate of the wave's union.  novote: the lane's answer is settled
+// (a decided shadow ray), it lists nothing.
+template <bool LDS, class C>
 __device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, C& c,
-                                           GrazePre pre) {
+                                           GrazePre pre, lfloat4* lnodes, bool novote = false) {
     if (S.n_graze_blk == 0) return;
     RT_T0(C, t_g);
     const float dd = len2(d);
@@ -670,6 +676,45 @@ __device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float&
     if (S.graze_res) {
         const uint32_t* mp = S.graze_mask + (size_t)lb_cell(S.graze_res, d) * S.graze_words;
         cfloat4* tp = cptr(S.graze_tri);
+        if (S.graze_lane) {
+            lfloat4* lpn = lnodes + 4 * S.n_bvh_nodes;
+            for (uint32_t w = 0; w < S.graze_words; ++w) {
+                uint32_t own = novote ? 0u : (w == 0 ? pre.m0 : (w == 1 ? pre.m1 : mp[w]));
+                RT_OPS(c, graze);
+                uint32_t real = 0u;  // the pairs of word w this lane grazes
+                while (own) {        // divergent: as many rounds as the longest list
+                    const uint32_t b = (uint32_t)__builtin_ctz(own);
+                    own &= own - 1u;
+                    const uint32_t pi = 32u * w + b;
+                    float4 a, e;
+                    if (LDS) {
+                        a = lpn[2 * pi];
+                        e = lpn[2 * pi + 1];
+                    } else {
+                        a = S.graze_pn[2 * pi];
+                        e = S.graze_pn[2 * pi + 1];
+                    }
+                    f2 nn = (bc(d.x) * f2{a.x, a.y} + bc(d.y) * f2{a.z, a.w}) + bc(d.z) * f2{e.x, e.y};
+                    nn *= nn;
+                    RT_OPS(c, graze_n);
+                    if (nn.x < lim || nn.y < lim) real |= 1u << b;
+                }
+                uint32_t done = 0u;  // wave-uniform
+                uint64_t pend;
+                while ((pend = __ballot((real & ~done) != 0u)) != 0ull) {
+                    uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)(real & ~done), (int)__builtin_ctzll(pend));
+                    done |= m;
+                    while (m) {
+                        const uint32_t pi = 32u * w + (uint32_t)__builtin_ctz(m);
+                        m &= m - 1u;
+                        RT_OPS(c, tri);
+                        tri_pair(ld_tri(tp + 6 * pi), o, d, bt, bk);
+                    }
+                }
+            }
+            RT_T1(C, c, cyc_graze, t_g);
+            return;
+        }
         cfloat4* pn = cptr(S.graze_pn);
         for (uint32_t w = 0; w < S.graze_words; ++w) {
             // the pairs this lane's direction cell lists: a superset of the pairs it grazes
@@ -770,7 +815,7 @@ __device__ __forceinline__ void scan_from(const DevScene& S, V3 o, V3 d, float& 
     planes(S, o, d, bt, bk, c);
     if (S.use_bvh) {
         bvh_walk<false, LDS>(S, o, d, bt, bk, 0.f, 0.f, c, lnodes);
-        graze_pass(S, o, d, bt, bk, c, gp);
+        graze_pass<LDS>(S, o, d, bt, bk, c, gp, lnodes);
     }
     linear_rest(S, o, d, bt, bk, c);
     RT_T1(C, c, cyc_scan, t_s);
@@ -802,7 +847,7 @@ __device__ __forceinline__ void scan_buffered(const DevScene& S, V3 o, V3 d, flo
             } while ((pend = __ballot(want)) != 0);
         }
         if (__ballot(!buf_ok)) bvh_walk<false, LDS>(S, o, d, bt, bk, 0.f, 0.f, c, lnodes, buf_ok);
-        graze_pass(S, o, d, bt, bk, c, gp);
+        graze_pass<LDS>(S, o, d, bt, bk, c, gp, lnodes);
     }
     linear_rest(S, o, d, bt, bk, c);
     RT_T1(C, c, cyc_scan, t_s);
@@ -944,7 +989,7 @@ __device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lp
             bvh_walk<true, LDS>(S, o, d, bt, bk, tlim, l2, c, lnodes, lb);
         done = shadow_decided(o, d, bt, l2);
         if (__ballot(!done) == 0) goto finish;
-        graze_pass(S, o, d, bt, bk, c, gp);
+        graze_pass<LDS>(S, o, d, bt, bk, c, gp, lnodes, done);
         done = shadow_decided(o, d, bt, l2);
         if (__ballot(!done) == 0) goto finish;
     }

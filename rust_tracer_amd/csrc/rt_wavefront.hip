@@ -305,6 +305,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
     const DevScene& S = P.S;
     if (LDS) {  // stage the hierarchy's node records in LDS
         for (int i = threadIdx.x; i < 4 * S.n_bvh_nodes; i += blockDim.x) rt_dyn_lds[i] = S.bvh_nodes[i];
+        // ... followed by the grazing pairs' normals for per-lane grazing sets
+        if (S.graze_lane && S.graze_res)
+            for (int i = threadIdx.x; i < 8 * S.n_graze_blk; i += blockDim.x)
+                rt_dyn_lds[4 * S.n_bvh_nodes + i] = S.graze_pn[i];
         __syncthreads();
     }
     lfloat4* lnodes = (lfloat4*)rt_dyn_lds;
@@ -670,6 +674,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
     const DevScene& S = P.S;
     if (LDS) {  // stage the hierarchy's node records in LDS
         for (int i = threadIdx.x; i < 4 * S.n_bvh_nodes; i += blockDim.x) rt_dyn_lds[i] = S.bvh_nodes[i];
+        // ... followed by the grazing pairs' normals for per-lane grazing sets
+        if (S.graze_lane && S.graze_res)
+            for (int i = threadIdx.x; i < 8 * S.n_graze_blk; i += blockDim.x)
+                rt_dyn_lds[4 * S.n_bvh_nodes + i] = S.graze_pn[i];
         __syncthreads();
     }
     lfloat4* lnodes = (lfloat4*)rt_dyn_lds;
@@ -1000,15 +1008,19 @@ hipError_t wave_occupancy(int* trace_blocks, int* shadow_blocks, int* combine_bl
 
 // hierarchy node records staged in LDS when they fit (RT_LDS_NODES=0: never; =trace /
 // =shadow: only that kernel, A/B)
+// LDS bytes of the staged records: node records, then the grazing pairs' normals
+static size_t lds_bytes(const WaveParams& p) {
+    return (size_t)p.S.n_bvh_nodes * 64 + ((p.S.graze_lane && p.S.graze_res) ? (size_t)p.S.n_graze_blk * 128 : 0);
+}
 static bool lds_nodes_for(const WaveParams& p, const char* kernel) {
-    size_t lds = (size_t)p.S.n_bvh_nodes * 64;
+    size_t lds = lds_bytes(p);
     const char* e = getenv("RT_LDS_NODES");
     if (e && (e[0] == '0' || (std::strcmp(e, "1") != 0 && std::strcmp(e, kernel) != 0))) return false;
     return p.S.use_bvh && lds > 0 && lds <= 36 * 1024;
 }
 
 hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream) {
-    const size_t lds = (size_t)p.S.n_bvh_nodes * 64;
+    const size_t lds = lds_bytes(p);
     const bool use = lds_nodes_for(p, "trace");
     if (p.count_mask & 1u) {
         if (use)
@@ -1025,7 +1037,7 @@ hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hi
 }
 
 hipError_t launch_wave_shadow(const WaveParams& p, int blocks, hipStream_t stream) {
-    const size_t lds = (size_t)p.S.n_bvh_nodes * 64;
+    const size_t lds = lds_bytes(p);
     const bool use = lds_nodes_for(p, "shadow");
     const bool count = (p.count_mask & 2u) != 0;
     if (use && count)
