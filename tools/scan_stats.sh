@@ -9,4 +9,4 @@ F="-O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -munsafe-fp-atom
 /opt/rocm/bin/hipcc $F -c -o build_stats/rt_kernels.o rt_kernels.hip
 /opt/rocm/bin/hipcc $F -c -o build_stats/rt_wavefront.o rt_wavefront.hip
 /opt/rocm/bin/hipcc $F -shared -o ../librt_hip_stats.so build_stats/rt_kernels.o build_stats/rt_wavefront.o \
-    build/rt_order.o build/rt_api.o build/rt_bvh.o build/scene.o build/image_io.o
+    build/rt_order.o build/rt_api.o build/rt_multi.o build/rt_bvh.o build/scene.o build/image_io.o
