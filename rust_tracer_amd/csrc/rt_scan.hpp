@@ -33,6 +33,11 @@ __device__ unsigned long long rt_scan_stats[16];
 #endif
 
 typedef float f2 __attribute__((ext_vector_type(2)));
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(3))) float4 lfloat4;
+#else
+typedef const float4 lfloat4;
+#endif
 
 __device__ __forceinline__ f2 bc(float x) { return f2{x, x}; }
 
@@ -332,6 +337,21 @@ __device__ __forceinline__ unsigned long long* ops_slot(const DevScene& S) {
 // ------------------------------------------------------------------ linear runs
 // Group loops prefetch record i+1 before testing record i; every section is padded by
 // one group so the look-ahead load stays inside the allocation.
+// The hierarchy's sphere pairs staged in LDS by the walk kernels (ldsph: their copy of
+// records [0, n_dsph_bvh), which every hierarchy leaf's run lies in): every lane reads the
+// same address (a broadcast) and the packed tests take the record from VGPRs.  No misses,
+// unlike the scalar data cache, which the light-buffer copies and the rest of the scene
+// share (+1.4%; reading the next record ahead, or moving it to SGPRs by readfirstlane, lost).
+__device__ __forceinline__ SphPair ld_sph_l(lfloat4* p) { return SphPair{p[0], p[1], p[2], p[3]}; }
+template <class C>
+__device__ __forceinline__ void run_dsph_lds(int b, int e, V3 o, V3 d, float& bt, uint32_t& bk, C& c,
+                                             lfloat4* ldsph) {
+    lfloat4* p = ldsph + 4 * b;
+    for (int i = b; i < e; ++i, p += 4) {
+        RT_OPS(c, dsph);
+        sph_pair(ld_sph_l(p), o, d, bt, bk);
+    }
+}
 template <class C>
 __device__ __forceinline__ void run_dsph(const DevScene& S, int b, int e, V3 o, V3 d, float& bt, uint32_t& bk,
                                          C& c) {
@@ -492,10 +512,13 @@ typedef const uint4 cuint4;
 // One leaf: its runs of pairs / general spheres / triangle pairs / cubes.
 template <class C>
 __device__ __forceinline__ void bvh_leaf(const DevScene& S, uint32_t li, V3 o, V3 d, float on, float tmax,
-                                         float& bt, uint32_t& bk, C& c) {
+                                         float& bt, uint32_t& bk, C& c, lfloat4* ldsph = nullptr) {
     cuint4* lp = (cuint4*)S.bvh_leaves + 2 * li;
     uint4 a = lp[0], b = lp[1];
-    run_dsph(S, (int)a.x, (int)a.y, o, d, bt, bk, c);
+    if (ldsph)  // a hierarchy leaf, in a kernel that staged the sphere pairs
+        run_dsph_lds((int)a.x, (int)a.y, o, d, bt, bk, c, ldsph);
+    else
+        run_dsph(S, (int)a.x, (int)a.y, o, d, bt, bk, c);
     run_gsph(S, (int)a.z, (int)a.w, o, d, bt, bk, c);
     run_tri(S, (int)b.x, (int)b.y, o, d, bt, bk, c);
     if (b.z < b.w) {
@@ -516,12 +539,12 @@ __device__ __forceinline__ bool shadow_decided(V3 o, V3 d, float bt, float l2) {
 
 // Walk the hierarchy.  SHADOW: t_max also stops at the light (tlim) and decided lanes
 // stop voting; the walk ends when every lane is decided.
-#if defined(__HIP_DEVICE_COMPILE__)
-typedef const __attribute__((address_space(3))) float4 lfloat4;
-#else
-typedef const float4 lfloat4;
-#endif
 
+// The LDS of the walk kernels' LDS variant: node records, then the grazing pairs' normals
+// (per-lane grazing sets), then the hierarchy's sphere pairs
+__device__ __forceinline__ lfloat4* lds_dsph(const DevScene& S, lfloat4* lnodes) {
+    return lnodes + 4 * S.n_bvh_nodes + ((S.graze_lane && S.graze_res) ? 8 * S.n_graze_blk : 0);
+}
 // LDS: node records staged in LDS by the kernel (lnodes != null), else read via SMEM
 // novote (shadow): the lane's hierarchy primitives are settled already (light buffer).
 template <bool SHADOW, bool LDS, class C>
@@ -559,7 +582,7 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
                 }
             }
 #endif
-            bvh_leaf(S, cur & ~BVH_LEAF, o, d, R.on, tmax, bt, bk, c);
+            bvh_leaf(S, cur & ~BVH_LEAF, o, d, R.on, tmax, bt, bk, c, LDS ? lds_dsph(S, lnodes) : nullptr);
             RT_T1(C, c, cyc_leaf, t_it);
             if (SHADOW) {
                 done = novote || shadow_decided(o, d, bt, l2);

@@ -309,6 +309,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         if (S.graze_lane && S.graze_res)
             for (int i = threadIdx.x; i < 8 * S.n_graze_blk; i += blockDim.x)
                 rt_dyn_lds[4 * S.n_bvh_nodes + i] = S.graze_pn[i];
+        // ... then the hierarchy's sphere pairs (rt_scan.hpp run_dsph_lds)
+        {
+            float4* dst = rt_dyn_lds + 4 * S.n_bvh_nodes + ((S.graze_lane && S.graze_res) ? 8 * S.n_graze_blk : 0);
+            for (int i = threadIdx.x; i < 4 * S.n_dsph_bvh; i += blockDim.x) dst[i] = S.dsph[i];
+        }
         __syncthreads();
     }
     lfloat4* lnodes = (lfloat4*)rt_dyn_lds;
@@ -678,6 +683,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
         if (S.graze_lane && S.graze_res)
             for (int i = threadIdx.x; i < 8 * S.n_graze_blk; i += blockDim.x)
                 rt_dyn_lds[4 * S.n_bvh_nodes + i] = S.graze_pn[i];
+        // ... then the hierarchy's sphere pairs (rt_scan.hpp run_dsph_lds)
+        {
+            float4* dst = rt_dyn_lds + 4 * S.n_bvh_nodes + ((S.graze_lane && S.graze_res) ? 8 * S.n_graze_blk : 0);
+            for (int i = threadIdx.x; i < 4 * S.n_dsph_bvh; i += blockDim.x) dst[i] = S.dsph[i];
+        }
         __syncthreads();
     }
     lfloat4* lnodes = (lfloat4*)rt_dyn_lds;
@@ -1006,17 +1016,19 @@ hipError_t wave_occupancy(int* trace_blocks, int* shadow_blocks, int* combine_bl
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(combine_blocks, combine_level_kernel, 256, 0);
 }
 
-// hierarchy node records staged in LDS when they fit (RT_LDS_NODES=0: never; =trace /
-// =shadow: only that kernel, A/B)
-// LDS bytes of the staged records: node records, then the grazing pairs' normals
+// The walk kernels' LDS variant stages the hierarchy's node records, the grazing pairs'
+// normals and the hierarchy's sphere pairs when they fit in 32 KB (five 256-thread blocks
+// per CU, the trace and shadow kernels' VGPR limit); RT_LDS_NODES=0: never, =trace /
+// =shadow: only that kernel (A/B)
 static size_t lds_bytes(const WaveParams& p) {
-    return (size_t)p.S.n_bvh_nodes * 64 + ((p.S.graze_lane && p.S.graze_res) ? (size_t)p.S.n_graze_blk * 128 : 0);
+    return (size_t)p.S.n_bvh_nodes * 64 + ((p.S.graze_lane && p.S.graze_res) ? (size_t)p.S.n_graze_blk * 128 : 0) +
+           (size_t)p.S.n_dsph_bvh * 64;
 }
 static bool lds_nodes_for(const WaveParams& p, const char* kernel) {
     size_t lds = lds_bytes(p);
     const char* e = getenv("RT_LDS_NODES");
     if (e && (e[0] == '0' || (std::strcmp(e, "1") != 0 && std::strcmp(e, kernel) != 0))) return false;
-    return p.S.use_bvh && lds > 0 && lds <= 36 * 1024;
+    return p.S.use_bvh && lds > 0 && lds <= 32 * 1024;
 }
 
 hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream) {
