@@ -376,7 +376,8 @@ def main():
         t.scene.sync_status()
     if seam is not None:
         seam["scene_create_ms"] = round(scene_create_ms, 2)
-        elapsed, kernel_ms_max = stats.tolist()
+    # the whole job's time: the slowest rank's timed region (max over ranks)
+    elapsed, kernel_ms_max = stats.tolist()
     node_rays, shadow_rays, pixels = cnt.tolist()
 
     if rank == 0:
