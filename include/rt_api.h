@@ -201,7 +201,7 @@ rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* camera,
                                 uint32_t world, float* d_rgb, uint64_t* d_counters,
                                 void* stream);
 
-/* Frame batch: n_frames (1..4) frames of one resolution, each with its own camera, in one
+/* Frame batch: n_frames (1..8) frames of one resolution, each with its own camera, in one
  * pipeline pass (the per-level launch and latency floor is paid once per batch; the frame
  * index sits above every queue-key bit, so frames stay contiguous in the sorted queues --
  * an ordering property only; level 0 is frame-uniform per wave).  d_rgb holds n_frames
@@ -213,7 +213,7 @@ rt_status rt_render_bands_batch_async(const rt_scene* scene, const rt_camera* ca
                                       float* d_rgb, uint64_t* d_counters, void* stream);
 
 /* The general stream-ordered render (every *_async render above is a special case of it):
- * n_frames (1..4) frames of one resolution, each with its own camera, spp jittered samples
+ * n_frames (1..8) frames of one resolution, each with its own camera, spp jittered samples
  * per pixel (spp > 1 needs n_frames == 1), this rank's row bands (as rt_render_bands_async).
  *  - d_rgb:  n_frames band buffers of f32 RGB (may be NULL when spp == 1 and d_rgb8 is set:
  *            then only the bytes are written);
