@@ -61,7 +61,7 @@ def parse():
     p.add_argument("--seed", type=int, default=None, help="jitter seed (default: 3 for config 5)")
     p.add_argument("--band-rows", type=int, default=8)
     p.add_argument("--batch", type=int, default=None,
-                   help="frames per pipeline pass (rt_render_bands_batch_async, <= 8; default: 2 for a "
+                   help="frames per pipeline pass (rt_render_bands_batch_async, <= 8; default: 5 for a "
                         "1080p frame per GPU, 1 for larger shares or spp > 1, else up to 8 while a pass "
                         "stays within 4 x 1080p of pixels per rank)")
     p.add_argument("--inflight", type=int, default=None,
@@ -287,13 +287,14 @@ def main():
     if args.batch is None:
         # N > 1 shares are latency-bound: up to 8 frames per pass (bounded workspace: <= 4 x
         # 1080p of pixels per pass and rank; 8 vs 4 frames: -9% / -6% / -3% ms per share-frame
-        # at N = 8 / 4 / 2); a whole 1080p frame per GPU renders 2 frames per pass (+1.8% over
-        # 1 and over 4 at 4 passes in flight; DESIGN.md "Frame batches")
+        # at N = 8 / 4 / 2); a whole 1080p frame per GPU renders 5 frames per pass (4 passes in
+        # flight, ~25 GB of workspace per pass: 885 vs 851 Mpixels/s at 2 frames per pass over
+        # 160 frames, 888 vs 840 over 20; DESIGN.md "Frame batches")
         share = band_rows_per_rank(args.height, args.band_rows, world) * args.width
         if args.spp > 1:
             args.batch = 1
         elif world == 1:
-            args.batch = 2 if share <= 1920 * 1088 else 1
+            args.batch = 5 if share <= 1920 * 1088 else 1
         else:
             args.batch = max(1, min(8, (4 * 1920 * 1088) // share))
     pipe = FramePipeline(scene, desc, args.width, args.height, args.depth, args.band_rows, rank, world, dev,
