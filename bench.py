@@ -61,9 +61,10 @@ def parse():
     p.add_argument("--seed", type=int, default=None, help="jitter seed (default: 3 for config 5)")
     p.add_argument("--band-rows", type=int, default=8)
     p.add_argument("--batch", type=int, default=None,
-                   help="frames per pipeline pass (rt_render_bands_batch_async, <= 8; default: 5 for a "
-                        "1080p frame per GPU, 1 for larger shares or spp > 1, else up to 8 while a pass "
-                        "stays within 4 x 1080p of pixels per rank)")
+                   help="frames per pipeline pass (rt_render_bands_batch_async, <= 8; default: the timed "
+                        "frames spread evenly over the slots, ceil(steps / inflight), capped at 5 for a "
+                        "1080p frame per GPU, 1 for larger shares or spp > 1, else 8 while a pass stays "
+                        "within 4 x 1080p of pixels per rank)")
     p.add_argument("--inflight", type=int, default=None,
                    help="frames in flight (F scene handles / HIP streams; default 4 = the box's hardware "
                         "queues per process); 1 = one at a time")
@@ -285,18 +286,20 @@ def main():
     scene_create_ms = (time.perf_counter() - t_sc) * 1e3
     inflight = max(1, args.inflight or 4)
     if args.batch is None:
-        # N > 1 shares are latency-bound: up to 8 frames per pass (bounded workspace: <= 4 x
-        # 1080p of pixels per pass and rank; 8 vs 4 frames: -9% / -6% / -3% ms per share-frame
-        # at N = 8 / 4 / 2); a whole 1080p frame per GPU renders 5 frames per pass (4 passes in
-        # flight, ~25 GB of workspace per pass: 885 vs 851 Mpixels/s at 2 frames per pass over
-        # 160 frames, 888 vs 840 over 20; DESIGN.md "Frame batches")
+        # The timed K frames are spread evenly over the F slots: B = ceil(K / F) frames per
+        # pass, capped.  N > 1 shares are latency-bound: up to 8 frames per pass (bounded
+        # workspace: <= 4 x 1080p of pixels per pass and rank); a whole 1080p frame per GPU
+        # up to 5 (~25 GB of workspace per slot).  K = 20, ms per share-frame on one MI355X
+        # (tools/share_burst.py): N = 1: B = 2 / 4 / 5 / 8: 2.46 / 2.51 / 2.31 / 2.36; N = 8:
+        # 0.533 / 0.464 / 0.389 / 0.381 (DESIGN.md "Frame batches")
         share = band_rows_per_rank(args.height, args.band_rows, world) * args.width
         if args.spp > 1:
-            args.batch = 1
+            cap = 1
         elif world == 1:
-            args.batch = 5 if share <= 1920 * 1088 else 1
+            cap = 5 if share <= 1920 * 1088 else 1
         else:
-            args.batch = max(1, min(8, (4 * 1920 * 1088) // share))
+            cap = max(1, min(8, (4 * 1920 * 1088) // share))
+        args.batch = max(1, min(cap, -(-args.steps // inflight)))
     pipe = FramePipeline(scene, desc, args.width, args.height, args.depth, args.band_rows, rank, world, dev,
                          spp=args.spp, seed=args.seed, inflight=inflight, batch=args.batch,
                          rgb8=args.output == "rgb8")
