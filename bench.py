@@ -223,7 +223,7 @@ def seam_stats(args, scene, pipe, tiler, dev):
             return c
         pipe.run(pipe.inflight * pipe.batch, cameras=cam)
         torch.cuda.synchronize()
-        k = 12
+        k = pipe.inflight * pipe.batch  # whole passes on every slot, as the headline's K frames
         e0.record(main)
         pipe.run(k, cameras=cam)
         e1.record(main)
@@ -236,7 +236,7 @@ def seam_stats(args, scene, pipe, tiler, dev):
             t.depth = 9
         pipe.run(pipe.inflight * pipe.batch)
         torch.cuda.synchronize()
-        k = 10
+        k = pipe.inflight * pipe.batch
         e0.record(main)
         pipe.run(k)
         e1.record(main)
