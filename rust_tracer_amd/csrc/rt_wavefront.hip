@@ -672,7 +672,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
 // a bit in the node record.
 
 #ifndef RT_SHADOW_WAVES
-#define RT_SHADOW_WAVES 5  // 96 VGPRs (measured: 4 -> 8.36 ms, 5 -> 8.04, 6 -> 11.2 with spills)
+#define RT_SHADOW_WAVES 6  // 80 VGPRs, 48 B scratch: +0.5 - 1% over 5 (96 VGPRs) at 20 frames in flight; 7 / 8: -2% / -4.5%
 #endif
 template <bool LDS, bool COUNT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_WAVES, 8))) void shadow_kernel(WaveParams P) {
