@@ -299,7 +299,9 @@ __device__ __forceinline__ void own_shape_test(const DevScene& S, uint32_t key, 
 #endif
 extern __shared__ float4 rt_dyn_lds[];
 
-template <bool COUNT, bool LDS>
+// DEEP: a level past the pixels and the inline shadow scans (level >= max(1, inline_levels)):
+// the instantiation without their code (fewer live registers across the walk)
+template <bool COUNT, bool LDS, bool DEEP = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES, 8))) void trace_level_kernel(
     WaveParams P, uint32_t level) {
     const DevScene& S = P.S;
@@ -373,7 +375,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
         uint32_t parent = 0, pix = 0, in_shape = 0;
         const uint32_t n = off + t;
         if (active) {
-            if (level == 0) {
+            if (!DEEP && level == 0) {
                 const uint32_t fr = P.frames > 1 ? t / P.frame_items : 0u;
                 PixelRef px = pixel_of(P, t - fr * P.frame_items);
                 if (!px.valid) {
@@ -580,7 +582,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WA
                 }
                 n_pre += (uint32_t)__builtin_popcount(decided);
             }
-            if (level < P.inline_levels) {  // the level's remaining shadow rays, right here
+            if (!DEEP && level < P.inline_levels) {  // the level's remaining shadow rays, right here
                 for (int li = 0; li < S.n_lights; ++li) {
                     const LightRec& L = S.lights[li];
                     if (L.kind != RT_LIGHT_POINT || ((decided >> li) & 1u)) continue;
@@ -1034,11 +1036,19 @@ static bool lds_nodes_for(const WaveParams& p, const char* kernel) {
 hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream) {
     const size_t lds = lds_bytes(p);
     const bool use = lds_nodes_for(p, "trace");
+    // the deep instantiation past level 0 and the inline shadow levels (RT_DEEP_KERNEL=0: never, A/B)
+    static const bool deep_ok = !(getenv("RT_DEEP_KERNEL") && getenv("RT_DEEP_KERNEL")[0] == '0');
+    const bool deep = deep_ok && level > 0 && level >= p.inline_levels && !(p.count_mask & 1u);
     if (p.count_mask & 1u) {
         if (use)
             hipLaunchKernelGGL((trace_level_kernel<true, true>), dim3(blocks), dim3(256), lds, stream, p, level);
         else
             hipLaunchKernelGGL((trace_level_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, p, level);
+    } else if (deep) {
+        if (use)
+            hipLaunchKernelGGL((trace_level_kernel<false, true, true>), dim3(blocks), dim3(256), lds, stream, p, level);
+        else
+            hipLaunchKernelGGL((trace_level_kernel<false, false, true>), dim3(blocks), dim3(256), 0, stream, p, level);
     } else {
         if (use)
             hipLaunchKernelGGL((trace_level_kernel<false, true>), dim3(blocks), dim3(256), lds, stream, p, level);
