@@ -301,8 +301,11 @@ extern __shared__ float4 rt_dyn_lds[];
 
 // DEEP: a level past the pixels and the inline shadow scans (level >= max(1, inline_levels)):
 // the instantiation without their code (fewer live registers across the walk)
+#ifndef RT_DEEP_WAVES
+#define RT_DEEP_WAVES RT_TRACE_WAVES
+#endif
 template <bool COUNT, bool LDS, bool DEEP = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES, 8))) void trace_level_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_DEEP_WAVES : RT_TRACE_WAVES, 8))) void trace_level_kernel(
     WaveParams P, uint32_t level) {
     const DevScene& S = P.S;
     if (LDS) {  // stage the hierarchy's node records in LDS
