@@ -300,11 +300,12 @@ __device__ __forceinline__ void own_shape_test(const DevScene& S, uint32_t key, 
 extern __shared__ float4 rt_dyn_lds[];
 
 // DEEP: a level past the pixels and the inline shadow scans (level >= max(1, inline_levels)):
-// the instantiation without their code (fewer live registers across the walk)
+// the instantiation without their code (fewer live registers across the walk).  FIRST:
+// level 0 only (its rays start at the camera: no task loads, no ray inside a shape).
 #ifndef RT_DEEP_WAVES
 #define RT_DEEP_WAVES RT_TRACE_WAVES
 #endif
-template <bool COUNT, bool LDS, bool DEEP = false>
+template <bool COUNT, bool LDS, bool DEEP = false, bool FIRST = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_DEEP_WAVES : RT_TRACE_WAVES, 8))) void trace_level_kernel(
     WaveParams P, uint32_t level) {
     const DevScene& S = P.S;
@@ -378,7 +379,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         uint32_t parent = 0, pix = 0, in_shape = 0;
         const uint32_t n = off + t;
         if (active) {
-            if (!DEEP && level == 0) {
+            if (FIRST || (!DEEP && level == 0)) {
                 const uint32_t fr = P.frames > 1 ? t / P.frame_items : 0u;
                 PixelRef px = pixel_of(P, t - fr * P.frame_items);
                 if (!px.valid) {
@@ -442,7 +443,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
             uint32_t bk = 0xFFFFFFFFu;
             bool buf_ok = false;
             uint32_t buf_leaf = 0;
-            if (in_shape) {  // the enclosing sphere first: its exit point bounds the walk from the start
+            if (!FIRST && in_shape) {  // the enclosing sphere first: its exit point bounds the walk from the start
                 const ShapeRec& R = S.shapes[in_shape - 1u];
                 if (R.kind == RT_SHAPE_SPHERE) {
                     RT_OPS(cnt, gsph);
@@ -460,7 +461,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                     }
                 }
             }
-            scan_buffered<LDS>(S, ro, rd, bt, bk, cnt, lnodes, buf_ok, buf_leaf);
+            if (FIRST)
+                scan_from<LDS>(S, ro, rd, bt, bk, cnt, lnodes);
+            else
+                scan_buffered<LDS>(S, ro, rd, bt, bk, cnt, lnodes, buf_ok, buf_leaf);
             if (bk == 0xFFFFFFFFu) {
                 // trace_ray -> BLACK: the parent's child slot gets BLACK (forest: direction 0)
                 P.node_flags[n] = NODE_MISS;
@@ -1047,6 +1051,11 @@ hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hi
             hipLaunchKernelGGL((trace_level_kernel<true, true>), dim3(blocks), dim3(256), lds, stream, p, level);
         else
             hipLaunchKernelGGL((trace_level_kernel<true, false>), dim3(blocks), dim3(256), 0, stream, p, level);
+    } else if (level == 0 && deep_ok) {
+        if (use)
+            hipLaunchKernelGGL((trace_level_kernel<false, true, false, true>), dim3(blocks), dim3(256), lds, stream, p, level);
+        else
+            hipLaunchKernelGGL((trace_level_kernel<false, false, false, true>), dim3(blocks), dim3(256), 0, stream, p, level);
     } else if (deep) {
         if (use)
             hipLaunchKernelGGL((trace_level_kernel<false, true, true>), dim3(blocks), dim3(256), lds, stream, p, level);
