@@ -829,7 +829,11 @@ __device__ __forceinline__ V3 light_sum(const DevScene& S, const MatRec& M, cons
 }
 
 // render.rs:57-68 + :100 for every node of `level`; children (level + 1) already reported.
-__global__ __launch_bounds__(256) void combine_level_kernel(WaveParams P, uint32_t level) {
+#ifndef RT_COMBINE_WAVES
+#define RT_COMBINE_WAVES 5
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_COMBINE_WAVES, 8))) void combine_level_kernel(
+    WaveParams P, uint32_t level) {
     const DevScene& S = P.S;
     const uint32_t off = P.levels[2 * level];
     const uint32_t count = min(P.levels[2 * level + 1], off < P.capacity ? P.capacity - off : 0u);
