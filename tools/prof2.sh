@@ -12,7 +12,7 @@ cat /sys/fs/cgroup/cpu.max > $OUT/cpu_max.txt 2>/dev/null
 timeout -k 10 300 python bench.py --steps 20 --warmup 4 $B "$@" > $OUT/bench.json 2> $OUT/bench.err || exit 1
 timeout -k 10 300 python bench.py --steps 10 --warmup 2 --inflight 1 --batch 1 $B "$@" > $OUT/bench1.json 2> $OUT/bench1.err || exit 2
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-    python bench.py --steps 12 --warmup 4 $B --count-frame 0 "$@" > $OUT/trace.log 2>&1 || exit 3
+    python bench.py --steps 20 --warmup 4 $B --count-frame 0 "$@" > $OUT/trace.log 2>&1 || exit 3
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace1 -o run -- \
     python bench.py --steps 6 --warmup 1 --inflight 1 --batch 1 $B --count-frame 0 "$@" > $OUT/trace1.log 2>&1 || exit 4
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- \

@@ -70,7 +70,7 @@ def main():
     # trace runs: warmup + slot set-up + steps frames; divide by all frames rendered
     f4 = bench["config"]["frames_in_flight"]
     # slot set-up (inflight x batch frames) + warm-up + timed frames
-    t4, f_t4, _ = trace_table(os.path.join(src, "trace"), 12 + 4 + f4)
+    t4, f_t4, _ = trace_table(os.path.join(src, "trace"), 20 + 4 + f4)  # tools/prof2.sh: --steps 20 --warmup 4
     t1, f_t1, _ = trace_table(os.path.join(src, "trace1"), 6 + 1 + 1)
     out += ["## rocprofv3 --kernel-trace (ms of kernel time per frame)", "",
             f"| kernel | {f4} frames in flight ({bench['config']['passes_in_flight']} passes x "
