@@ -264,6 +264,18 @@ rt_status rt_unpermute_bands_async(const float* d_gathered, uint32_t x_res, uint
 rt_status rt_unpermute_bands_u8_async(const uint8_t* d_gathered, uint32_t x_res, uint32_t y_res,
                                       uint32_t band_rows, uint32_t world, uint8_t* d_frame, void* stream);
 
+/* A gathered frame batch in one launch: d_gathered holds, per rank, stride_frames band
+ * buffers of which the first n_frames are filled (rank-major: rank r's buffer of frame f
+ * is the (r * stride_frames + f)-th buffer of rt_band_rows_per_rank rows) -- what one
+ * gather of every rank's rt_render_bands_batch_async output gives; frame f lands at
+ * d_frames + f * y_res * x_res * 3. */
+rt_status rt_unpermute_bands_batch_async(const float* d_gathered, uint32_t x_res, uint32_t y_res,
+                                         uint32_t band_rows, uint32_t world, uint32_t n_frames,
+                                         uint32_t stride_frames, float* d_frames, void* stream);
+rt_status rt_unpermute_bands_batch_u8_async(const uint8_t* d_gathered, uint32_t x_res, uint32_t y_res,
+                                            uint32_t band_rows, uint32_t world, uint32_t n_frames,
+                                            uint32_t stride_frames, uint8_t* d_frames, void* stream);
+
 /* Saves a row-major RGB8 frame (Color::as_u8 values) as PNG, BMP or PPM, chosen by the
  * file extension (.png default) -- bmp.rs:8-19 / main.rs:71-74 (host code). */
 rt_status rt_write_image(const char* path, const uint8_t* rgb8, uint32_t x_res, uint32_t y_res);

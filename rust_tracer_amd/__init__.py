@@ -457,6 +457,15 @@ def unpermute_bands_u8_async(d_gathered_ptr, x_res, y_res, band_rows, world, d_f
           "rt_unpermute_bands_u8_async")
 
 
+def unpermute_bands_batch_async(d_gathered_ptr, x_res, y_res, band_rows, world, n_frames, stride_frames,
+                                d_frames_ptr, stream_ptr, rgb8=False):
+    """rt_unpermute_bands_batch_async (_u8 with rgb8): n_frames frames of one gather of every
+    rank's batch band buffers (stride_frames buffers per rank) into consecutive frames."""
+    f = lib().rt_unpermute_bands_batch_u8_async if rgb8 else lib().rt_unpermute_bands_batch_async
+    check(f(C.c_void_p(d_gathered_ptr), x_res, y_res, band_rows, world, n_frames, stride_frames,
+            C.c_void_p(d_frames_ptr), C.c_void_p(stream_ptr)), "rt_unpermute_bands_batch_async")
+
+
 def quantize_u8_async(d_rgb_ptr, n, d_rgb8_ptr, stream_ptr):
     check(lib().rt_quantize_u8_async(C.c_void_p(d_rgb_ptr), n, C.c_void_p(d_rgb8_ptr),
                                      C.c_void_p(stream_ptr)), "rt_quantize_u8_async")

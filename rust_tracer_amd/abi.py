@@ -137,6 +137,8 @@ def lib():
     L.rt_scene_uses_rccl.argtypes = [vp]
     L.rt_scene_uses_rccl.restype = C.c_int32
     L.rt_unpermute_bands_u8_async.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp]
+    for f in (L.rt_unpermute_bands_batch_async, L.rt_unpermute_bands_batch_u8_async):
+        f.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp]
     L.rt_band_rows_per_rank.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
     L.rt_band_rows_per_rank.restype = C.c_uint32
     L.rt_unpermute_bands_async.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,

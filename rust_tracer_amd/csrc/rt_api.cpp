@@ -28,10 +28,12 @@ namespace rtdev {
 hipError_t launch_render(const RenderParams& p, int blocks, hipStream_t stream);
 hipError_t render_occupancy(uint32_t depth, int* blocks_per_cu);
 hipError_t launch_unpermute(const float* in, uint32_t x_res, uint32_t y_res, uint32_t band_rows,
-                            uint32_t world, uint32_t rows_per_rank, float* out, hipStream_t stream);
+                            uint32_t world, uint32_t rows_per_rank, float* out, hipStream_t stream,
+                            uint32_t frames = 1, uint32_t rank_rows = 0);
 hipError_t launch_quantize(const float* in, size_t n, uint8_t* out, hipStream_t stream);
 hipError_t launch_unpermute_u8(const uint8_t* in, uint32_t x_res, uint32_t y_res, uint32_t band_rows,
-                               uint32_t world, uint32_t rows_per_rank, uint8_t* out, hipStream_t stream);
+                               uint32_t world, uint32_t rows_per_rank, uint8_t* out, hipStream_t stream,
+                               uint32_t frames = 1, uint32_t rank_rows = 0);
 bool rt_cube_table_check(const float* table);
 hipError_t wave_occupancy(int* trace_blocks, int* shadow_blocks, int* combine_blocks);
 hipError_t launch_wave_shadow(const WaveParams& p, int blocks, hipStream_t stream);
@@ -2068,6 +2070,30 @@ rt_status rt_unpermute_bands_u8_async(const uint8_t* d_gathered, uint32_t x_res,
         return RT_ERR_INVALID_ARG;
     uint32_t rpr = rt_band_rows_per_rank(y_res, band_rows, world);
     HIP_TRY(launch_unpermute_u8(d_gathered, x_res, y_res, band_rows, world, rpr, d_frame, (hipStream_t)stream));
+    return RT_OK;
+}
+
+rt_status rt_unpermute_bands_batch_async(const float* d_gathered, uint32_t x_res, uint32_t y_res,
+                                         uint32_t band_rows, uint32_t world, uint32_t n_frames,
+                                         uint32_t stride_frames, float* d_frames, void* stream) {
+    if (!d_gathered || !d_frames || band_rows == 0 || world == 0 || x_res == 0 || y_res == 0 || n_frames == 0 ||
+        stride_frames < n_frames || n_frames > 65535u)
+        return RT_ERR_INVALID_ARG;
+    const uint32_t rpr = rt_band_rows_per_rank(y_res, band_rows, world);
+    HIP_TRY(launch_unpermute(d_gathered, x_res, y_res, band_rows, world, rpr, d_frames, (hipStream_t)stream, n_frames,
+                             stride_frames * rpr));
+    return RT_OK;
+}
+
+rt_status rt_unpermute_bands_batch_u8_async(const uint8_t* d_gathered, uint32_t x_res, uint32_t y_res,
+                                            uint32_t band_rows, uint32_t world, uint32_t n_frames,
+                                            uint32_t stride_frames, uint8_t* d_frames, void* stream) {
+    if (!d_gathered || !d_frames || band_rows == 0 || world == 0 || x_res == 0 || y_res == 0 || n_frames == 0 ||
+        stride_frames < n_frames || n_frames > 65535u)
+        return RT_ERR_INVALID_ARG;
+    const uint32_t rpr = rt_band_rows_per_rank(y_res, band_rows, world);
+    HIP_TRY(launch_unpermute_u8(d_gathered, x_res, y_res, band_rows, world, rpr, d_frames, (hipStream_t)stream,
+                                n_frames, stride_frames * rpr));
     return RT_OK;
 }
 

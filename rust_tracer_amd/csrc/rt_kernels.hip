@@ -286,17 +286,21 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
 
 // Scatter gathered per-rank band buffers into the row-major frame (one block row per frame
 // row); T = float (RGB f32) or uint8_t (RGB8, Color::as_u8 values).
+// Frame batches (blockIdx.z = frame f): rank r's bands of frame f start at row
+// r * rank_rows + f * rows_per_rank of `in` (rank_rows = rows_per_rank for one frame), and
+// frame f lands at out + f * height rows.
 template <class T>
 __global__ void unpermute_kernel(const T* __restrict__ in, uint32_t row_floats, uint32_t height,
-                                 uint32_t band_rows, uint32_t world, uint32_t rows_per_rank,
+                                 uint32_t band_rows, uint32_t world, uint32_t rows_per_rank, uint32_t rank_rows,
                                  T* __restrict__ out) {
     uint32_t v = blockIdx.y;
     if (v >= height) return;
+    const uint32_t f = blockIdx.z;
     uint32_t band = v / band_rows;
     uint32_t rank = band % world;
     uint32_t lr = (band / world) * band_rows + (v - band * band_rows);
-    const T* src = in + ((size_t)rank * rows_per_rank + lr) * row_floats;
-    T* dst = out + (size_t)v * row_floats;
+    const T* src = in + ((size_t)rank * rank_rows + (size_t)f * rows_per_rank + lr) * row_floats;
+    T* dst = out + ((size_t)f * height + v) * row_floats;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < row_floats; i += gridDim.x * blockDim.x)
         dst[i] = src[i];
 }
@@ -354,20 +358,22 @@ hipError_t render_occupancy(uint32_t depth, int* blocks_per_cu) {
 }
 
 hipError_t launch_unpermute(const float* in, uint32_t x_res, uint32_t y_res, uint32_t band_rows,
-                            uint32_t world, uint32_t rows_per_rank, float* out, hipStream_t stream) {
+                            uint32_t world, uint32_t rows_per_rank, float* out, hipStream_t stream,
+                            uint32_t frames, uint32_t rank_rows) {
     uint32_t row_floats = x_res * 3u;
-    dim3 grid((row_floats + 255) / 256, y_res);
+    dim3 grid((row_floats + 255) / 256, y_res, frames);
     hipLaunchKernelGGL(unpermute_kernel<float>, grid, dim3(256), 0, stream, in, row_floats, y_res, band_rows, world,
-                       rows_per_rank, out);
+                       rows_per_rank, rank_rows ? rank_rows : rows_per_rank, out);
     return hipGetLastError();
 }
 
 hipError_t launch_unpermute_u8(const uint8_t* in, uint32_t x_res, uint32_t y_res, uint32_t band_rows,
-                               uint32_t world, uint32_t rows_per_rank, uint8_t* out, hipStream_t stream) {
+                               uint32_t world, uint32_t rows_per_rank, uint8_t* out, hipStream_t stream,
+                               uint32_t frames, uint32_t rank_rows) {
     uint32_t row_bytes = x_res * 3u;
-    dim3 grid((row_bytes + 255) / 256, y_res);
+    dim3 grid((row_bytes + 255) / 256, y_res, frames);
     hipLaunchKernelGGL(unpermute_kernel<uint8_t>, grid, dim3(256), 0, stream, in, row_bytes, y_res, band_rows, world,
-                       rows_per_rank, out);
+                       rows_per_rank, rank_rows ? rank_rows : rows_per_rank, out);
     return hipGetLastError();
 }
 

@@ -14,7 +14,7 @@ independent, so the only exchange step is assembling the frame:
 import torch
 import torch.distributed as dist
 
-from . import DeviceScene, abi, band_rows_per_rank, unpermute_bands_async, unpermute_bands_u8_async
+from . import DeviceScene, abi, band_rows_per_rank, unpermute_bands_batch_async
 
 
 def band_rows_per_rank_py(y_res, band_rows, world):
@@ -61,7 +61,8 @@ class FrameTiler:
         self.gathered = None
         self.frames = None          # [batch, H, W, 3]: the last pass's assembled frames (rank 0)
         if rank == 0 and world > 1:
-            self.gathered = torch.zeros((world, self.rpr, width, 3), dtype=dt, device=self.device)
+            # one gather per pass: every rank's `batch` band buffers, rank-major
+            self.gathered = torch.zeros((world, self.batch, self.rpr, width, 3), dtype=dt, device=self.device)
             self.frames = torch.zeros((self.batch, height, width, 3), dtype=dt, device=self.device)
         elif world == 1:
             self.frames = self.locals[:, :height]
@@ -88,28 +89,29 @@ class FrameTiler:
                                                 stream)
 
     def assemble(self):
-        """Gather every rank's bands of the last pass's frames on rank 0 and restore row
-        order (no-op at world 1)."""
+        """Gather every rank's bands of the last pass's frames on rank 0 -- one gather for the
+        whole pass -- and restore row order, every frame of the pass in one launch (no-op at
+        world 1)."""
         if self.world == 1:
             return self.frame
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        for b in range(self.last):
-            local = self.locals[b]
-            if dist.get_backend() == "gloo":
-                # CPU rehearsal of the exchange (several ranks sharing one GPU); RCCL runs
-                # the same gather directly on device buffers
-                host = local.cpu()
-                glist = [torch.empty_like(host) for _ in range(self.world)] if self.rank == 0 else None
-                dist.gather(host, gather_list=glist, dst=0)
-                if self.rank == 0:
-                    self.gathered.copy_(torch.stack(glist))
-            else:
-                glist = list(self.gathered.unbind(0)) if self.rank == 0 else None
-                dist.gather(local, gather_list=glist, dst=0)
+        n = self.last
+        local = self.locals[:n]
+        if dist.get_backend() == "gloo":
+            # CPU rehearsal of the exchange (several ranks sharing one GPU); RCCL runs the
+            # same gather directly on device buffers
+            host = local.cpu()
+            glist = [torch.empty_like(host) for _ in range(self.world)] if self.rank == 0 else None
+            dist.gather(host, gather_list=glist, dst=0)
             if self.rank == 0:
-                unpermute = unpermute_bands_u8_async if self.rgb8 else unpermute_bands_async
-                unpermute(self.gathered.data_ptr(), self.w, self.h, self.band_rows, self.world,
-                          self.frames[b].data_ptr(), stream)
+                for r in range(self.world):
+                    self.gathered[r, :n].copy_(glist[r])
+        else:
+            glist = [self.gathered[r, :n] for r in range(self.world)] if self.rank == 0 else None
+            dist.gather(local, gather_list=glist, dst=0)
+        if self.rank == 0:
+            unpermute_bands_batch_async(self.gathered.data_ptr(), self.w, self.h, self.band_rows, self.world, n,
+                                        self.batch, self.frames.data_ptr(), stream, rgb8=self.rgb8)
         return self.frame
 
     def step(self):
