@@ -1799,6 +1799,13 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     if (frames > 1) {  // the frame index above every key bit: frames are contiguous in sorted queues (ordering only)
         uint32_t fbits = 0;
         while ((1u << fbits) < frames) fbits++;
+        // a batch's task keys take 3 radix passes of 8 bits anyway: key mode 7 fills them with
+        // 5 more origin bits (RT_TASK_FINE=0: off, A/B)
+        const char* tf = std::getenv("RT_TASK_FINE");
+        if (!(tf && tf[0] == '0') && p.key_mode == 7 && task_bits == 16u && fbits >= 1 && fbits <= 3) {
+            p.task_fine = 1u;
+            task_bits = 21u;
+        }
         p.task_frame_shift = task_bits;
         p.shadow_frame_shift = shadow_bits;
         task_bits += fbits;

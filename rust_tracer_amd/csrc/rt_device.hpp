@@ -195,6 +195,7 @@ struct WaveParams {
     uint32_t frames;                   // frames in this pass (1: rt_render_bands_async)
     uint32_t frame_items;              // level-0 items per frame (total_items / frames)
     uint32_t task_frame_shift;         // task key |= frame << this (frames > 1)
+    uint32_t task_fine;                // key mode 7 with 5 more origin bits (a batch's 3 radix passes have room)
     uint32_t shadow_frame_shift;       // shadow key |= frame << this (frames > 1)
     size_t frame_floats;               // output floats per frame (rows_local x width x 3)
     FrameCam cams[RT_MAX_FRAMES];      // frames > 1: each frame's camera (render.rs:155-186)

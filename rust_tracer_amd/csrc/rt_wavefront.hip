@@ -113,6 +113,11 @@ __device__ __forceinline__ uint32_t morton21(const DevScene& S, V3 p) {
 }
 
 // task ordering key: 16 bits (modes 0-2) or 24 bits (mode 3)
+// key of a ray inside a sphere / cube (key mode 7): the flag above the outside keys' bits |
+// the shape's centre (15-bit Morton)
+__device__ __forceinline__ uint32_t inside_key(const WaveParams& P, uint32_t center_key) {
+    return P.task_fine ? (1u << 20) | (center_key << 5) : (1u << 15) | center_key;
+}
 __device__ __forceinline__ uint32_t task_key(const WaveParams& P, V3 o, V3 d) {
     if (P.key_mode == 0) return (octant(d) << 13) | (morton15(P.S, o) >> 2);  // 16 bits: 2 radix passes
     // cube-map face of d (3 bits) x 2x2 cells of the face (2 bits) | 13-bit coarse origin
@@ -127,7 +132,10 @@ __device__ __forceinline__ uint32_t task_key(const WaveParams& P, V3 o, V3 d) {
         const V3 q = add(o, mul(d, ahead));
         uint32_t cu = u > 0.f ? 1u : 0u, cv = v > 0.f ? 1u : 0u;
         uint32_t dir = (face << 2) | (cu << 1) | cv;
-        if (P.key_mode == 7) return (dir << 10) | (morton15(P.S, q) >> 5);  // 15 bits: bit 15 marks inside rays
+        if (P.key_mode == 7) {  // 15 bits (20 when task_fine): the bit above marks inside rays
+            if (P.task_fine) return (dir << 15) | morton15(P.S, q);
+            return (dir << 10) | (morton15(P.S, q) >> 5);
+        }
         return (dir << 11) | (morton15(P.S, q) >> 4);
     }
     if (P.key_mode >= 3) {  // face x 8x8 cells (< 384) and the 15-bit Morton origin
@@ -537,7 +545,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 Task T = {rro.x, rro.y, rro.z, rrd.x, rrd.y, rrd.z, (n << 1) | 0u, refl_in ? cpix | (own + 1u) : cpix};
                 P.tasks[slot] = T;
                 if (P.task_keys)
-                    P.task_keys[slot] = (refl_in ? (1u << 15) | S.shapes[own].center_key : task_key(P, rro, rrd)) | fkey;
+                    P.task_keys[slot] = (refl_in ? inside_key(P, S.shapes[own].center_key) : task_key(P, rro, rrd)) | fkey;
                 hit_flags |= F_HAS_R;
             } else {
                 atomicOr(P.overflow, 1u);
@@ -550,7 +558,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 Task T = {tro.x, tro.y, tro.z, trd.x, trd.y, trd.z, (n << 1) | 1u, refr_in ? cpix | (own + 1u) : cpix};
                 P.tasks[slot] = T;
                 if (P.task_keys)
-                    P.task_keys[slot] = (refr_in ? (1u << 15) | S.shapes[own].center_key : task_key(P, tro, trd)) | fkey;
+                    P.task_keys[slot] = (refr_in ? inside_key(P, S.shapes[own].center_key) : task_key(P, tro, trd)) | fkey;
                 hit_flags |= F_HAS_T;
             } else {
                 atomicOr(P.overflow, 1u);
