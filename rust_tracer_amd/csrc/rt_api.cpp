@@ -1806,6 +1806,15 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
             p.task_fine = 1u;
             task_bits = 21u;
         }
+        // ... and the shadow keys a fourth distance bit when 3 passes still hold them
+        // (RT_SHADOW_FINE=0: off, A/B)
+        const char* sf = std::getenv("RT_SHADOW_FINE");
+        if (!(sf && sf[0] == '0') && p.shadow_cell == 2u && p.shadow_fine == 18u && shadow_bits + 1u + fbits <= 24u &&
+            6ull * s->S.lb_res * s->S.lb_res * 16u < (1u << 18)) {
+            p.shadow_cell = 3u;
+            p.shadow_fine = 19u;
+            shadow_bits += 1u;
+        }
         p.task_frame_shift = task_bits;
         p.shadow_frame_shift = shadow_bits;
         task_bits += fbits;

@@ -648,10 +648,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                                 const bool lb = L.lb_base != 0xFFFFFFFFu && D <= S.lb_dmax &&
                                                 len2(raw) <= RT_LB_LMAX * RT_LB_LMAX;
                                 if (!lb) {
-                                    low = (1u << 17) | (mort >> 1);
+                                    low = (1u << (P.shadow_fine - 1u)) | (mort >> (19u - P.shadow_fine));
                                 } else if (P.shadow_cell == 2u) {  // cell | 3-bit distance from the light
                                     const float dl = sqrtf(len2(raw)) * (8.f / RT_LB_LMAX);
                                     low = (lb_cell(S.lb_res, neg(norm(raw))) << 3) | (uint32_t)fminf(dl, 7.f);
+                                } else if (P.shadow_cell == 3u) {  // cell | 4-bit distance (frame batches)
+                                    const float dl = sqrtf(len2(raw)) * (16.f / RT_LB_LMAX);
+                                    low = (lb_cell(S.lb_res, neg(norm(raw))) << 4) | (uint32_t)fminf(dl, 15.f);
                                 } else {
                                     low = lb_cell(S.lb_res, neg(norm(raw)));
                                 }
