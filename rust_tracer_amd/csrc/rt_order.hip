@@ -28,7 +28,10 @@
 
 namespace rtdev {
 
-constexpr uint32_t SORT_THREADS = 256, SORT_ITEMS = 16, SORT_TILE = SORT_THREADS * SORT_ITEMS;
+#ifndef RT_SORT_ITEMS
+#define RT_SORT_ITEMS 16
+#endif
+constexpr uint32_t SORT_THREADS = 256, SORT_ITEMS = RT_SORT_ITEMS, SORT_TILE = SORT_THREADS * SORT_ITEMS;
 constexpr uint32_t SORT_MAX_DIGIT_BITS = 11, SORT_MAX_DIGITS = 1u << SORT_MAX_DIGIT_BITS;
 
 // the queue being ordered: a task level (offset / count in levels[2l], levels[2l + 1]) or
