@@ -188,6 +188,9 @@ def seam_stats(args, scene, pipe, tiler, dev):
       render.rs:43-45), frames in flight as the headline."""
     out = {}
     main = torch.cuda.current_stream(dev)
+    # one frame at a time and the rt_render seam: the whole chip for the one pass
+    # (FramePipeline gives each of its passes 75%)
+    scene.set_grid_share(100)
     tiler.step()
     torch.cuda.synchronize()
     n1 = 5
@@ -212,6 +215,8 @@ def seam_stats(args, scene, pipe, tiler, dev):
     c = scene.clone(dev.index)
     out["scene_clone_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
     c.close()
+    if pipe.inflight > 1:
+        scene.set_grid_share(pipe.grid_share)
     if args.spp == 1:
         # an animation: every frame its own camera (the origin moves 0.01 per frame along x),
         # frames in flight and frames per pass as the headline -- the batches hold distinct views

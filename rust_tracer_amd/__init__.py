@@ -304,6 +304,11 @@ class DeviceScene:
                 "planes", "graze_normals", "cycles_nodes", "cycles_leaves", "cycles_graze", "cycles_scans",
                 "cycles_load", "cycles_post", "cycles_self")
 
+    def set_grid_share(self, percent):
+        """rt_scene_set_grid_share: persistent grids at `percent` % of a full chip (frames in
+        flight: several passes side by side)."""
+        check(self._L.rt_scene_set_grid_share(self.h, int(percent)), "rt_scene_set_grid_share")
+
     def set_scan_counting(self, enable=True):
         """Run the instrumented (counting) kernels from now on (rt_scene_set_scan_counting)."""
         check(self._L.rt_scene_set_scan_counting(self.h, 1 if enable else 0), "rt_scene_set_scan_counting")

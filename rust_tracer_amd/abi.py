@@ -150,6 +150,7 @@ def lib():
     L.rt_scene_device_bytes.restype = C.c_uint64
     L.rt_scene_scan_ops.argtypes = [vp, P(C.c_uint64), C.c_uint32, C.c_int32]
     L.rt_scene_set_scan_counting.argtypes = [vp, C.c_int32]
+    L.rt_scene_set_grid_share.argtypes = [vp, C.c_int32]
     L.rt_forest_create.argtypes = [vp, P(rt_camera), C.c_uint32, P(vp)]
     L.rt_forest_destroy.argtypes = [vp]
     L.rt_forest_render.argtypes = [vp, P(C.c_float)]

@@ -1119,6 +1119,7 @@ struct rt_scene {
     int occ[3] = {0, 0, 0};  // blocks per CU for the MAXF 7 / 15 / 63 variants
     int occ_trace = 0, occ_shadow = 0, occ_combine = 0;
     bool count_ops = false;  // rt_scene_set_scan_counting
+    int grid_pct = 100;      // rt_scene_set_grid_share: % of a full chip for persistent grids
     Workspace ws;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -1547,6 +1548,13 @@ rt_status rt_scene_scan_ops(rt_scene* s, uint64_t* out, uint32_t n, int32_t rese
 
 int32_t rt_scene_uses_bvh(const rt_scene* s) { return (s && s->S.use_bvh) ? 1 : 0; }
 
+rt_status rt_scene_set_grid_share(rt_scene* s, int32_t percent) {
+    if (!s || percent < 1 || percent > 100) return RT_ERR_INVALID_ARG;
+    if (s->multi) (void)rt_multi_each(s->multi, [&](rt_scene* c) { return rt_scene_set_grid_share(c, percent); });
+    s->grid_pct = percent;
+    return RT_OK;
+}
+
 rt_status rt_scene_set_scan_counting(rt_scene* s, int32_t enable) {
     if (!s) return RT_ERR_INVALID_ARG;
     if (s->multi) (void)rt_multi_each(s->multi, [&](rt_scene* c) { return rt_scene_set_scan_counting(c, enable); });
@@ -1897,9 +1905,10 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     int sb = s->num_cus * s->occ_shadow;
     int cb = s->num_cus * s->occ_combine;
     {
-        // A/B: RT_GRID_PCT = persistent grids at this % of a full chip (trace, shadow)
+        // the persistent trace / shadow grids at grid_pct % of a full chip
+        // (rt_scene_set_grid_share; RT_GRID_PCT overrides it, A/B)
         const char* e = std::getenv("RT_GRID_PCT");
-        const int pct = e ? std::atoi(e) : 100;
+        const int pct = e ? std::atoi(e) : s->grid_pct;
         if (pct > 0 && pct < 100) {
             tb = std::max(1, tb * pct / 100);
             sb = std::max(1, sb * pct / 100);

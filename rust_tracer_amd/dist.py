@@ -130,7 +130,7 @@ class FramePipeline:
     band buffer).  Every frame is rendered and gathered in full."""
 
     def __init__(self, scene: DeviceScene, desc, width, height, depth, band_rows=8, rank=0, world=1,
-                 device=None, spp=1, seed=0, inflight=4, batch=1, rgb8=False):
+                 device=None, spp=1, seed=0, inflight=4, batch=1, rgb8=False, grid_share=75):
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.inflight = max(1, int(inflight))
         self.world = world
@@ -139,6 +139,12 @@ class FramePipeline:
                                   depth, band_rows, rank, world, self.device, spp=spp, seed=seed, batch=batch,
                                   rgb8=rgb8)
                        for i in range(self.inflight)]
+        # several passes share the GPU: each pass's persistent grids take 75% of the chip
+        # (DESIGN.md "Frames in flight"; one pass at a time keeps the whole chip)
+        self.grid_share = int(grid_share)
+        if self.inflight > 1:
+            for t in self.tilers:
+                t.scene.set_grid_share(self.grid_share)
         self.frame_index = 0        # frames enqueued so far (the `cameras` callback's argument)
         self.pass_index = 0         # passes enqueued so far: pass k runs on slot k % inflight
         self.batch = self.tilers[0].batch
