@@ -308,9 +308,9 @@ rt_status rt_scene_scan_ops(rt_scene* scene, uint64_t* out, uint32_t n, int32_t 
 rt_status rt_scene_set_scan_counting(rt_scene* scene, int32_t enable);
 
 /* Frames in flight: the share (percent, 1..100, default 100) of a full chip that one
- * render pass's persistent trace and shadow grids take.  Several passes on several
- * streams then run side by side instead of one filling every CU slot until its queue is
- * drained (bench / FramePipeline: 75 with 4 passes in flight).  Results do not change. */
+ * render pass's persistent trace grids take.  Several passes on several streams then run
+ * side by side instead of one filling every CU slot until its level is drained (bench /
+ * FramePipeline: 75 with 4 passes in flight).  Results do not change. */
 rt_status rt_scene_set_grid_share(rt_scene* scene, int32_t percent);
 
 /* 1 if the scene's scans walk the culling hierarchy (the default; RT_BVH=0 in the
