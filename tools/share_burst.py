@@ -1,6 +1,6 @@
 """One rank's share of a K-frame burst (bench.py's timed region) on one GPU, no gather:
 K frames in passes of B frames over F slots, for world sizes / B values.
-usage: python tools/share_burst.py  (env WORLDS=8,4,2 BATCHES=4,5,8 FLIGHT=4 K=20 REPS=3)"""
+usage: python tools/share_burst.py  (env WORLDS=8,4,2 BATCHES=4,5,8 FLIGHT=4 K=20 REPS=3 GRID_SHARE=75)"""
 import os
 import sys
 import time
@@ -20,6 +20,10 @@ def main():
     reps = int(os.environ.get("REPS", "3"))
     desc = SceneDesc.synth_config(3)
     scenes = [DeviceScene(desc) for _ in range(F)]
+    share = int(os.environ.get("GRID_SHARE", "75"))  # as FramePipeline with passes in flight
+    if F > 1:
+        for s in scenes:
+            s.set_grid_share(share)
     streams = [torch.cuda.Stream() for _ in scenes]
     cnt = torch.zeros(3, dtype=torch.int64, device="cuda")
     cam = abi.camera(w, h)
