@@ -79,6 +79,13 @@ def test_rt_render_rejects_bad_arguments():
     assert L.rt_render(None, C.byref(cam), 1, None, rgb, None) == 1
     assert L.rt_unpermute_bands_async(None, 4, 4, 8, 1, None, None) == 1
     assert L.rt_quantize_u8_async(None, 4, None, None) == 1
+    buf = (C.c_float * 48)()
+    # frame batches: n_frames within stride_frames, both > 0
+    assert L.rt_unpermute_bands_batch_async(None, 4, 4, 8, 1, 1, 1, buf, None) == 1
+    assert L.rt_unpermute_bands_batch_async(buf, 4, 4, 8, 1, 2, 1, buf, None) == 1
+    assert L.rt_unpermute_bands_batch_async(buf, 4, 4, 8, 1, 0, 1, buf, None) == 1
+    assert L.rt_unpermute_bands_batch_u8_async(None, 4, 4, 8, 1, 1, 1, None, None) == 1
+    assert L.rt_scene_set_grid_share(None, 50) == 1
 
 
 def test_host_my_scene_matches_oracle_restatement_bit_for_bit():
