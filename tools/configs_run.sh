@@ -7,5 +7,5 @@ mkdir -p $OUT
 for c in 2 3 4; do
   timeout -k 10 300 python bench.py --config $c --steps 20 --warmup 4 --check 1 --cpu-baseline 0 --seam-stats 0 --count-frame 0 > $OUT/config$c.json 2> $OUT/config$c.err || exit $c
 done
-timeout -k 10 400 python bench.py --config 5 --steps 2 --warmup 1 --check 1 --cpu-baseline 0 --seam-stats 0 --count-frame 0 > $OUT/config5.json 2> $OUT/config5.err || exit 5
+timeout -k 10 400 python bench.py --config 5 --steps 4 --warmup 1 --check 1 --cpu-baseline 0 --seam-stats 0 --count-frame 0 > $OUT/config5.json 2> $OUT/config5.err || exit 5
 echo done
