@@ -230,8 +230,9 @@ struct WaveParams {
     const uint32_t* shadow_in;         // the shadow entries the shadow kernel reads
     uint32_t key_mode;                 // task key variant (A/B)
     float key_ahead;                   // modes 5 / 6: the key's point lies key_ahead x (scene radius) ahead
-    uint32_t shadow_fine;              // 18 / 21: shadow key = light | 18- / 21-bit Morton (3 sort passes); 0: 16-bit key
-    uint32_t shadow_cell;              // 1 (with shadow_fine 18): light | light-buffer cell, or light | flag | Morton >> 1
+    uint32_t shadow_fine;              // 18 / 19 / 21: bits below the light index (3 sort passes); 0: 16-bit key
+    uint32_t shadow_cell;              // light | light-buffer cell (1), x 3-bit (2) / 4-bit (3, shadow_fine 19)
+                                       // distance from the light; rays that walk: light | flag | Morton
     uint32_t light_shift;              // shadow key = (light << light_shift) | (Morton >> (15 - light_shift))
     uint32_t count_mask;               // bit 0: trace kernels add to scan_ops, bit 1: shadow kernel
     // ray forest (render_tree.rs; set only when building an rt_forest): per node
