@@ -35,7 +35,7 @@ hipError_t launch_unpermute_u8(const uint8_t* in, uint32_t x_res, uint32_t y_res
                                uint32_t world, uint32_t rows_per_rank, uint8_t* out, hipStream_t stream,
                                uint32_t frames = 1, uint32_t rank_rows = 0);
 bool rt_cube_table_check(const float* table);
-hipError_t wave_occupancy(int* trace_blocks, int* shadow_blocks, int* combine_blocks);
+hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_blocks, int* combine_blocks);
 hipError_t launch_wave_shadow(const WaveParams& p, int blocks, hipStream_t stream);
 hipError_t launch_wave_init(uint32_t* levels, uint32_t n_words, uint32_t total_items, uint32_t* overflow,
                             hipStream_t stream);
@@ -1896,7 +1896,7 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     }
     if (s->occ_trace == 0) {
         int a = 0, b = 0, c = 0;
-        HIP_TRY(wave_occupancy(&a, &b, &c));
+        HIP_TRY(wave_occupancy(p, &a, &b, &c));
         s->occ_trace = a > 0 ? a : 1;
         s->occ_shadow = b > 0 ? b : 1;
         s->occ_combine = c > 0 ? c : 1;

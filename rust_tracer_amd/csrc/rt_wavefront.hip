@@ -22,6 +22,7 @@
 // post-order combine keeps the reference's exact operation order (pixel values reach
 // |4000| in config 3, so a reassociated "throughput" formulation would break 1e-4).
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <type_traits>
 
@@ -1031,19 +1032,12 @@ hipError_t launch_wave_init(uint32_t* levels, uint32_t n_words, uint32_t total_i
     return hipGetLastError();
 }
 
-hipError_t wave_occupancy(int* trace_blocks, int* shadow_blocks, int* combine_blocks) {
-    hipError_t e =
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(trace_blocks, trace_level_kernel<false, false>, 256, 0);
-    if (e != hipSuccess) return e;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<false, false>, 256, 0);
-    if (e != hipSuccess) return e;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(combine_blocks, combine_level_kernel, 256, 0);
-}
-
 // The walk kernels' LDS variant stages the hierarchy's node records, the grazing pairs'
 // normals and the hierarchy's sphere pairs when they fit in 32 KB (five 256-thread blocks
-// per CU, the trace and shadow kernels' VGPR limit); RT_LDS_NODES=0: never, =trace /
-// =shadow: only that kernel (A/B)
+// per CU, the trace kernel's VGPR limit; config 3 stages 22.5 KB, which leaves the shadow
+// kernel its six); RT_LDS_NODES=0: never, =trace / =shadow: only that kernel (A/B).  The
+// hierarchy's triangle pairs staged as well (27.9 KB; records from LDS in VGPRs instead of
+// SGPRs, shadow kernel down to five blocks) lost 7.5%: 865 / 867 / 862 vs 936 / 932 / 933.
 static size_t lds_bytes(const WaveParams& p) {
     return (size_t)p.S.n_bvh_nodes * 64 + ((p.S.graze_lane && p.S.graze_res) ? (size_t)p.S.n_graze_blk * 128 : 0) +
            (size_t)p.S.n_dsph_bvh * 64;
@@ -1053,6 +1047,26 @@ static bool lds_nodes_for(const WaveParams& p, const char* kernel) {
     const char* e = getenv("RT_LDS_NODES");
     if (e && (e[0] == '0' || (std::strcmp(e, "1") != 0 && std::strcmp(e, kernel) != 0))) return false;
     return p.S.use_bvh && lds > 0 && lds <= 32 * 1024;
+}
+
+// Blocks per CU of the instantiations that launch: the LDS variants at the scene's LDS
+// bytes (the persistent grids are sized from these, so that every block is resident)
+hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_blocks, int* combine_blocks) {
+    const size_t lds = lds_bytes(p);
+    const bool aware = !getenv("RT_OCC_NOLDS");  // A/B: size the grids as if no LDS were used
+    hipError_t e = aware && lds_nodes_for(p, "trace")
+                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(trace_blocks, trace_level_kernel<false, true>, 256, lds)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(trace_blocks, trace_level_kernel<false, false>, 256, 0);
+    if (e != hipSuccess) return e;
+    e = aware && lds_nodes_for(p, "shadow")
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<true, false>, 256, lds)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<false, false>, 256, 0);
+    if (e != hipSuccess) return e;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(combine_blocks, combine_level_kernel, 256, 0);
+    if (getenv("RT_OCC_DEBUG"))
+        fprintf(stderr, "rt occupancy: lds %zu B (nodes %d, graze blocks %d, sphere pairs %d, tri pairs %d); blocks per CU trace %d shadow %d combine %d\n",
+                lds, p.S.n_bvh_nodes, p.S.n_graze_blk, p.S.n_dsph_bvh, p.S.n_tri_bvh, *trace_blocks, *shadow_blocks, *combine_blocks);
+    return e;
 }
 
 hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream) {
