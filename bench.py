@@ -62,9 +62,9 @@ def parse():
     p.add_argument("--band-rows", type=int, default=8)
     p.add_argument("--batch", type=int, default=None,
                    help="frames per pipeline pass (rt_render_bands_batch_async, <= 8; default: the timed "
-                        "frames spread evenly over the slots, ceil(steps / inflight), capped at 5 for a "
-                        "1080p frame per GPU, 1 for larger shares or spp > 1, else 8 while a pass stays "
-                        "within 4 x 1080p of pixels per rank)")
+                        "frames spread evenly over the slots, q = ceil(steps / inflight) per slot in equal "
+                        "passes of up to 8 frames (a divisor of q where one is close); 1 for a share above "
+                        "1080p at N = 1 or spp > 1, and a pass stays within 4 x 1080p of pixels per rank at N > 1)")
     p.add_argument("--inflight", type=int, default=None,
                    help="frames in flight (F scene handles / HIP streams; default 4 = the box's hardware "
                         "queues per process); 1 = one at a time")
@@ -291,20 +291,31 @@ def main():
     scene_create_ms = (time.perf_counter() - t_sc) * 1e3
     inflight = max(1, args.inflight or 4)
     if args.batch is None:
-        # The timed K frames are spread evenly over the F slots: B = ceil(K / F) frames per
-        # pass, capped.  N > 1 shares are latency-bound: up to 8 frames per pass (bounded
-        # workspace: <= 4 x 1080p of pixels per pass and rank); a whole 1080p frame per GPU
-        # up to 5 (~25 GB of workspace per slot).  K = 20, ms per share-frame on one MI355X
-        # (tools/share_burst.py): N = 1: B = 2 / 4 / 5 / 8: 2.46 / 2.51 / 2.31 / 2.36; N = 8:
-        # 0.533 / 0.464 / 0.389 / 0.381 (DESIGN.md "Frame batches")
+        # The timed K frames are spread evenly over the F slots: q = ceil(K / F) frames per
+        # slot, in r = ceil(q / cap) passes of B frames -- a divisor of q when one is near
+        # ceil(q / r), so that every slot runs the same passes.  Up to 8 frames per pass
+        # (bounded workspace: <= 4 x 1080p of pixels per pass and rank; ~40 GB per slot at
+        # 8 whole 1080p frames).  ms per share-frame on one MI355X at K = 20 (tools/share_burst.py):
+        # N = 1: B = 2 / 4 / 5 / 8: 2.46 / 2.51 / 2.31 / 2.36; N = 8: 0.533 / 0.464 / 0.389 /
+        # 0.381; N = 1 at K = 160 (tools/ab_batch.sh): B = 5 / 8: 919 / 938 Mpixels/s
+        # (DESIGN.md "Frame batches")
         share = band_rows_per_rank(args.height, args.band_rows, world) * args.width
         if args.spp > 1:
             cap = 1
         elif world == 1:
-            cap = 5 if share <= 1920 * 1088 else 1
+            cap = 8 if share <= 1920 * 1088 else 1
         else:
             cap = max(1, min(8, (4 * 1920 * 1088) // share))
-        args.batch = max(1, min(cap, -(-args.steps // inflight)))
+        q = -(-args.steps // inflight)
+        r = -(-q // cap)
+        b = -(-q // r)
+        for d in range(b, 0, -1):
+            if 2 * d < b:
+                break
+            if q % d == 0:
+                b = d
+                break
+        args.batch = max(1, b)
     pipe = FramePipeline(scene, desc, args.width, args.height, args.depth, args.band_rows, rank, world, dev,
                          spp=args.spp, seed=args.seed, inflight=inflight, batch=args.batch,
                          rgb8=args.output == "rgb8")
