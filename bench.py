@@ -74,8 +74,13 @@ def parse():
     p.add_argument("--cpu-rows-step", type=int, default=None,
                    help="CPU baseline renders every k-th row of the frame")
     p.add_argument("--backend", default="nccl", help="nccl (RCCL) or gloo (CPU rehearsal)")
-    p.add_argument("--check", type=int, default=0,
-                   help="rank 0 compares the assembled frame with a single-launch render")
+    p.add_argument("--check", type=int, default=1,
+                   help="rank 0 compares the timed passes' assembled frames with a single-launch render "
+                        "(untimed, on the device; 0 to skip)")
+    p.add_argument("--force-gather", type=int, default=0,
+                   help="at N = 1 under torchrun: assemble every pass through the process group's gather "
+                        "and the un-permute kernel anyway (a one-rank RCCL communicator; tests the N > 1 "
+                        "exchange on one GPU)")
     p.add_argument("--output", choices=("f32", "rgb8"), default="f32",
                    help="f32 frames (the parity contract), or Color::as_u8 bytes only: fused into the "
                         "render and gathered at 3 B per pixel (N > 1)")
@@ -107,17 +112,37 @@ def scene_label(config):
     return "synth seed 2 (600 spheres, 25 cubes, 100 triangles, 2 planes, 3 point lights)"
 
 
-def cpu_baseline(args, desc):
+def oracle_rows_check(gpu, cpu, rows):
+    """The GPU frame against the oracle on the rows the CPU baseline rendered (untimed;
+    tolerance 1e-4 per channel, north_star): max |diff|, NaN agreement, bit-exact share."""
+    import numpy as np
+    g, c = gpu[rows].astype(np.float64), cpu[rows].astype(np.float64)
+    nan_g, nan_c = np.isnan(g), np.isnan(c)
+    d = np.abs(g - c)
+    d[nan_g & nan_c] = 0.0
+    same = np.array_equal(gpu[rows].view(np.uint32), cpu[rows].view(np.uint32))
+    exact = float(np.mean(np.all(gpu[rows].view(np.uint32) == cpu[rows].view(np.uint32), axis=-1)))
+    mx = float(np.nanmax(d)) if d.size else 0.0
+    ok = bool(np.array_equal(nan_g, nan_c)) and mx <= 1e-4
+    return {"rows": len(rows), "pixels": int(len(rows) * gpu.shape[1]), "max_abs_diff": mx,
+            "nan_pattern_equal": bool(np.array_equal(nan_g, nan_c)), "bit_exact_pixel_frac": round(exact, 6),
+            "all_bit_exact": bool(same), "tolerance": 1e-4, "ok": ok}
+
+
+def cpu_baseline(args, desc, gpu_frame=None):
     """Single-threaded CPU oracle (the reference's algorithm, restated in C++) on every
-    k-th row of the same frame.  Mpixels/s = rendered pixels / wall time."""
+    k-th row of the same frame.  Mpixels/s = rendered pixels / wall time.  With the GPU's
+    single-launch frame, the rendered rows double as a parity check (`oracle_check`)."""
     from oracle.oracle import OracleScene
     o = OracleScene(desc)
     rows = range(0, args.height, args.cpu_rows_step)
     t0 = time.perf_counter()
-    _, cnt = o.render(args.width, args.height, args.depth, rows=(0, args.height, args.cpu_rows_step),
-                      threads=1, spp=args.spp, seed=args.seed)
+    img, cnt = o.render(args.width, args.height, args.depth, rows=(0, args.height, args.cpu_rows_step),
+                        threads=1, spp=args.spp, seed=args.seed)
     dt = time.perf_counter() - t0
+    check = oracle_rows_check(gpu_frame, img, list(rows)) if gpu_frame is not None else None
     return {
+        "oracle_check": check,
         "value": round(cnt["pixels"] / args.spp / dt / 1e6, 6),
         "unit": "Mpixels/s",
         "cores": 1,
@@ -270,7 +295,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_pg = world > 1 or bool(args.force_gather)
+    if use_pg:
         # one process per GPU; ranks share a device only in a --backend gloo rehearsal
         torch.cuda.set_device(local_rank % torch.cuda.device_count())
         if args.backend == "nccl":
@@ -318,14 +344,14 @@ def main():
         args.batch = max(1, b)
     pipe = FramePipeline(scene, desc, args.width, args.height, args.depth, args.band_rows, rank, world, dev,
                          spp=args.spp, seed=args.seed, inflight=inflight, batch=args.batch,
-                         rgb8=args.output == "rgb8")
+                         rgb8=args.output == "rgb8", force_gather=bool(args.force_gather))
     batch = pipe.batch
     tilers = pipe.tilers
     tiler = tilers[0]
     main_stream = torch.cuda.current_stream(dev)
 
     def barrier():
-        if world > 1:
+        if use_pg:
             if args.backend == "nccl":
                 dist.barrier(device_ids=[dev.index])
             else:
@@ -372,26 +398,32 @@ def main():
     red_dev = dev if args.backend == "nccl" else torch.device("cpu")
     stats = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=red_dev)
     cnt = cnt.to(red_dev)
-    if world > 1:
+    if use_pg:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
         dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
     frame_check = None
+    frame_checked = 0
+    single_ref = None
     if args.check:
-        # the timed frames' last assembled frame of every slot, then a fresh single frame,
-        # against one rt_render_spp launch of the whole frame
-        frames = [f.cpu().numpy() for f in pipe.frames()]
+        # the timed passes' assembled frames of every slot (pipe.frames() first checks every
+        # slot's overflow status), then a fresh single frame, against one rt_render_spp launch
+        # of the whole frame -- bit for bit, compared on the device
+        frames = list(pipe.frames())
         single = tiler.step()
         if rank == 0:
-            frames.append(single.cpu().numpy())
+            frames.append(single)
         torch.cuda.synchronize()
         if rank == 0:
-            import numpy as np
             ref, _, _, ref8 = scene.render(args.width, args.height, args.depth, device=dev.index, spp=args.spp,
                                            seed=args.seed, want_u8=args.output == "rgb8")
+            single_ref = ref
             if args.output == "rgb8":
-                frame_check = all(bool(np.array_equal(f, ref8)) for f in frames)
+                r = torch.from_numpy(ref8).to(dev)
+                frame_check = all(bool(torch.equal(f, r)) for f in frames)
             else:
-                frame_check = all(bool(np.array_equal(f.view(np.uint32), ref.view(np.uint32))) for f in frames)
+                r = torch.from_numpy(ref).to(dev).view(torch.int32)
+                frame_check = all(bool(torch.equal(f.contiguous().view(torch.int32), r)) for f in frames)
+            frame_checked = len(frames)
     seam = seam_stats(args, scene, pipe, tiler, dev) if (args.seam_stats and world == 1) else None
     for t in tilers:  # every stream-ordered pass of the run, incl. the timed ones, was complete
         t.scene.sync_status()
@@ -430,7 +462,21 @@ def main():
             "culling": {"hierarchy": scene.uses_bvh,
                         "linear_scan_flops_per_launch": brute_flops,
                         "linear_scan_equivalent_TFLOPs": round(brute_flops / (kernel_ms / 1e3) / 1e12, 3)},
-            "ceilings": {"no_fma_contraction": 0.5},
+            # structural ceilings of the algorithmic frac: the reference never
+            # fuses a*b+c (-ffp-contract=off: no FMA), and unpacked f32 issues one lane op per
+            # cycle where the 157.3 peak counts 2-wide packed FMA
+            "ceilings": {"no_fma_contraction": 0.5, "unpacked": 0.25},
+            # executed-instruction view beside the algorithmic frac: the profile's
+            # SQ_INSTS_VALU per frame (wave instructions, packed ones counted once) over the
+            # VALU issue slots of this frame time (1024 SIMDs x 2.4 GHz)
+            "executed_valu": ({
+                "sq_insts_valu_per_frame": traffic["sq_insts_valu_per_frame"],
+                "issue_slots_per_frame": round(1024 * 2.4e9 * kernel_ms / 1e3),
+                "issue_frac": round(traffic["sq_insts_valu_per_frame"] / (1024 * 2.4e9 * kernel_ms / 1e3), 4),
+                "wave_cycle_shares": traffic.get("wave_cycle_shares"),
+                "source": traffic.get("sq_source"),
+            } if traffic and traffic.get("sq_insts_valu_per_frame") else None),
+            "profile_commit": traffic.get("commit") if traffic else None,
             "hbm": {
                 "algorithmic_bytes_per_launch": args.spp * (scene.device_bytes + args.width * args.height * 12 / world),
                 "achieved_GBps": round((traffic["bytes_per_launch"] / (kernel_ms / 1e3) / 1e9), 3)
@@ -472,12 +518,13 @@ def main():
         }
         if frame_check is not None:
             out["frame_check"] = frame_check
+            out["frame_check_frames"] = frame_checked
         if seam is not None:
             out["seam"] = seam
         if world == 1 and args.cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args, desc)
+            out["cpu_baseline"] = cpu_baseline(args, desc, single_ref)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

@@ -171,7 +171,9 @@ rt_status rt_scene_clone(const rt_scene* src, int32_t device, rt_scene** out);
  * on devices[0] with RCCL (ncclGather over xGMI, communicators from ncclCommInitAll) and
  * un-permute them there before the copy to the caller's buffers.  The result equals the
  * one-device rt_render bit for bit (pixels are independent).  n_devices == 1 is
- * rt_scene_create.  A device listed twice shares that GPU between two band shares, which
+ * rt_scene_create, unless the environment sets RT_FORCE_RCCL=1: then the one device gets a
+ * one-rank RCCL communicator and renders go through the same band render, ncclGather and
+ * un-permute as n > 1 (a one-GPU machine runs the RCCL exchange this way).  A device listed twice shares that GPU between two band shares, which
  * then exchange bands by device copies (RCCL puts one rank per device; a test
  * configuration).  The stream-ordered entry points act on devices[0] only. */
 rt_status rt_scene_create_multi(const rt_scene_desc* desc, const int32_t* devices, uint32_t n_devices,
@@ -226,10 +228,11 @@ rt_status rt_render_bands_ex_async(const rt_scene* scene, const rt_camera* cams,
                                    uint32_t spp, uint32_t seed, uint32_t band_rows, uint32_t rank, uint32_t world,
                                    float* d_rgb, uint8_t* d_rgb8, uint64_t* d_counters, void* stream);
 
-/* Waits for every stream-ordered render enqueued on `scene` so far and reports whether one of
- * them overflowed a ray queue: RT_ERR_CAPACITY (that frame is incomplete; the flag is then
- * cleared) or RT_OK.  rt_render / rt_render_spp never need it: they grow the pool and render
- * again. */
+/* Waits for every stream-ordered render enqueued on `scene` so far, on every stream one ran
+ * on (the scene records an event per such stream after each render), and reports whether
+ * one of them overflowed a ray queue: RT_ERR_CAPACITY (that frame is incomplete; the flag is
+ * then cleared, and the next pass on this scene gets a node pool twice as large) or RT_OK.
+ * rt_render / rt_render_spp never need it: they grow the pool and render again. */
 rt_status rt_scene_sync_status(rt_scene* scene);
 
 /* Stochastic supersampling (BASELINE config 5; the reference has no equivalent, SURVEY.md

@@ -308,6 +308,12 @@ class DeviceScene:
         """rt_scene_set_grid_share: persistent grids at `percent` % of a full chip (frames in
         flight: several passes side by side)."""
         check(self._L.rt_scene_set_grid_share(self.h, int(percent)), "rt_scene_set_grid_share")
+        self._grid_share = int(percent)
+
+    @property
+    def grid_share(self):
+        """The share set by set_grid_share (100 = a full chip, the default of a new handle)."""
+        return getattr(self, "_grid_share", 100)
 
     def set_scan_counting(self, enable=True):
         """Run the instrumented (counting) kernels from now on (rt_scene_set_scan_counting)."""

@@ -153,15 +153,19 @@ void cube_triangles(std::vector<float>& out) {
 // The combine pass skips a shadowed point light of a node (rt_wavefront.hip light_sum)
 // only when its term f * ((l.n * 0) * kd + (pw * 0) * ks) is exactly +-0: the Schlick r0
 // and the fresnel factor finite for either side of the surface (n1 + n2 = 1 + ri != 0,
-// |1 - r0| x (1 + |n|)^5 finite for |n| <= 1e3), (m.h)^power finite (power in [0, 1e6],
-// m.h <= 1 + eps), finite diffuse / specular colours.
-bool dark_zero(const rt_material& m) {
+// |1 - r0| x (1 + |n|)^5 finite for |n| <= 1e3), (m.h)^power finite (power in [0, 1e6] and
+// power x ln(nmax (1 + 1e-5)) < 80, nmax = the scene's largest hit-normal length: planes
+// shade with the unnormalised transform * normal, plane.rs:75, so m.h can exceed 1 and
+// (m.h)^power overflow to inf, where the reference's inf * BLACK is NaN, material.rs:211),
+// finite diffuse / specular colours.
+bool dark_zero(const rt_material& m, double nmax) {
     auto finite_tex = [](const rt_texture& t) {
         return t.kind == RT_TEX_CHECKERBOARD ||
                (std::isfinite(t.color.r) && std::isfinite(t.color.g) && std::isfinite(t.color.b));
     };
     const float ri = m.refraction_index;
     if (!(std::isfinite(m.power) && m.power >= 0.f && m.power <= 1e6f && std::isfinite(ri))) return false;
+    if (!(std::isfinite(nmax) && (double)m.power * std::log(std::max(1.0, nmax) * (1.0 + 1e-5)) < 80.0)) return false;
     for (int entering = 0; entering < 2; entering++) {
         const float n1 = entering ? 1.f : ri, n2 = entering ? ri : 1.f;
         const float q = (n1 - n2) / (n1 + n2), r0 = q * q;
@@ -170,7 +174,7 @@ bool dark_zero(const rt_material& m) {
     return finite_tex(m.diffuse) && finite_tex(m.specular);
 }
 
-rt_status mat_rec(const rt_material& m, MatRec& M) {
+rt_status mat_rec(const rt_material& m, MatRec& M, double nmax) {
     if (m.kind != RT_MAT_PHONG && m.kind != RT_MAT_TEXTURE_PHONG) return RT_ERR_INVALID_ARG;
     const rt_texture* tx[3] = {&m.ambient, &m.diffuse, &m.specular};
     for (int k = 0; k < 3; k++) {
@@ -180,7 +184,7 @@ rt_status mat_rec(const rt_material& m, MatRec& M) {
     }
     std::memset(&M, 0, sizeof(M));
     M.kind = m.kind;
-    M.dark_zero = dark_zero(m) ? 1 : 0;
+    M.dark_zero = dark_zero(m, nmax) ? 1 : 0;
     M.power = m.power;
     M.reflectivity = m.reflectivity;
     M.refraction_index = m.refraction_index;
@@ -1123,9 +1127,11 @@ struct rt_scene {
     Workspace ws;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    hipEvent_t ev_last = nullptr;  // recorded after every stream-ordered render (rt_scene_sync_status)
-    bool ev_last_set = false;
+    // one event per stream a stream-ordered render ran on, recorded after each such render:
+    // rt_scene_sync_status and rt_scene_destroy wait for every one of them
+    std::vector<std::pair<hipStream_t, hipEvent_t>> ev_streams;
     uint32_t pool_floor = 0;       // node-pool size the next pass grows to (after a reported overflow)
+    double normal_max = 1.0;       // largest hit-normal length (dark_zero of an edited material)
     rt_multi_state* multi = nullptr;  // rt_scene_create_multi: the other devices' clones (rt_multi.cpp)
 };
 
@@ -1280,6 +1286,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     std::vector<CubeIn> cube_in;
     uint64_t flops = 0;
     bool normals_ok = true;  // DevScene::dark_skip: every hit normal finite with |n| <= 1e3
+    double nmax = 1.0;       // largest hit-normal length (unit normals; planes: |transform * n|)
     for (uint32_t i = 0; i < d->n_shapes; i++) {
         const rt_shape& s = d->shapes[i];
         if (s.material < 0 || (uint32_t)s.material >= d->n_materials) return RT_ERR_BAD_MATERIAL;
@@ -1315,6 +1322,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
                 F3 v = fnorm(fcross(n, u));
                 F3 tn = vec3_mul(s.transform, n);  // `self.transform * self.normal` (plane.rs:79)
                 if (!(std::fabs(tn.x) <= 1e3f && std::fabs(tn.y) <= 1e3f && std::fabs(tn.z) <= 1e3f)) normals_ok = false;
+                nmax = std::max(nmax, std::sqrt((double)tn.x * tn.x + (double)tn.y * tn.y + (double)tn.z * tn.z));
                 const float a[15] = {n.x, n.y, n.z, o.x, o.y, o.z, tn.x, tn.y, tn.z, u.x, u.y, u.z, v.x, v.y, v.z};
                 std::memcpy(R.a, a, sizeof(a));
                 for (int r = 0; r < 3; r++) put4(plane, inv.m[r][0], inv.m[r][1], inv.m[r][2], inv.m[r][3]);
@@ -1399,7 +1407,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     if (!rt_cube_table_check(cubetri.data())) return RT_ERR_UNSUPPORTED;
     std::vector<MatRec> mats(d->n_materials);
     for (uint32_t i = 0; i < d->n_materials; i++) {
-        rt_status r = mat_rec(d->materials[i], mats[i]);
+        rt_status r = mat_rec(d->materials[i], mats[i], nmax);
         if (r != RT_OK) return r;
     }
     // ---- one allocation, 256-B aligned sections
@@ -1499,11 +1507,11 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     S.amb_b = d->ambient.b;
     sc->flops_per_scan = flops;
     sc->n_point_lights = n_point;
+    sc->normal_max = nmax;
     sc->num_cus = g_num_cus(sc->device);
     HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&sc->ev0));
     HIP_TRY(hipEventCreate(&sc->ev1));
-    HIP_TRY(hipEventCreateWithFlags(&sc->ev_last, hipEventDisableTiming));
     *out = sc.release();
     return RT_OK;
 }
@@ -1514,11 +1522,12 @@ rt_status rt_scene_destroy(rt_scene* s) {
     s->multi = nullptr;
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
+    for (auto& se : s->ev_streams) (void)hipEventSynchronize(se.second);  // renders on other streams
     free_workspace(s->ws);
     if (s->dmem) (void)hipFree(s->dmem);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
-    if (s->ev_last) (void)hipEventDestroy(s->ev_last);
+    for (auto& se : s->ev_streams) (void)hipEventDestroy(se.second);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
     return RT_OK;
@@ -2009,8 +2018,14 @@ rt_status rt_render_bands_ex_async(const rt_scene* scene, const rt_camera* cams,
                            cams);
     }
     if (st != RT_OK) return st;
-    HIP_TRY(hipEventRecord(s->ev_last, hs));
-    s->ev_last_set = true;
+    hipEvent_t ev = nullptr;
+    for (auto& se : s->ev_streams)
+        if (se.first == hs) ev = se.second;
+    if (!ev) {
+        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        s->ev_streams.emplace_back(hs, ev);
+    }
+    HIP_TRY(hipEventRecord(ev, hs));
     return RT_OK;
 }
 
@@ -2039,7 +2054,7 @@ rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* cam, uin
 rt_status rt_scene_sync_status(rt_scene* s) {
     if (!s) return RT_ERR_INVALID_ARG;
     HIP_TRY(hipSetDevice(s->device));
-    if (s->ev_last_set) HIP_TRY(hipEventSynchronize(s->ev_last));
+    for (auto& se : s->ev_streams) HIP_TRY(hipEventSynchronize(se.second));
     if (!s->ws.overflow) return RT_OK;
     uint32_t v = 0;
     HIP_TRY(hipMemcpy(&v, s->ws.overflow + 1, sizeof(v), hipMemcpyDeviceToHost));
@@ -2076,13 +2091,13 @@ rt_status rt_scene_clone(const rt_scene* src, int32_t device, rt_scene** out) {
     rebase(S.shapes); rebase(S.mats); rebase(S.lights); rebase(S.bvh_nodes); rebase(S.bvh_leaves);
     rebase(S.graze_blk); rebase(S.graze_tri); rebase(S.graze_pn); rebase(S.graze_mask); rebase(S.scan_ops);
     sc->flops_per_scan = src->flops_per_scan;
+    sc->normal_max = src->normal_max;
     sc->n_point_lights = src->n_point_lights;
     sc->num_cus = g_num_cus(sc->device);
     sc->count_ops = src->count_ops;
     HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&sc->ev0));
     HIP_TRY(hipEventCreate(&sc->ev1));
-    HIP_TRY(hipEventCreateWithFlags(&sc->ev_last, hipEventDisableTiming));
     *out = sc.release();
     return RT_OK;
 }
@@ -2391,7 +2406,7 @@ rt_status rt_scene_set_material(rt_scene* s, uint32_t index, const rt_material* 
     HIP_TRY(hipMemcpy(&cur, s->S.mats + index, sizeof(cur), hipMemcpyDeviceToHost));
     if (m->kind != cur.kind) return RT_ERR_INVALID_ARG;  // the same kind, as the GUI's edits
     MatRec M;
-    rt_status r = mat_rec(*m, M);
+    rt_status r = mat_rec(*m, M, s->normal_max);
     if (r != RT_OK) return r;
     HIP_TRY(hipMemcpy(const_cast<MatRec*>(s->S.mats) + index, &M, sizeof(M), hipMemcpyHostToDevice));
     if (s->multi) return rt_multi_each(s->multi, [&](rt_scene* c) { return rt_scene_set_material(c, index, m); });

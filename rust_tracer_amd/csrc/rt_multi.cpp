@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -168,14 +169,14 @@ rt_status rt_multi_render(rt_scene* s, const rt_camera* cam, uint32_t depth, uin
     rt_status st = ensure_buffers(m, bf, ff, rgb8 != nullptr);
     if (st != RT_OK) return st;
     hipStream_t s0 = m->streams[0];
+    std::vector<char> redo(world, 1);  // ranks whose bands (re-)render in this attempt
+    MHIP(hipSetDevice(m->devices[0]));
+    MHIP(hipEventRecord(m->ev0, s0));
     for (int attempt = 0;; attempt++) {
         for (uint32_t r = 0; r < world; r++) {
+            if (!redo[r]) continue;
             MHIP(hipSetDevice(m->devices[r]));
             MHIP(hipMemsetAsync(m->counters[r], 0, 3 * sizeof(unsigned long long), m->streams[r]));
-        }
-        MHIP(hipSetDevice(m->devices[0]));
-        MHIP(hipEventRecord(m->ev0, s0));
-        for (uint32_t r = 0; r < world; r++) {
             st = rt_render_bands_ex_async(m->ranks[r], cam, 1, depth, spp, seed, band_rows, r, world, m->band[r],
                                           rgb8 ? m->band8[r] : nullptr, (uint64_t*)m->counters[r], m->streams[r]);
             if (st != RT_OK) return st;
@@ -223,11 +224,14 @@ rt_status rt_multi_render(rt_scene* s, const rt_camera* cam, uint32_t depth, uin
         }
         MHIP(hipEventRecord(m->ev1, s0));
         MHIP(hipStreamSynchronize(s0));
-        // a rank whose ray queues overflowed re-renders with a grown pool (rt_scene_sync_status)
+        // only a rank whose ray queues overflowed renders its bands again, with a grown pool
+        // (rt_scene_sync_status); every other rank's band buffer is still valid, and the
+        // exchange (a collective: every rank takes part) runs once more
         bool overflow = false;
         for (uint32_t r = 0; r < world; r++) {
             st = rt_scene_sync_status(m->ranks[r]);
-            if (st == RT_ERR_CAPACITY)
+            redo[r] = st == RT_ERR_CAPACITY;
+            if (redo[r])
                 overflow = true;
             else if (st != RT_OK)
                 return st;
@@ -272,7 +276,11 @@ rt_status rt_scene_create_multi(const rt_scene_desc* desc, const int32_t* device
         if (devices[r] < 0 || devices[r] >= n_visible) return RT_ERR_INVALID_ARG;
     rt_scene* s0 = nullptr;
     rt_status st = rt_scene_create(desc, devices[0], &s0);
-    if (st != RT_OK || n_devices == 1) {
+    // RT_FORCE_RCCL=1: one device still renders through the band render + ncclGather (a
+    // one-rank communicator) + un-permute, so a one-GPU machine executes the RCCL exchange
+    const char* force = std::getenv("RT_FORCE_RCCL");
+    const bool force_rccl = force && force[0] == '1';
+    if (st != RT_OK || (n_devices == 1 && !force_rccl)) {
         *out = s0;
         return st;
     }

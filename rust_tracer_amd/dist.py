@@ -14,7 +14,7 @@ independent, so the only exchange step is assembling the frame:
 import torch
 import torch.distributed as dist
 
-from . import DeviceScene, abi, band_rows_per_rank, unpermute_bands_batch_async
+from . import DeviceScene, RtError, abi, band_rows_per_rank, unpermute_bands_batch_async
 
 
 def band_rows_per_rank_py(y_res, band_rows, world):
@@ -38,14 +38,17 @@ class FrameTiler:
     """Renders this rank's share of a frame and gathers the frame on rank 0."""
 
     def __init__(self, scene: DeviceScene, width, height, depth, band_rows=8, rank=0, world=1,
-                 device=None, spp=1, seed=0, batch=1, rgb8=False):
+                 device=None, spp=1, seed=0, batch=1, rgb8=False, force_gather=False):
         """rgb8: render and gather only Color::as_u8 bytes (3 B per pixel instead of 12; the
-        level-0 combine writes them, rt_render_bands_ex_async with no float buffer)."""
+        level-0 combine writes them, rt_render_bands_ex_async with no float buffer).
+        force_gather: at world 1 too, assemble through the process group's gather and the
+        un-permute kernel (a one-rank communicator: runs the RCCL exchange on one GPU)."""
         self.scene = scene
         self.rgb8 = bool(rgb8) and spp == 1
         self.spp, self.seed = spp, seed
         self.w, self.h, self.depth = width, height, depth
         self.band_rows, self.rank, self.world = band_rows, rank, world
+        self.gather = world > 1 or bool(force_gather)
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.rpr = band_rows_per_rank(height, band_rows, world)
         assert self.rpr == band_rows_per_rank_py(height, band_rows, world)
@@ -60,11 +63,11 @@ class FrameTiler:
         self.counters = torch.zeros(3, dtype=torch.int64, device=self.device)
         self.gathered = None
         self.frames = None          # [batch, H, W, 3]: the last pass's assembled frames (rank 0)
-        if rank == 0 and world > 1:
+        if rank == 0 and self.gather:
             # one gather per pass: every rank's `batch` band buffers, rank-major
             self.gathered = torch.zeros((world, self.batch, self.rpr, width, 3), dtype=dt, device=self.device)
             self.frames = torch.zeros((self.batch, height, width, 3), dtype=dt, device=self.device)
-        elif world == 1:
+        elif not self.gather:
             self.frames = self.locals[:, :height]
         self.frame = self.frames[0] if self.frames is not None else None
         self.last = 1               # frames in the last pass
@@ -91,8 +94,8 @@ class FrameTiler:
     def assemble(self):
         """Gather every rank's bands of the last pass's frames on rank 0 -- one gather for the
         whole pass -- and restore row order, every frame of the pass in one launch (no-op at
-        world 1)."""
-        if self.world == 1:
+        world 1 unless force_gather)."""
+        if not self.gather:
             return self.frame
         stream = torch.cuda.current_stream(self.device).cuda_stream
         n = self.last
@@ -130,18 +133,21 @@ class FramePipeline:
     band buffer).  Every frame is rendered and gathered in full."""
 
     def __init__(self, scene: DeviceScene, desc, width, height, depth, band_rows=8, rank=0, world=1,
-                 device=None, spp=1, seed=0, inflight=4, batch=1, rgb8=False, grid_share=75):
+                 device=None, spp=1, seed=0, inflight=4, batch=1, rgb8=False, grid_share=75,
+                 force_gather=False):
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.inflight = max(1, int(inflight))
         self.world = world
         # slot i > 0: a clone of the scene (device copy, own workspace and stream)
         self.tilers = [FrameTiler(scene if i == 0 else scene.clone(self.device.index), width, height,
                                   depth, band_rows, rank, world, self.device, spp=spp, seed=seed, batch=batch,
-                                  rgb8=rgb8)
+                                  rgb8=rgb8, force_gather=force_gather)
                        for i in range(self.inflight)]
+        self.gather = self.tilers[0].gather
         # several passes share the GPU: each pass's persistent grids take 75% of the chip
         # (DESIGN.md "Frames in flight"; one pass at a time keeps the whole chip)
         self.grid_share = int(grid_share)
+        self._caller_share = scene.grid_share   # slot 0 is the caller's scene: restored by close()
         if self.inflight > 1:
             for t in self.tilers:
                 t.scene.set_grid_share(self.grid_share)
@@ -187,7 +193,7 @@ class FramePipeline:
                 if latency_events is not None:
                     ev[1].record(st)
                     latency_events.append(ev)
-            if self.world > 1:
+            if self.gather:
                 main.wait_stream(st)
                 self.tilers[i].assemble()
                 self._reuse[i] = torch.cuda.Event()
@@ -195,10 +201,33 @@ class FramePipeline:
         for s in self.streams:
             main.wait_stream(s)
 
+    def sync(self):
+        """Wait for every slot's enqueued passes; raises RtError(RT_ERR_CAPACITY) if one of
+        them overflowed a ray queue (its frames are incomplete -- the slot's next pass gets a
+        grown pool, rt_scene_sync_status)."""
+        err = None
+        for t in self.tilers:  # every slot (each grows its own pool), then the first error
+            try:
+                t.scene.sync_status()
+            except RtError as e:
+                err = err or e
+        if err is not None:
+            raise err
+
     def frames(self):
-        """every frame of each slot's last pass, assembled (rank 0; [] elsewhere)"""
+        """every frame of each slot's last pass, assembled (rank 0; [] elsewhere).  Checks
+        every slot's overflow status first: an incomplete frame is never returned."""
+        self.sync()
         return [t.frames[b] for t in self.tilers if t.frames is not None for b in range(t.last)]
+
+    def set_material(self, index, material):
+        """rt_scene_set_material on every slot's scene (slot clones are independent copies),
+        after the passes enqueued so far (the GUI's material edit, gui.rs:221-236)."""
+        torch.cuda.synchronize(self.device)
+        for t in self.tilers:
+            t.scene.set_material(index, material)
 
     def close(self):
         for t in self.tilers[1:]:
             t.scene.close()
+        self.tilers[0].scene.set_grid_share(self._caller_share)

@@ -1,9 +1,12 @@
 """GPU tests of the drop-in seam beyond one device and one float frame:
 
 - multi-device scenes (rt_scene_create_multi): the frame tiled over ranks, gathered and
-  un-permuted, equals the one-device rt_render bit for bit -- with one device (the RCCL
-  communicator of one rank) and with one GPU listed 2 / 3 times (band shares exchanged by
-  device copies: the multi-rank band logic on a one-GPU box);
+  un-permuted, equals the one-device rt_render bit for bit -- with one GPU listed 2 / 3 times
+  (band shares exchanged by device copies: the multi-rank band logic on a one-GPU box), and
+  with RT_FORCE_RCCL=1 and one device: a one-rank RCCL communicator (ncclCommInitAll), the
+  grouped ncclGather and the un-permute kernel really execute on the one-GPU box;
+- bench.py under torchrun --nproc-per-node 1 --backend nccl --force-gather 1: the
+  process-group path's RCCL gather (torch.distributed over RCCL) with frame_check;
 - queue overflow is never a silent RT_OK: the stream-ordered entry points latch it and
   rt_scene_sync_status raises RT_ERR_CAPACITY; rt_render grows its pool and renders the
   full frame (render.rs:40-103 traces every ray);
@@ -47,7 +50,8 @@ def test_multi_device_scene_equals_single(devices):
     single.close()
     multi = DeviceScene(desc, devices=devices)
     assert multi.device_count == len(devices)
-    # RCCL is used only when every listed device is distinct and there is more than one
+    # without RT_FORCE_RCCL, one device is a plain scene and a repeated device exchanges
+    # bands by device copies: no RCCL
     assert not multi.uses_rccl
     img, cnt, ms, img8 = multi.render(w, h, depth, want_u8=True)
     img2, cnt2, _, _ = multi.render(w, h, depth)  # buffers reused
@@ -56,6 +60,92 @@ def test_multi_device_scene_equals_single(devices):
     assert np.array_equal(img8, ref8)
     assert cnt == rcnt and cnt2 == rcnt
     assert ms > 0
+
+
+@pytest.mark.parametrize("w,h", [(320, 180), (3840, 2160)])
+def test_forced_rccl_one_rank(monkeypatch, w, h):
+    """RT_FORCE_RCCL=1 with devices=[0]: rt_scene_create_multi builds a one-rank RCCL
+    communicator, and rt_render runs the band render, the grouped ncclGather (rt_multi.cpp)
+    and the un-permute kernel.  Config 3 at 320x180 and the whole config 4 frame (3840x2160,
+    depth 8) equal the one-device rt_render bit for bit (render.rs:32-37 tiled)."""
+    desc = SceneDesc.synth_config(3)
+    single = DeviceScene(desc, device=0)
+    ref, rcnt, _, ref8 = single.render(w, h, 8, want_u8=True)
+    single.close()
+    monkeypatch.setenv("RT_FORCE_RCCL", "1")
+    multi = DeviceScene(desc, devices=[0])
+    assert multi.uses_rccl and multi.device_count == 1
+    img, cnt, ms, img8 = multi.render(w, h, 8, want_u8=True)
+    img2, cnt2, _, _ = multi.render(w, h, 8)  # communicator and buffers reused
+    multi.close()
+    assert same_bits(img, ref) and same_bits(img2, ref)
+    assert np.array_equal(img8, ref8)
+    assert cnt == rcnt and cnt2 == rcnt
+    assert ms > 0
+
+
+def test_forced_rccl_overflow_rerenders(monkeypatch):
+    """A one-rank RCCL scene whose node pool is far too small: the rank re-renders with a
+    grown pool, the gather runs again, and the frame is complete."""
+    desc = SceneDesc.synth_config(3)
+    single = DeviceScene(desc, device=0)
+    ref, rcnt, _, _ = single.render(256, 144, 8)
+    single.close()
+    monkeypatch.setenv("RT_FORCE_RCCL", "1")
+    monkeypatch.setenv("RT_NODE_CAP", str(256 * 144 + 4096))
+    multi = DeviceScene(desc, devices=[0])
+    assert multi.uses_rccl
+    img, cnt, _, _ = multi.render(256, 144, 8)
+    multi.close()
+    assert same_bits(img, ref) and cnt == rcnt
+
+
+def test_torchrun_one_rank_nccl_gather():
+    """bench.py under torchrun with one rank, backend nccl (RCCL) and --force-gather 1: every
+    pass is assembled through torch.distributed.gather over a one-rank RCCL communicator and
+    the un-permute kernel (dist.py FrameTiler.assemble), and frame_check holds."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", "29613", "bench.py", "--backend", "nccl",
+           "--force-gather", "1", "--check", "1", "--steps", "4", "--warmup", "1", "--inflight", "2",
+           "--cpu-baseline", "0", "--count-frame", "0", "--seam-stats", "0"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 1
+    assert out["frame_check"] is True and out["frame_check_frames"] >= 3
+
+
+def test_pipeline_overflow_is_raised(monkeypatch):
+    """FramePipeline with a node pool far too small: frames() raises RT_ERR_CAPACITY instead
+    of returning incomplete frames; the slots' next passes get grown pools and are complete."""
+    from rust_tracer_amd.dist import FramePipeline
+    desc = SceneDesc.synth_config(3)
+    w, h, depth = 192, 108, 8
+    s = DeviceScene(desc, device=0)
+    ref, _, _, _ = s.render(w, h, depth)
+    monkeypatch.setenv("RT_NODE_CAP", str(w * h + 1024))
+    pipe = FramePipeline(s, desc, w, h, depth, inflight=2, batch=1)
+    pipe.run(2)
+    with pytest.raises(RtError) as e:
+        pipe.frames()
+    assert e.value.status == abi.RT_ERR_CAPACITY
+    for attempt in range(6):  # each reported overflow doubles that slot's pool
+        pipe.run(2)
+        try:
+            frames = pipe.frames()
+            break
+        except RtError as e:
+            assert e.status == abi.RT_ERR_CAPACITY
+    assert attempt >= 1
+    assert len(frames) == 2 and all(same_bits(f.cpu().numpy(), ref) for f in frames)
+    pipe.close()
+    assert s.grid_share == 100  # the caller's scene gets its grid share back
+    s.close()
 
 
 def test_multi_device_ragged_and_spp():
@@ -248,6 +338,42 @@ def test_shadowed_light_skip_is_exact(name, monkeypatch):
         oimg, ocnt = OracleScene(desc).render(w, h, 8)
         compare(img, oimg)
         assert cnt == ocnt
+
+
+def _scaled_plane_scene():
+    """A floor plane whose transform scales its normal to length 2 (plane.rs:75 shades with
+    transform * normal, not normalised) and a specular power of 500: (m.h)^power overflows to
+    inf, so a shadowed light's term is inf * BLACK = NaN in the reference (material.rs:211) --
+    the combine's shadowed-light skip must not apply there."""
+    from rust_tracer_amd import Matrix
+    d = SceneDesc()
+    floor = d.phong((0.1, 0.1, 0.1), (0.5, 0.5, 0.5), (1, 1, 1), 500.0, 0.0, 0.0)
+    ball = d.phong((0.1, 0.0, 0.0), (1, 0, 0), (1, 1, 1), 60.0, 0.0, 0.0)
+    d.plane(floor, (0.0, -1.0, 0.0), (0.0, 1.0, 0.0), Matrix.scale(2.0, 2.0, 2.0))
+    d.sphere(ball, Matrix.translate(0.0, -1.0, 0.0) * Matrix.scale(0.6, 0.6, 0.6))
+    d.point_light((0.0, 10.0, 0.0), (1, 1, 1))
+    d.point_light((3.0, 6.0, -4.0), (0.5, 0.5, 0.5))
+    d.set_ambient((0.1, 0.1, 0.1))
+    return d
+
+
+def test_scaled_plane_normal_high_power():
+    """Shadowed light on a plane with |transform * n| = 2 and power 500: NaN / inf exactly as
+    the oracle and as the full evaluation (RT_NO_DARK_SKIP=1)."""
+    desc = _scaled_plane_scene()
+    w, h = 96, 96
+    s = DeviceScene(desc, device=0)
+    img, cnt, _, _ = s.render(w, h, 4)
+    s.close()
+    ref, rcnt = OracleScene(desc).render(w, h, 4)
+    assert cnt == rcnt
+    assert np.isnan(ref).any()  # the scene really reaches the inf * BLACK case
+    nan_g, nan_r = np.isnan(img), np.isnan(ref)
+    assert np.array_equal(nan_g, nan_r)
+    eq = img.view(np.uint32) == ref.view(np.uint32)
+    d = np.abs(img.astype(np.float64) - ref.astype(np.float64))
+    d[eq | (nan_g & nan_r)] = 0.0
+    assert float(d.max()) <= TOL
 
 
 @pytest.mark.parametrize("depth", [65, 200])
