@@ -510,6 +510,8 @@ def main():
                 "parallelism": f"row-bands x{world}" + ((" + RCCL gather" if args.backend == "nccl"
                                                           else f" + {args.backend} gather (rehearsal)")
                                                          if world > 1 else ""),
+                "workspace_bytes_per_slot": max(t.scene.workspace_bytes for t in tilers),
+                "workspace_bytes_all_slots": sum(t.scene.workspace_bytes for t in tilers),
                 "node_rays_per_frame": node_rays / steps,
                 "shadow_rays_per_frame": shadow_rays / steps,
             },

@@ -178,6 +178,18 @@ rt_status rt_scene_clone(const rt_scene* src, int32_t device, rt_scene** out);
  * configuration).  The stream-ordered entry points act on devices[0] only. */
 rt_status rt_scene_create_multi(const rt_scene_desc* desc, const int32_t* devices, uint32_t n_devices,
                                 rt_scene** out);
+/* The specular power function of the device path (rt_powf.hpp: glibc's powf evaluation,
+ * bit-identical to the libm powf the reference's f32::powf calls, material.rs:211), over
+ * arrays -- verification hooks: rt_powf_batch_async on the device (d_* device pointers,
+ * stream-ordered), rt_powf_batch_host the same code compiled for the host. */
+rt_status rt_powf_batch_async(const float* d_x, const float* d_y, float* d_out, uint64_t n, void* stream);
+rt_status rt_powf_batch_host(const float* x, const float* y, float* out, uint64_t n);
+
+/* Device bytes the scene's render workspace holds now (node pool, ray and shadow queues,
+ * sort buffers, frame buffers of rt_render): it grows with the largest pass rendered so far
+ * (pixels x frames per pass x RT_NODE_FACTOR node slots) and after a reported overflow. */
+uint64_t rt_scene_workspace_bytes(const rt_scene* scene);
+
 /* Devices a scene renders on (1 unless made by rt_scene_create_multi), and whether its band
  * exchange runs over RCCL. */
 int32_t rt_scene_device_count(const rt_scene* scene);

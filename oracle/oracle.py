@@ -56,6 +56,7 @@ def lib():
     L.oracle_forest_destroy.argtypes = [vp]
     L.oracle_scene_set_material.argtypes = [vp, C.c_uint32, P(abi.rt_material)]
     L.oracle_as_u8.argtypes = [fa, C.c_uint64, P(C.c_uint8)]
+    L.oracle_powf_batch.argtypes = [fa, fa, fa, C.c_uint64]
     for n in ("identity",):
         getattr(L, "oracle_matrix_" + n).argtypes = [fa]
     for n in ("scale", "translate"):
@@ -188,4 +189,14 @@ def as_u8(rgb):
     out = np.zeros(rgb.shape, np.uint8)
     lib().oracle_as_u8(rgb.ctypes.data_as(C.POINTER(C.c_float)), rgb.size,
                        out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return out
+
+
+def powf(x, y):
+    """libm powf (the reference's f32::powf) elementwise over float32 arrays."""
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.ascontiguousarray(y, np.float32)
+    out = np.empty_like(x)
+    fp = C.POINTER(C.c_float)
+    lib().oracle_powf_batch(x.ctypes.data_as(fp), y.ctypes.data_as(fp), out.ctypes.data_as(fp), x.size)
     return out

@@ -1102,6 +1102,11 @@ rt_status oracle_scene_set_material(oracle_scene* s, uint32_t index, const rt_ma
     return RT_ERR_INVALID_ARG;
 }
 
+// f32::powf of the reference (material.rs:211): the platform libm's powf, over arrays
+void oracle_powf_batch(const float* x, const float* y, float* out, uint64_t n) {
+    for (uint64_t i = 0; i < n; i++) out[i] = powf(x[i], y[i]);
+}
+
 void oracle_as_u8(const float* rgb, uint64_t n, uint8_t* out) {
     for (uint64_t k = 0; k < n; k++) out[k] = sat_u8(255.f * rgb[k]);
 }

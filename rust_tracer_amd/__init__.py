@@ -296,6 +296,11 @@ class DeviceScene:
         return int(self._L.rt_scene_device_bytes(self.h))
 
     @property
+    def workspace_bytes(self):
+        """rt_scene_workspace_bytes: device bytes of this handle's render workspace."""
+        return int(self._L.rt_scene_workspace_bytes(self.h))
+
+    @property
     def uses_bvh(self):
         """True when scans walk the culling hierarchy (RT_BVH=0 at creation turns it off)."""
         return bool(self._L.rt_scene_uses_bvh(self.h))

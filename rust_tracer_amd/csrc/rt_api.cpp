@@ -1097,6 +1097,19 @@ bool self_shadow_enabled() {
     return !(e && e[0] == '0');
 }
 
+// Workspace sizing: node slots per level-0 item, shadow-queue slots per node slot
+// (measured need, config 3: 3.66 node rays per pixel, 2.0 queued shadow rays per node)
+uint64_t node_factor() {
+    const char* e = std::getenv("RT_NODE_FACTOR");
+    const long v = e ? std::atol(e) : 6;
+    return v >= 2 ? (uint64_t)v : 2u;
+}
+double shadow_factor() {
+    const char* e = std::getenv("RT_SHADOW_FACTOR");
+    const double v = e ? std::atof(e) : 2.0;
+    return v >= 0.25 ? v : 0.25;
+}
+
 // Device path: "wave" (level-synchronous, default) or "mega" (per-pixel megakernel),
 // chosen with RT_PIPELINE for A/B measurement.
 bool use_megakernel() {
@@ -1534,6 +1547,19 @@ rt_status rt_scene_destroy(rt_scene* s) {
 }
 
 uint64_t rt_scene_flops_per_scan(const rt_scene* s) { return s ? s->flops_per_scan : 0; }
+
+uint64_t rt_scene_workspace_bytes(const rt_scene* s) {
+    if (!s) return 0;
+    const Workspace& w = s->ws;
+    uint64_t b = (uint64_t)w.out_floats * 4 + w.out8_bytes + 4 * 8 + 64;
+    b += (uint64_t)w.capacity * (sizeof(Task) + 4 + 3 * 16 + 4 + 2 * 16);  // tasks, node arrays
+    if (w.forest) b += (uint64_t)w.capacity * (2 * 16 + 4 + 4);
+    b += (uint64_t)w.sort_capacity * 8;                                      // task keys, permutation
+    b += (uint64_t)w.shadow_capacity * 4 + (uint64_t)w.sort_shadow_capacity * 8;
+    b += (uint64_t)w.sort_tmp_words * 4;
+    if (w.levels) b += RT_LEVEL_TABLE_WORDS * 4 + 64;
+    return b;
+}
 uint64_t rt_scene_device_bytes(const rt_scene* s) { return s ? (uint64_t)s->dbytes : 0; }
 
 rt_status rt_scene_scan_ops(rt_scene* s, uint64_t* out, uint32_t n, int32_t reset) {
@@ -1711,13 +1737,15 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     total *= frames;
     if (total >= (1ull << 30)) return RT_ERR_UNSUPPORTED;
     p.total_items = (uint32_t)total;
-    // node / task pool: level 0 plus room for ~11 secondary nodes per pixel on average
-    // (config 3 needs 2.7); an overflow is reported, never silently truncated.  A shadow
-    // entry packs (node << light_bits) | light, so nodes stay below 2^(32 - light_bits).
+    // node / task pool: RT_NODE_FACTOR (default 6) nodes per level-0 item -- config 3
+    // traces 3.66 node rays per pixel, config 4 the same scene at 4K; an overflow is
+    // reported, never silently truncated, and the next pass gets twice the pool (rt_render
+    // retries by itself).  A shadow entry packs (node << light_bits) | light, so nodes stay
+    // below 2^(32 - light_bits).
     p.light_bits = light_bits(s);
     const uint64_t max_cap = pool_cap_limit(s);
     if (total >= max_cap) return RT_ERR_UNSUPPORTED;
-    uint64_t want = std::max<uint64_t>(total * 12u, 1u << 20);
+    uint64_t want = std::max<uint64_t>(total * node_factor(), 1u << 20);
     if (const char* e = std::getenv("RT_NODE_CAP")) want = std::max<uint64_t>(total + 1, std::strtoull(e, nullptr, 0));
     if (&w == &s->ws) want = std::max<uint64_t>(want, s->pool_floor);
     if (want > max_cap) want = max_cap;
@@ -1730,8 +1758,11 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         HIP_TRY(hipMalloc(&w.overflow, 64));
         HIP_TRY(hipMemset(w.overflow, 0, 64));
     }
-    // shadow queue: one entry per point light per hit node
-    uint64_t want_sh = std::min<uint64_t>((uint64_t)w.capacity * s->n_point_lights, 0x7FFFFFFFu);
+    // shadow queue: at most one entry per point light per hit node; RT_SHADOW_FACTOR
+    // (default 2) entries per node slot, at most the point lights (config 3 queues 2.0 per
+    // traced node: the trace kernel decides the rest; overflow reported like the node pool's)
+    uint64_t want_sh = std::min<uint64_t>(
+        (uint64_t)((double)w.capacity * std::min<double>(shadow_factor(), (double)s->n_point_lights)), 0x7FFFFFFFu);
     if (want_sh == 0) want_sh = 1;
     if (w.shadow_capacity < want_sh) {
         if (w.shadow) (void)hipFree(w.shadow);

@@ -4,13 +4,15 @@
 //
 // Numerics: compiled with -ffp-contract=off, IEEE division/sqrt and f32 denormals on,
 // so every +,-,*,/,sqrt is the same correctly rounded operation the reference
-// executes, in the same order.  powf/atan2f/acosf come from ocml (<= 1-2 ulp from glibc).
+// executes, in the same order.  powf is glibc's own evaluation (rt_powf.hpp, bit-identical to
+// the reference's libm powf); atan2f / acosf (textured spheres only) come from ocml (<= 1-2 ulp).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/rt_api.h"
 #include "rt_device.hpp"
+#include "rt_powf.hpp"
 
 namespace rtdev {
 
@@ -269,7 +271,7 @@ __device__ __forceinline__ V3 reflected_energy_ne(V3 E, V3 l, V3 n, V3 ne, V3 kd
     float mh = dot(n, hv);
     V3 spec = v3(0.f, 0.f, 0.f);
     if (!(mh < 0.f)) {
-        float pw = powf(mh, power);
+        float pw = rtpow::powf_glibc(mh, power);  // material.rs:211, glibc's powf
         spec = v3((pw * E.x) * ks.x, (pw * E.y) * ks.y, (pw * E.z) * ks.z);
     }
     return v3((ln * E.x) * kd.x + spec.x, (ln * E.y) * kd.y + spec.y, (ln * E.z) * kd.z + spec.z);
@@ -328,7 +330,7 @@ __device__ __forceinline__ void node_weights(const MatRec& M, V3 rd, V3 n, V3 ne
         const float mh = dot(n, hv);
         if (!(mh < 0.f)) {
             f.flags |= F_SPEC;
-            f.pw = powf(mh, M.power);
+            f.pw = rtpow::powf_glibc(mh, M.power);
         }
     }
     if (M.refraction_index > RT_EPS) {

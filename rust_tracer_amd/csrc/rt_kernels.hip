@@ -21,9 +21,11 @@
 //
 // Numerics: compiled with -ffp-contract=off, IEEE division/sqrt and f32 denormals on,
 // so every +,-,*,/,sqrt is the same correctly rounded operation the reference
-// executes, in the same order.  powf/atan2f/acosf come from ocml (<= 1-2 ulp from glibc).
+// executes, in the same order.  powf is glibc's evaluation (rt_powf.hpp); atan2f / acosf
+// (textured spheres only) come from ocml (<= 1-2 ulp from glibc).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <algorithm>
 
 #include "../../include/rt_api.h"
 #include "rt_device.hpp"
@@ -202,7 +204,7 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
                 float mh = dot(h.n, hv);
                 if (!(mh < 0.f)) {
                     f.flags |= F_SPEC;
-                    f.pw = powf(mh, power);
+                    f.pw = rtpow::powf_glibc(mh, power);
                 }
                 trace_refl = child_ok;
             }
@@ -386,3 +388,25 @@ hipError_t launch_quantize(const float* in, size_t n, uint8_t* out, hipStream_t 
 }
 
 }  // namespace rtdev
+
+// ---- powf verification hooks (tests/test_powf.py): the device's powf (rt_powf.hpp) over
+// arrays, on the device and compiled for the host, against the oracle's libm powf
+__global__ void powf_batch_kernel(const float* x, const float* y, float* out, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = rtpow::powf_glibc(x[i], y[i]);
+}
+
+extern "C" rt_status rt_powf_batch_async(const float* d_x, const float* d_y, float* d_out, uint64_t n, void* stream) {
+    if (n == 0) return RT_OK;
+    if (!d_x || !d_y || !d_out) return RT_ERR_INVALID_ARG;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096u);
+    hipLaunchKernelGGL(powf_batch_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_x, d_y, d_out, n);
+    return hipGetLastError() == hipSuccess ? RT_OK : RT_ERR_HIP;
+}
+
+extern "C" rt_status rt_powf_batch_host(const float* x, const float* y, float* out, uint64_t n) {
+    if (n && (!x || !y || !out)) return RT_ERR_INVALID_ARG;
+    for (uint64_t i = 0; i < n; i++) out[i] = rtpow::powf_glibc(x[i], y[i]);
+    return RT_OK;
+}
