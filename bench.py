@@ -236,6 +236,18 @@ def seam_stats(args, scene, pipe, tiler, dev):
             walls.append((time.perf_counter() - t0) * 1e3)
         out["rt_render_with_host_copy_ms"] = round(min(walls), 3)
         out["rt_render_with_host_copy_mpixels_per_s"] = round(args.width * args.height / (min(walls) / 1e3) / 1e6, 3)
+        # the same seam into a page-locked caller buffer (rt_host_alloc: a RenderBuffer
+        # allocated for DMA)
+        from rust_tracer_amd import HostFrame
+        hf = HostFrame(args.width, args.height)
+        scene.render(args.width, args.height, args.depth, out=hf.array)
+        walls = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            scene.render(args.width, args.height, args.depth, out=hf.array)
+            walls.append((time.perf_counter() - t0) * 1e3)
+        hf.close()
+        out["rt_render_pinned_host_copy_ms"] = round(min(walls), 3)
     t0 = time.perf_counter()
     c = scene.clone(dev.index)
     out["scene_clone_ms"] = round((time.perf_counter() - t0) * 1e3, 2)

@@ -159,6 +159,13 @@ typedef struct rt_scene rt_scene;
 rt_status rt_scene_create(const rt_scene_desc* desc, int32_t device, rt_scene** out);
 rt_status rt_scene_destroy(rt_scene* scene);
 
+/* Page-locked host memory for a caller's frame buffer (the RenderBuffer a render() caller
+ * owns, render.rs:5-19): rt_render's device-to-host copy of the frame then runs at the
+ * link's DMA rate instead of through a pageable staging copy.  Any host pointer stays
+ * valid for rt_render; this is an optional fast path.  rt_host_free releases it. */
+rt_status rt_host_alloc(uint64_t bytes, void** out);
+rt_status rt_host_free(void* ptr);
+
 /* A second handle of the same scene on `device` (-1 = current), copied device-to-device (no
  * host rebuild): its own workspace and stream, so two handles can render concurrently
  * (frames in flight) or on two GPUs. */

@@ -331,12 +331,15 @@ class DeviceScene:
               "rt_scene_scan_ops")
         return dict(zip(self.SCAN_OPS, (int(v) for v in out)))
 
-    def render(self, x_res, y_res, depth, want_u8=False, device=-1, spp=1, seed=0, cam=None):
+    def render(self, x_res, y_res, depth, want_u8=False, device=-1, spp=1, seed=0, cam=None, out=None):
         """render.rs:31-38 -> (rgb float32 [y_res, x_res, 3], counters dict, kernel_ms, rgb8).
         spp > 1: jittered supersampling (rt_render_spp, BASELINE config 5).  cam: an
-        abi.rt_camera (default Camera::new(x_res, y_res), render.rs:166-176)."""
+        abi.rt_camera (default Camera::new(x_res, y_res), render.rs:166-176).  out: the
+        caller's float32 [y_res, x_res, 3] buffer to fill (e.g. a HostFrame's array)."""
         cam = cam if cam is not None else camera(x_res, y_res)
-        rgb = np.zeros((y_res, x_res, 3), np.float32)
+        if out is not None:
+            assert out.dtype == np.float32 and out.shape == (y_res, x_res, 3) and out.flags.c_contiguous
+        rgb = out if out is not None else np.zeros((y_res, x_res, 3), np.float32)
         rgb8 = np.zeros((y_res, x_res, 3), np.uint8) if want_u8 else None
         cnt = abi.rt_counters()
         ms = C.c_float(0)
@@ -448,6 +451,31 @@ class DeviceForest:
         return {"num_trees": n, "num_intersections": int(sizes.sum()), "smallest_tree": int(sizes.min()),
                 "largest_tree": int(sizes.max()), "median": int(sizes[n // 2]), "p90": at(0.9),
                 "p95": at(0.95), "p99": at(0.99)}
+
+
+class HostFrame:
+    """A float32 [h, w, 3] frame in page-locked host memory (rt_host_alloc): rt_render's
+    device-to-host copy into it runs at the link's DMA rate."""
+
+    def __init__(self, w, h):
+        self._L = lib()
+        self.ptr = C.c_void_p()
+        n = w * h * 3 * 4
+        check(self._L.rt_host_alloc(n, C.byref(self.ptr)), "rt_host_alloc")
+        buf = (C.c_uint8 * n).from_address(self.ptr.value)
+        self.array = np.frombuffer(buf, dtype=np.float32).reshape(h, w, 3)
+
+    def close(self):
+        if self.ptr:
+            self.array = None
+            self._L.rt_host_free(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def write_image(path, rgb8):

@@ -151,6 +151,8 @@ def lib():
     L.rt_scene_workspace_bytes.argtypes = [vp]
     L.rt_powf_batch_async.argtypes = [vp, vp, vp, C.c_uint64, vp]
     L.rt_powf_batch_host.argtypes = [vp, vp, vp, C.c_uint64]
+    L.rt_host_alloc.argtypes = [C.c_uint64, C.POINTER(vp)]
+    L.rt_host_free.argtypes = [vp]
     L.rt_scene_workspace_bytes.restype = C.c_uint64
     L.rt_scene_scan_ops.argtypes = [vp, P(C.c_uint64), C.c_uint32, C.c_int32]
     L.rt_scene_set_scan_counting.argtypes = [vp, C.c_int32]

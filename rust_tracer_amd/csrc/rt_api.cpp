@@ -51,6 +51,8 @@ hipError_t launch_sort(const uint32_t* levels, int32_t level, uint32_t cap, uint
                          uint32_t max_digit);
 uint32_t sort_max_tiles(uint32_t cap);
 uint32_t sort_max_digits();
+hipError_t launch_spp_accumulate(const float* samples, uint32_t n, size_t frame_floats, uint32_t first, uint32_t spp,
+                                 float* out, uint8_t* out8, hipStream_t stream);
 }  // namespace rtdev
 
 using namespace rtdev;
@@ -1061,6 +1063,9 @@ struct Workspace {
     float4* node_dc = nullptr;       // [2 x capacity] children's directions
     uint32_t* node_key = nullptr;
     uint32_t* node_pixel = nullptr;
+    // sample batches: one band buffer per sample of a batch (launch_bands_wave)
+    float* spp_buf = nullptr;
+    size_t spp_buf_floats = 0;
 };
 
 // RT_SORT=0 keeps the queues in production order, RT_SORT=shadow orders only the
@@ -1251,7 +1256,7 @@ void free_workspace(Workspace& w) {
                     (void*)w.node_flags, (void*)w.levels, (void*)w.overflow, (void*)w.node_ps, (void*)w.node_n,
                     (void*)w.node_d, (void*)w.node_lit, (void*)w.node_ec, (void*)w.task_keys, (void*)w.perm,
                     (void*)w.shadow_keys, (void*)w.shadow_sorted, (void*)w.sort_tmp, (void*)w.node_dc,
-                    (void*)w.node_key, (void*)w.node_pixel})
+                    (void*)w.node_key, (void*)w.node_pixel, (void*)w.spp_buf})
         if (b) (void)hipFree(b);
     w = Workspace();
 }
@@ -1546,6 +1551,21 @@ rt_status rt_scene_destroy(rt_scene* s) {
     return RT_OK;
 }
 
+rt_status rt_host_alloc(uint64_t bytes, void** out) {
+    if (!out || bytes == 0) return RT_ERR_INVALID_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return RT_ERR_NO_DEVICE;
+    HIP_TRY(hipHostMalloc(out, bytes, hipHostMallocPortable));
+    return RT_OK;
+}
+
+rt_status rt_host_free(void* ptr) {
+    if (!ptr) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipHostFree(ptr));
+    return RT_OK;
+}
+
 uint64_t rt_scene_flops_per_scan(const rt_scene* s) { return s ? s->flops_per_scan : 0; }
 
 uint64_t rt_scene_workspace_bytes(const rt_scene* s) {
@@ -1557,6 +1577,7 @@ uint64_t rt_scene_workspace_bytes(const rt_scene* s) {
     b += (uint64_t)w.sort_capacity * 8;                                      // task keys, permutation
     b += (uint64_t)w.shadow_capacity * 4 + (uint64_t)w.sort_shadow_capacity * 8;
     b += (uint64_t)w.sort_tmp_words * 4;
+    b += (uint64_t)w.spp_buf_floats * 4;
     if (w.levels) b += RT_LEVEL_TABLE_WORDS * 4 + 64;
     return b;
 }
@@ -1679,13 +1700,58 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
                                uint32_t rank, uint32_t world, const PassOut& o, hipStream_t stream,
                                WaveParams* forest_params, uint32_t* forest_levels, uint32_t spp = 1,
                                uint32_t sample = 0, uint32_t seed = 0, uint32_t frames = 1,
-                               const rt_camera* cams = nullptr);
+                               const rt_camera* cams = nullptr, bool spp_batch = false);
 
-// spp samples: one pipeline run per sample, in sample order (the level-0 combine adds
-// sample k's colour to the running sum of samples 0..k-1 and the last one divides)
+// Samples per pipeline pass for spp > 1: RT_SPP_BATCH, else as many (<= RT_MAX_FRAMES) as
+// keep a pass within RT_SPP_BATCH_ITEMS level-0 items (default 2^25: 4 x 3840x2160 or
+// 8 x 1920x1080; the pass's workspace grows with its items).
+static uint32_t spp_batch_size(uint32_t spp, uint64_t frame_items) {
+    if (const char* e = std::getenv("RT_SPP_BATCH")) {
+        const int v = std::atoi(e);
+        return (uint32_t)std::max(1, std::min(v, (int)RT_MAX_FRAMES));
+    }
+    const char* ei = std::getenv("RT_SPP_BATCH_ITEMS");
+    const uint64_t cap = ei ? std::strtoull(ei, nullptr, 0) : (1ull << 25);
+    uint32_t b = 1;
+    while (b < RT_MAX_FRAMES && b < spp && (uint64_t)(b + 1) * frame_items <= cap) b++;
+    return b;
+}
+
+// spp samples in sample order.  Batched (the default): B samples per pipeline pass, each a
+// "frame" of the pass with the same camera and its own jitter (sample index = base + frame),
+// its raw colour written to its own buffer; spp_accumulate_kernel then folds the batch into
+// the running sum in sample order and the last batch divides -- the same f32 operations as
+// one pass per sample, where the level-0 combine adds sample k's colour to the running sum
+// of samples 0..k-1 and the last one divides (RT_SPP_BATCH=1).
 static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
                                    uint32_t band_rows, uint32_t rank, uint32_t world, const PassOut& o,
                                    hipStream_t stream) {
+    const uint32_t rows_local = rt_band_rows_per_rank(cam->y_res, band_rows, world);
+    const uint64_t frame_items = (uint64_t)((cam->x_res + 7) / 8) * ((rows_local + 7) / 8) * 64u;
+    const uint32_t sb = spp > 1 && o.rgb && (uint64_t)cam->x_res * cam->y_res < (1ull << RT_FRAME_SHIFT)
+                            ? spp_batch_size(spp, frame_items) : 1u;
+    if (sb > 1) {
+        Workspace& w = s->ws;
+        const size_t frame_floats = (size_t)rows_local * cam->x_res * 3u;
+        if (w.spp_buf_floats < sb * frame_floats) {
+            if (w.spp_buf) (void)hipFree(w.spp_buf);
+            w.spp_buf = nullptr;
+            w.spp_buf_floats = 0;
+            HIP_TRY(hipMalloc(&w.spp_buf, sb * frame_floats * sizeof(float)));
+            w.spp_buf_floats = sb * frame_floats;
+        }
+        rt_camera cams[RT_MAX_FRAMES];
+        for (uint32_t f = 0; f < sb; f++) cams[f] = *cam;
+        const PassOut ob{w.spp_buf, nullptr, o.counters, o.latch, o.may_sync};
+        for (uint32_t k = 0; k < spp; k += sb) {
+            const uint32_t b = std::min(sb, spp - k);
+            rt_status st = wave_pipeline(s, w, cam, depth, band_rows, rank, world, ob, stream, nullptr, nullptr, spp, k,
+                                         seed, b, cams, true);
+            if (st != RT_OK) return st;
+            HIP_TRY(launch_spp_accumulate(w.spp_buf, b, frame_floats, k, spp, o.rgb, o.rgb8, stream));
+        }
+        return RT_OK;
+    }
     for (uint32_t k = 0; k < spp; k++) {
         rt_status st = wave_pipeline(s, s->ws, cam, depth, band_rows, rank, world, o, stream, nullptr, nullptr, spp, k,
                                      seed);
@@ -1697,11 +1763,19 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
 static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
                                uint32_t rank, uint32_t world, const PassOut& o, hipStream_t stream,
                                WaveParams* forest_params, uint32_t* forest_levels, uint32_t spp, uint32_t sample,
-                               uint32_t seed, uint32_t frames, const rt_camera* cams) {
+                               uint32_t seed, uint32_t frames, const rt_camera* cams, bool spp_batch) {
     if (frames == 0 || frames > RT_MAX_FRAMES || (frames > 1 && (!cams || forest_params))) return RT_ERR_INVALID_ARG;
     WaveParams p;
     std::memset(&p, 0, sizeof(p));
     p.spp = spp;
+    p.spp_batch = spp_batch ? 1u : 0u;
+    // queue keys of a sample batch: "mix" (default) -- no sample index in the keys, the
+    // samples of one place share waves; "mixfine" -- the same with a frame batch's finer
+    // 21-bit task / 4-bit-distance shadow keys; "frame" -- the sample index above the key bits
+    // like a frame batch (RT_SPP_KEYS, A/B)
+    const char* sk = std::getenv("RT_SPP_KEYS");
+    const int spp_keys = !spp_batch ? 2 : (!sk ? 0 : (std::strcmp(sk, "mixfine") == 0 ? 1 : (std::strcmp(sk, "frame") == 0 ? 2 : 0)));
+    p.frame_keys = spp_keys == 2 ? 1u : 0u;
     p.sample = sample;
     p.seed = seed;
     p.S = s->S;
@@ -1844,13 +1918,14 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         p.shadow_cell = (cell && p.shadow_fine == 18u && s->S.lb_res && cells < (1u << 17)) ? cell : 0u;
     }
     if (p.shadow_fine) shadow_bits = p.shadow_fine + lbits;
-    if (frames > 1) {  // the frame index above every key bit: frames are contiguous in sorted queues (ordering only)
+    if (frames > 1 && spp_keys != 0) {  // the frame index above every key bit: frames are contiguous in sorted queues (ordering only)
         uint32_t fbits = 0;
         while ((1u << fbits) < frames) fbits++;
+        if (!p.frame_keys) fbits = 0;  // "mixfine": the finer keys without the sample index
         // a batch's task keys take 3 radix passes of 8 bits anyway: key mode 7 fills them with
         // 5 more origin bits (RT_TASK_FINE=0: off, A/B)
         const char* tf = std::getenv("RT_TASK_FINE");
-        if (!(tf && tf[0] == '0') && p.key_mode == 7 && task_bits == 16u && fbits >= 1 && fbits <= 3) {
+        if (!(tf && tf[0] == '0') && p.key_mode == 7 && task_bits == 16u && fbits <= 3) {
             p.task_fine = 1u;
             task_bits = 21u;
         }

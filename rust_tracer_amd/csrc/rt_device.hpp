@@ -243,6 +243,11 @@ struct WaveParams {
     // supersampling (rt_render_spp): this pipeline run traces sample `sample` of `spp`;
     // level 0 jitters the primary ray (spp > 1) and the level-0 combine accumulates
     uint32_t spp, sample, seed;
+    // sample batches (rt_api.cpp launch_bands_wave): this pass's `frames` are samples
+    // sample + f of one camera; the level-0 combine writes each sample's raw colour to its
+    // own buffer (out + f x frame_floats) and spp_accumulate_kernel sums them in sample order
+    uint32_t spp_batch;
+    uint32_t frame_keys;               // frames > 1: the frame index sits above the queue keys' bits
     uint32_t self_shadow;              // trace decides shadow rays its own shape settles (A/B: RT_SELF_SHADOW=0)
     uint32_t inline_levels;            // trace levels < this trace their own shadow rays (RT_INLINE_SHADOW)
     uint32_t sched;                    // work distribution of trace / shadow launches (rt_wavefront.hip sched_base)

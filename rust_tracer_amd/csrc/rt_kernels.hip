@@ -389,6 +389,39 @@ hipError_t launch_quantize(const float* in, size_t n, uint8_t* out, hipStream_t 
 
 }  // namespace rtdev
 
+namespace rtdev {
+
+// ---- sample batches (rt_api.cpp launch_bands_wave): the batch's samples first .. first + n - 1
+// were rendered into n buffers of frame_floats floats; fold them into `out` in sample order
+// -- sample 0 starts the sum, each later sample is added to it (the f32 sample-order sum of
+// rt_render_spp, include/rt_api.h) -- and the batch holding the last sample divides by spp
+// and writes Color::as_u8 (color.rs:43-46) of the mean.
+__global__ void spp_accumulate_kernel(const float* samples, uint32_t n, size_t frame_floats, uint32_t first,
+                                      uint32_t spp, float* out, uint8_t* out8) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const bool last = first + n == spp;
+    const float fs = (float)spp;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < frame_floats; i += stride) {
+        float acc = first == 0 ? samples[i] : out[i] + samples[i];
+        for (uint32_t j = 1; j < n; j++) acc = acc + samples[(size_t)j * frame_floats + i];
+        if (last) {
+            acc = acc / fs;
+            if (out8) out8[i] = as_u8(acc);
+        }
+        out[i] = acc;
+    }
+}
+
+hipError_t launch_spp_accumulate(const float* samples, uint32_t n, size_t frame_floats, uint32_t first, uint32_t spp,
+                                 float* out, uint8_t* out8, hipStream_t stream) {
+    const uint32_t blocks = (uint32_t)std::min<size_t>((frame_floats + 255) / 256, 8192u);
+    hipLaunchKernelGGL(spp_accumulate_kernel, dim3(blocks), dim3(256), 0, stream, samples, n, frame_floats, first, spp,
+                       out, out8);
+    return hipGetLastError();
+}
+
+}  // namespace rtdev
+
 // ---- powf verification hooks (tests/test_powf.py): the device's powf (rt_powf.hpp) over
 // arrays, on the device and compiled for the host, against the oracle's libm powf
 __global__ void powf_batch_kernel(const float* x, const float* y, float* out, uint64_t n) {

@@ -417,9 +417,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                         active = false;
                     } else {
                         float fu = (float)px.u, fv = (float)px.v;
-                        if (P.spp > 1) {  // sample `P.sample` of the pixel: (u + jx, v + jy)
-                            fu = fu + spp_jitter(P.seed, pix, P.sample, 0u);
-                            fv = fv + spp_jitter(P.seed, pix, P.sample, 1u);
+                        if (P.spp > 1) {  // sample `P.sample` (+ frame: a sample batch) of the pixel: (u + jx, v + jy)
+                            const uint32_t smp = P.sample + (P.spp_batch ? fr : 0u);
+                            fu = fu + spp_jitter(P.seed, pix, smp, 0u);
+                            fv = fv + spp_jitter(P.seed, pix, smp, 1u);
                         }
                         // the frame's camera (cams[0] = the camera when frames == 1); a
                         // wave's 64 items are one tile of one frame: fr is wave-uniform
@@ -552,7 +553,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         // ---- children -> level k+1 queue
         uint32_t nc = (want_refl ? 1u : 0u) + (want_refr ? 1u : 0u);
         uint32_t my = wave_append(&P.levels[2 * (level + 1) + 1], nc, lane);
-        const uint32_t fkey = P.frames > 1 ? ((pix >> RT_FRAME_SHIFT) << P.task_frame_shift) : 0u;
+        const uint32_t fkey = (P.frames > 1 && P.frame_keys) ? ((pix >> RT_FRAME_SHIFT) << P.task_frame_shift) : 0u;
         // inside keys: the children carry the frame bits and the enclosing shape + 1
         const uint32_t cpix = inside_keys ? (pix & ~RT_INSIDE_MASK) : pix, own = sh_key >> 4;
         if (want_refl) {
@@ -677,7 +678,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                             }
                             P.shadow_keys[slot] = (P.shadow_fine ? (((uint32_t)li << P.shadow_fine) | low)
                                                                    : ((uint32_t)li << P.light_shift) | (mort >> (15u - P.light_shift)))
-                                                  | (P.frames > 1 ? ((pix >> RT_FRAME_SHIFT) << P.shadow_frame_shift) : 0u);
+                                                  | ((P.frames > 1 && P.frame_keys) ? ((pix >> RT_FRAME_SHIFT) << P.shadow_frame_shift) : 0u);
                         }
                     } else
                         atomicOr(P.overflow, 2u);
@@ -927,7 +928,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_COMBINE_
             bool last = true;
             if (P.out) {  // (null: an RGB8-only pass, spp == 1)
                 float* o = P.out + (size_t)fr * P.frame_floats + i * 3u;
-                if (P.spp > 1) {  // the f32 sum of the samples in sample order, then / spp
+                if (P.spp_batch) {  // this sample's raw colour; spp_accumulate_kernel sums in sample order
+                    last = false;
+                } else if (P.spp > 1) {  // the f32 sum of the samples in sample order, then / spp
                     if (P.sample > 0) c = v3(o[0] + c.x, o[1] + c.y, o[2] + c.z);
                     last = P.sample + 1 == P.spp;
                     if (last) {
@@ -1069,10 +1072,21 @@ static bool lds_nodes_for(const WaveParams& p, const char* kernel) {
 hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_blocks, int* combine_blocks) {
     const size_t lds = lds_bytes(p);
     const bool aware = !getenv("RT_OCC_NOLDS");  // A/B: size the grids as if no LDS were used
-    hipError_t e = aware && lds_nodes_for(p, "trace")
-                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(trace_blocks, trace_level_kernel<false, true>, 256, lds)
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(trace_blocks, trace_level_kernel<false, false>, 256, 0);
+    // every trace instantiation launch_wave_trace may pick (generic, level 0, deep levels):
+    // the grid is sized by the least occupancy among them, so every block is resident
+    const bool tl = aware && lds_nodes_for(p, "trace");
+    int tv[3] = {0, 0, 0};
+    hipError_t e =
+        tl ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&tv[0], trace_level_kernel<false, true>, 256, lds)
+           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&tv[0], trace_level_kernel<false, false>, 256, 0);
     if (e != hipSuccess) return e;
+    e = tl ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&tv[1], trace_level_kernel<false, true, false, true>, 256, lds)
+           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&tv[1], trace_level_kernel<false, false, false, true>, 256, 0);
+    if (e != hipSuccess) return e;
+    e = tl ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&tv[2], trace_level_kernel<false, true, true>, 256, lds)
+           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&tv[2], trace_level_kernel<false, false, true>, 256, 0);
+    if (e != hipSuccess) return e;
+    *trace_blocks = std::min(tv[0], std::min(tv[1], tv[2]));
     e = aware && lds_nodes_for(p, "shadow")
             ? hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<true, false>, 256, lds)
             : hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<false, false>, 256, 0);

@@ -113,3 +113,49 @@ def test_spp_zero_rejected_and_mega_unsupported():
     finally:
         del os.environ["RT_PIPELINE"]
     s.close()
+
+
+@pytest.mark.parametrize("keys", ["mix", "mixfine", "frame"])
+def test_sample_batches_change_nothing(monkeypatch, keys):
+    """Samples batched B per pipeline pass (each a frame of the pass with its own jitter,
+    summed in sample order by spp_accumulate_kernel) equal one pass per sample
+    (RT_SPP_BATCH=1) bit for bit, RGB8 included -- 19 samples: batches of 8, 8 and 3, so the
+    running sum crosses batches and the last batch is partial; every queue-key variant."""
+    desc = SceneDesc.synth_config(5)
+    w, h, spp = 160, 90, 19
+    monkeypatch.setenv("RT_SPP_BATCH", "1")
+    s = DeviceScene(desc, device=0)
+    ref, rcnt, _, ref8 = s.render(w, h, 8, spp=spp, seed=3, want_u8=True)
+    s.close()
+    monkeypatch.setenv("RT_SPP_BATCH", "8")
+    monkeypatch.setenv("RT_SPP_KEYS", keys)
+    s = DeviceScene(desc, device=0)
+    img, cnt, _, img8 = s.render(w, h, 8, spp=spp, seed=3, want_u8=True)
+    s.close()
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+    assert np.array_equal(img8, ref8) and cnt == rcnt
+
+
+def test_sample_batches_in_bands(monkeypatch):
+    """A band share (rank 1 of 3) of a supersampled frame: batched samples equal one pass per
+    sample (the multi-GPU path of config 5)."""
+    import torch
+    from rust_tracer_amd import abi, band_rows_per_rank
+    desc = SceneDesc.synth_config(5)
+    w, h, spp, world = 200, 117, 10, 3
+    dev = torch.device("cuda", 0)
+    rpr = band_rows_per_rank(h, 8, world)
+    outs = []
+    for b in ("1", "4"):
+        monkeypatch.setenv("RT_SPP_BATCH", b)
+        s = DeviceScene(desc, device=0)
+        out = torch.full((rpr, w, 3), -1.0, device=dev)
+        cnt = torch.zeros(3, dtype=torch.int64, device=dev)
+        s.render_bands_async(abi.camera(w, h), 8, 8, 1, world, out.data_ptr(), cnt.data_ptr(),
+                             torch.cuda.current_stream(dev).cuda_stream, spp=spp, seed=3)
+        torch.cuda.synchronize()
+        s.sync_status()
+        outs.append((out.cpu().numpy(), cnt.cpu().numpy()))
+        s.close()
+    assert np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))
+    assert np.array_equal(outs[0][1], outs[1][1])
