@@ -1773,8 +1773,13 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     // samples of one place share waves; "mixfine" -- the same with a frame batch's finer
     // 21-bit task / 4-bit-distance shadow keys; "frame" -- the sample index above the key bits
     // like a frame batch (RT_SPP_KEYS, A/B)
-    const char* sk = std::getenv("RT_SPP_KEYS");
-    const int spp_keys = !spp_batch ? 2 : (!sk ? 0 : (std::strcmp(sk, "mixfine") == 0 ? 1 : (std::strcmp(sk, "frame") == 0 ? 2 : 0)));
+    // (frame batches: RT_FRAME_KEYS, default "frame")
+    const char* sk = std::getenv(spp_batch ? "RT_SPP_KEYS" : "RT_FRAME_KEYS");
+    const int key_default = spp_batch ? 0 : 2;
+    const int spp_keys = !sk ? key_default
+                             : (std::strcmp(sk, "mixfine") == 0 ? 1
+                                                                : (std::strcmp(sk, "frame") == 0 ? 2
+                                                                                                 : (std::strcmp(sk, "mix") == 0 ? 0 : key_default)));
     p.frame_keys = spp_keys == 2 ? 1u : 0u;
     p.sample = sample;
     p.seed = seed;
@@ -1918,6 +1923,21 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         p.shadow_cell = (cell && p.shadow_fine == 18u && s->S.lb_res && cells < (1u << 17)) ? cell : 0u;
     }
     if (p.shadow_fine) shadow_bits = p.shadow_fine + lbits;
+    if (frames == 1 && !forest_params) {
+        // RT_FINE1=1 (A/B): one frame gets a batch's finer keys too -- 21-bit task keys and
+        // the 4-bit shadow distance (3 radix passes each)
+        const char* f1 = std::getenv("RT_FINE1");
+        if (f1 && f1[0] == '1' && p.key_mode == 7 && task_bits == 16u) {
+            p.task_fine = 1u;
+            task_bits = 21u;
+            if (p.shadow_cell == 2u && p.shadow_fine == 18u && shadow_bits + 1u <= 24u &&
+                6ull * s->S.lb_res * s->S.lb_res * 16u < (1u << 18)) {
+                p.shadow_cell = 3u;
+                p.shadow_fine = 19u;
+                shadow_bits += 1u;
+            }
+        }
+    }
     if (frames > 1 && spp_keys != 0) {  // the frame index above every key bit: frames are contiguous in sorted queues (ordering only)
         uint32_t fbits = 0;
         while ((1u << fbits) < frames) fbits++;
