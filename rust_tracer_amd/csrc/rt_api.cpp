@@ -1861,6 +1861,10 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     }
     p.self_shadow = self_shadow_enabled() ? 1u : 0u;
     {
+        const char* e = std::getenv("RT_REVERSE");  // bit mask of levels traced from the queue's end (A/B)
+        p.reverse_levels = e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
+    }
+    {
         // primary hits are coherent (8x8 tiles): their shadow rays are traced inline by the
         // trace kernel (config 3: -2%); deeper levels' hit points are scattered and go
         // through the sorted shadow queue (inlining levels 0-1: +20%, all: x2.4)

@@ -13,6 +13,30 @@
 #include "../../include/rt_api.h"
 #include "rt_device.hpp"
 #include "rt_powf.hpp"
+// the specular power (material.rs:211): glibc's powf, bit for bit; RT_POWF_OCML=1 builds
+// ocml's powf instead (timing A/B only -- not the reference's values)
+#if RT_POWF_OCML
+#define RT_POW(x, y) powf((x), (y))
+#elif RT_POWF_LDS
+// the tables in LDS: every kernel that shades calls rt_pow_stage() first
+__shared__ rtpow::Log2Entry rt_pow_log2[16];
+__shared__ uint64_t rt_pow_exp2[32];
+struct LdsTabs {
+    __device__ static inline rtpow::Log2Entry log2(int i) { return rt_pow_log2[i]; }
+    __device__ static inline uint64_t exp2(uint32_t i) { return rt_pow_exp2[i]; }
+};
+__device__ __forceinline__ void rt_pow_stage() {
+    if (threadIdx.x < 16) rt_pow_log2[threadIdx.x] = rtpow::kLog2Tab[threadIdx.x];
+    if (threadIdx.x < 32) rt_pow_exp2[threadIdx.x] = rtpow::kExp2Tab[threadIdx.x];
+    __syncthreads();
+}
+#define RT_POW(x, y) rtpow::powf_glibc<true, LdsTabs>((x), (y))
+#else
+#define RT_POW(x, y) rtpow::powf_glibc((x), (y))
+#endif
+#if !RT_POWF_LDS
+__device__ __forceinline__ void rt_pow_stage() {}
+#endif
 
 namespace rtdev {
 
@@ -271,7 +295,7 @@ __device__ __forceinline__ V3 reflected_energy_ne(V3 E, V3 l, V3 n, V3 ne, V3 kd
     float mh = dot(n, hv);
     V3 spec = v3(0.f, 0.f, 0.f);
     if (!(mh < 0.f)) {
-        float pw = rtpow::powf_glibc(mh, power);  // material.rs:211, glibc's powf
+        float pw = RT_POW(mh, power);  // material.rs:211, glibc's powf
         spec = v3((pw * E.x) * ks.x, (pw * E.y) * ks.y, (pw * E.z) * ks.z);
     }
     return v3((ln * E.x) * kd.x + spec.x, (ln * E.y) * kd.y + spec.y, (ln * E.z) * kd.z + spec.z);
@@ -330,7 +354,7 @@ __device__ __forceinline__ void node_weights(const MatRec& M, V3 rd, V3 n, V3 ne
         const float mh = dot(n, hv);
         if (!(mh < 0.f)) {
             f.flags |= F_SPEC;
-            f.pw = rtpow::powf_glibc(mh, M.power);
+            f.pw = RT_POW(mh, M.power);
         }
     }
     if (M.refraction_index > RT_EPS) {

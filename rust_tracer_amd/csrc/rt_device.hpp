@@ -253,6 +253,7 @@ struct WaveParams {
     uint32_t sched;                    // work distribution of trace / shadow launches (rt_wavefront.hip sched_base)
     uint32_t* task_clock;              // debug (RT_TASK_CLOCK): [0] count, then {level, base, ticks, lanes} per wave iteration
     uint32_t task_clock_cap;
+    uint32_t reverse_levels;           // bit k: level k's queue is traced from its end (A/B, RT_REVERSE)
     uint32_t task_w_min;               // narrowest trace task (rays per wave iteration; 64 = never narrowed)
     float task_w_fill;                 // trace tasks are narrowed while a level has fewer than fill x wave slots of them
 };

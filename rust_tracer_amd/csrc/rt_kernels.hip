@@ -36,6 +36,7 @@ namespace rtdev {
 
 template <int MAXF>
 __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
+    rt_pow_stage();
     const DevScene& S = P.S;
     const V3 cam_o = v3(P.cam_ox, P.cam_oy, P.cam_oz);
     const uint32_t lane = lane_id();

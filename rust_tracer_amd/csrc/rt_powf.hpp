@@ -100,7 +100,14 @@ RT_HD inline int checkint(uint32_t iy) {
 RT_HD inline bool zeroinfnan(uint32_t ix) { return 2 * ix - 1 >= 2u * 0x7f800000 - 1; }
 RT_HD inline bool issignaling(uint32_t ix) { return 2 * (ix ^ 0x00400000) > 2u * 0x7fc00000; }
 
-template <bool FMA>
+// Where the tables are read from: the constexpr copies (constant memory on the device), or
+// a kernel's LDS copy (rt_common.hpp RT_POWF_LDS, staged by rt_pow_stage).
+struct ConstTabs {
+    RT_HD static inline Log2Entry log2(int i) { return kLog2Tab[i]; }
+    RT_HD static inline uint64_t exp2(uint32_t i) { return kExp2Tab[i]; }
+};
+
+template <bool FMA, class Tabs = ConstTabs>
 RT_HD inline double log2_inline(uint32_t ix) {
     const double A[5] = RT_POWF_LOG2_POLY;
     // x = 2^k z, z in [OFF, 2 OFF) with OFF = 0x3f330000; 16 subintervals
@@ -109,8 +116,9 @@ RT_HD inline double log2_inline(uint32_t ix) {
     const uint32_t top = tmp & 0xff800000;
     const uint32_t iz = ix - top;
     const int k = (int32_t)top >> 23;  // arithmetic shift
-    const double invc = kLog2Tab[i].invc;
-    const double logc = kLog2Tab[i].logc;
+    const Log2Entry e = Tabs::log2(i);
+    const double invc = e.invc;
+    const double logc = e.logc;
     const double z = (double)as_f32(iz);
     // log2(x) = log1p(z / c - 1) / ln2 + log2(c) + k
     const double r = madd<FMA>(z, invc, -1.0);
@@ -125,7 +133,7 @@ RT_HD inline double log2_inline(uint32_t ix) {
     return y;
 }
 
-template <bool FMA>
+template <bool FMA, class Tabs = ConstTabs>
 RT_HD inline float exp2_inline(double xd, uint32_t sign_bias) {
     const double C[3] = RT_EXP2F_POLY;
     // x = k / 32 + r with r in [-1/64, 1/64]
@@ -134,7 +142,7 @@ RT_HD inline float exp2_inline(double xd, uint32_t sign_bias) {
     kd -= RT_EXP2F_SHIFT_SCALED;
     const double r = xd - kd;
     // exp2(x) = 2^(k/32) * 2^r ~= s * (C0 r^3 + C1 r^2 + C2 r + 1)
-    uint64_t t = kExp2Tab[ki % 32];
+    uint64_t t = Tabs::exp2(ki % 32);
     const uint64_t ski = ki + sign_bias;
     t += ski << (52 - 5);
     const double s = as_f64(t);
@@ -148,7 +156,7 @@ RT_HD inline float exp2_inline(double xd, uint32_t sign_bias) {
 
 // glibc's powf (e_powf.c __powf), value for value; the special cases return what glibc's
 // helpers compute (__math_oflowf / __math_uflowf / __math_invalidf / __math_divzerof).
-template <bool FMA = true>
+template <bool FMA = true, class Tabs = ConstTabs>
 RT_HD inline float powf_glibc(float x, float y) {
     uint32_t sign_bias = 0;
     uint32_t ix = as_u32(x), iy = as_u32(y);
@@ -183,7 +191,7 @@ RT_HD inline float powf_glibc(float x, float y) {
             ix -= 23 << 23;
         }
     }
-    const double logx = log2_inline<FMA>(ix);
+    const double logx = log2_inline<FMA, Tabs>(ix);
     const double ylogx = (double)y * logx;  // cannot overflow: y is single precision
     if ((as_u64(ylogx) >> 47 & 0xffff) >= as_u64(126.0) >> 47) {  // |y * log(x)| >= 126
         if (ylogx > 0x1.fffffffd1d571p+6) {  // __math_oflowf: (+-0x1p97f) * 0x1p97f
@@ -195,7 +203,7 @@ RT_HD inline float powf_glibc(float x, float y) {
             return tiny * 0x1p-95f;
         }
     }
-    return exp2_inline<FMA>(ylogx, sign_bias);
+    return exp2_inline<FMA, Tabs>(ylogx, sign_bias);
 }
 
 }  // namespace rtpow

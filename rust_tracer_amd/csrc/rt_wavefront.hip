@@ -377,6 +377,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
     // sorted levels, grid-stride: this lane's next permutation entry is requested one
     // iteration ahead, so a task costs one dependent load (the task), not two
     const bool pf_on = level > 0 && P.perm && P.sched == 0;
+    const bool rev = level > 0 && ((P.reverse_levels >> min(level, 31u)) & 1u);
     const uint32_t pf_stride = gridDim.x * (blockDim.x >> 6) * W;
     uint32_t pf_slot = 0;
     bool pf_have = false;
@@ -395,13 +396,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         uint32_t pf_next = 0;
         if (pf_on) {
             const uint32_t tn = t + pf_stride;
-            pf_next = (lane < W && tn < count) ? P.perm[off + tn] : 0u;
+            pf_next = (lane < W && tn < count) ? P.perm[off + (rev ? count - 1u - tn : tn)] : 0u;
         }
         typedef decltype(cnt) CntT;
         RT_T0(CntT, t_load);
         V3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
         uint32_t parent = 0, pix = 0, in_shape = 0;
-        const uint32_t n = off + t;
+        // rev: the sorted queue is taken from its end (the keys' high end first)
+        const uint32_t n = off + ((rev && active) ? count - 1u - t : t);
         if (active) {
             if (FIRST || (!DEEP && level == 0)) {
                 const uint32_t fr = P.frames > 1 ? t / P.frame_items : 0u;
@@ -862,6 +864,7 @@ __device__ __forceinline__ V3 light_sum(const DevScene& S, const MatRec& M, cons
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_COMBINE_WAVES, 8))) void combine_level_kernel(
     WaveParams P, uint32_t level) {
+    rt_pow_stage();
     const DevScene& S = P.S;
     const uint32_t off = P.levels[2 * level];
     const uint32_t count = min(P.levels[2 * level + 1], off < P.capacity ? P.capacity - off : 0u);
@@ -966,6 +969,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_COMBINE_
 // (E, dir) of a missing child = (BLACK, 0); a missed child wrote (BLACK, 0) at build time.
 // dirty != null: only nodes of marked pixels are shaded (render_forest_filter).
 __global__ __launch_bounds__(256) void forest_shade_level_kernel(WaveParams P, uint32_t level, float* frame) {
+    rt_pow_stage();
     const DevScene& S = P.S;
     const uint32_t off = P.levels[2 * level];
     const uint32_t count = min(P.levels[2 * level + 1], off < P.capacity ? P.capacity - off : 0u);
