@@ -77,6 +77,10 @@ def parse():
     p.add_argument("--check", type=int, default=1,
                    help="rank 0 compares the timed passes' assembled frames with a single-launch render "
                         "(untimed, on the device; 0 to skip)")
+    p.add_argument("--animate", type=int, default=0,
+                   help="1: every frame its own camera (an animation: the origin moves 0.01 along x per frame, "
+                        "64-frame cycle) instead of K identical frames; the frame check renders each frame's "
+                        "own camera")
     p.add_argument("--force-gather", type=int, default=0,
                    help="at N = 1 under torchrun: assemble every pass through the process group's gather "
                         "and the un-permute kernel anyway (a one-rank RCCL communicator; tests the N > 1 "
@@ -255,13 +259,16 @@ def seam_stats(args, scene, pipe, tiler, dev):
     if pipe.inflight > 1:
         scene.set_grid_share(pipe.grid_share)
     if args.spp == 1:
-        # an animation: every frame its own camera (the origin moves 0.01 per frame along x),
-        # frames in flight and frames per pass as the headline -- the batches hold distinct views
+        # the other workload beside the headline: an animation (every frame its own camera,
+        # the origin moving 0.01 per frame along x) when the headline repeats one camera, or
+        # the repeated camera when the headline is the animation; frames in flight and frames
+        # per pass as the headline
         from rust_tracer_amd import abi as _abi
 
         def cam(i):
             c = _abi.camera(args.width, args.height)
-            c.origin[0] = 0.01 * (i % 64)
+            if not args.animate:
+                c.origin[0] = 0.01 * (i % 64)
             return c
         pipe.run(pipe.inflight * pipe.batch, cameras=cam)
         torch.cuda.synchronize()
@@ -271,8 +278,9 @@ def seam_stats(args, scene, pipe, tiler, dev):
         e1.record(main)
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / k
-        out["distinct_cameras_ms_per_frame"] = round(ms, 4)
-        out["distinct_cameras_mpixels_per_s"] = round(args.width * args.height / (ms / 1e3) / 1e6, 3)
+        tag = "identical_frames" if args.animate else "distinct_cameras"
+        out[f"{tag}_ms_per_frame"] = round(ms, 4)
+        out[f"{tag}_mpixels_per_s"] = round(args.width * args.height / (ms / 1e3) / 1e6, 3)
     if args.spp == 1 and args.depth == 8:
         for t in pipe.tilers:
             t.depth = 9
@@ -369,7 +377,15 @@ def main():
             else:
                 dist.barrier()
 
-    run_frames = pipe.run
+    from rust_tracer_amd import abi as _abi
+
+    def anim_cam(i):
+        c = _abi.camera(args.width, args.height)
+        c.origin[0] = 0.01 * (i % 64)
+        return c
+
+    def run_frames(n, lat=None):
+        pipe.run(n, lat, cameras=anim_cam if args.animate else None)
 
     # slot set-up (untimed, like the scene upload): each slot's workspace is sized by its
     # first full pass
@@ -421,21 +437,32 @@ def main():
         # slot's overflow status), then a fresh single frame, against one rt_render_spp launch
         # of the whole frame -- bit for bit, compared on the device
         frames = list(pipe.frames())
+        fcams = pipe.frame_cameras()
         single = tiler.step()
         if rank == 0:
             frames.append(single)
+            fcams.append(tiler.last_cams[0])
         torch.cuda.synchronize()
         if rank == 0:
-            ref, _, _, ref8 = scene.render(args.width, args.height, args.depth, device=dev.index, spp=args.spp,
-                                           seed=args.seed, want_u8=args.output == "rgb8")
-            single_ref = ref
-            if args.output == "rgb8":
-                r = torch.from_numpy(ref8).to(dev)
-                frame_check = all(bool(torch.equal(f, r)) for f in frames)
-            else:
-                r = torch.from_numpy(ref).to(dev).view(torch.int32)
-                frame_check = all(bool(torch.equal(f.contiguous().view(torch.int32), r)) for f in frames)
+            refs = {}
+            frame_check = True
+            for f, c in zip(frames, fcams):
+                key = tuple(c.origin)
+                if key not in refs:
+                    ref, _, _, ref8 = scene.render(args.width, args.height, args.depth, device=dev.index,
+                                                   spp=args.spp, seed=args.seed, want_u8=args.output == "rgb8",
+                                                   cam=c)
+                    if single_ref is None and key == tuple(_abi.camera(args.width, args.height).origin):
+                        single_ref = ref
+                    refs[key] = (torch.from_numpy(ref8).to(dev) if args.output == "rgb8"
+                                 else torch.from_numpy(ref).to(dev).view(torch.int32))
+                r = refs[key]
+                same = torch.equal(f, r) if args.output == "rgb8" else torch.equal(f.contiguous().view(torch.int32), r)
+                frame_check = frame_check and bool(same)
             frame_checked = len(frames)
+            if single_ref is None:  # the oracle row check needs Camera::new's frame
+                single_ref = scene.render(args.width, args.height, args.depth, device=dev.index, spp=args.spp,
+                                          seed=args.seed)[0]
     seam = seam_stats(args, scene, pipe, tiler, dev) if (args.seam_stats and world == 1) else None
     for t in tilers:  # every stream-ordered pass of the run, incl. the timed ones, was complete
         t.scene.sync_status()
@@ -516,6 +543,8 @@ def main():
                 "width": args.width, "height": args.height, "depth": args.depth,
                 "leaf_primitives": 100 if args.config == 2 else 1000,
                 "spp": args.spp, "seed": args.seed, "band_rows": args.band_rows,
+                "frames": ("animation: frame i's camera origin x = 0.01 (i mod 64)" if args.animate
+                           else "K renders of Camera::new (the reference's bench -n loop, main.rs:137-140)"),
                 "frames_in_flight": inflight * batch, "passes_in_flight": inflight,
                 "frames_per_pass": batch, "pass_latency_ms": round(latency_ms, 4), "output": args.output,
                 "msamples_per_s": round(args.width * args.height * args.spp * steps / elapsed / 1e6, 3),

@@ -1102,6 +1102,13 @@ bool self_shadow_enabled() {
     return !(e && e[0] == '0');
 }
 
+// rt_render on a one-device scene: band shares rendered side by side (RT_SEAM_SPLIT)
+int seam_split() {
+    const char* e = std::getenv("RT_SEAM_SPLIT");
+    const int v = e ? std::atoi(e) : 2;
+    return v < 1 ? 1 : (v > 8 ? 8 : v);
+}
+
 // Workspace sizing: node slots per level-0 item, shadow-queue slots per node slot
 // (measured need, config 3: 3.66 node rays per pixel, 2.0 queued shadow rays per node)
 uint64_t node_factor() {
@@ -1151,6 +1158,8 @@ struct rt_scene {
     uint32_t pool_floor = 0;       // node-pool size the next pass grows to (after a reported overflow)
     double normal_max = 1.0;       // largest hit-normal length (dark_zero of an edited material)
     rt_multi_state* multi = nullptr;  // rt_scene_create_multi: the other devices' clones (rt_multi.cpp)
+    rt_multi_state* split = nullptr;  // rt_render's band shares on this one device (seam_split)
+    int split_n = 0;
 };
 
 rt_multi_state*& rt_scene_multi(rt_scene* s) { return s->multi; }
@@ -1538,6 +1547,8 @@ rt_status rt_scene_destroy(rt_scene* s) {
     if (!s) return RT_ERR_INVALID_ARG;
     if (s->multi) rt_multi_free(s->multi);
     s->multi = nullptr;
+    if (s->split) rt_multi_free(s->split);
+    s->split = nullptr;
     (void)hipSetDevice(s->device);
     if (s->stream) (void)hipStreamSynchronize(s->stream);
     for (auto& se : s->ev_streams) (void)hipEventSynchronize(se.second);  // renders on other streams
@@ -1607,6 +1618,7 @@ int32_t rt_scene_uses_bvh(const rt_scene* s) { return (s && s->S.use_bvh) ? 1 : 
 rt_status rt_scene_set_grid_share(rt_scene* s, int32_t percent) {
     if (!s || percent < 1 || percent > 100) return RT_ERR_INVALID_ARG;
     if (s->multi) (void)rt_multi_each(s->multi, [&](rt_scene* c) { return rt_scene_set_grid_share(c, percent); });
+    if (s->split) (void)rt_multi_each(s->split, [&](rt_scene* c) { return rt_scene_set_grid_share(c, percent); });
     s->grid_pct = percent;
     return RT_OK;
 }
@@ -1614,6 +1626,7 @@ rt_status rt_scene_set_grid_share(rt_scene* s, int32_t percent) {
 rt_status rt_scene_set_scan_counting(rt_scene* s, int32_t enable) {
     if (!s) return RT_ERR_INVALID_ARG;
     if (s->multi) (void)rt_multi_each(s->multi, [&](rt_scene* c) { return rt_scene_set_scan_counting(c, enable); });
+    if (s->split) (void)rt_multi_each(s->split, [&](rt_scene* c) { return rt_scene_set_scan_counting(c, enable); });
     s->count_ops = enable != 0;
     return RT_OK;
 }
@@ -1769,13 +1782,15 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     std::memset(&p, 0, sizeof(p));
     p.spp = spp;
     p.spp_batch = spp_batch ? 1u : 0u;
-    // queue keys of a sample batch: "mix" (default) -- no sample index in the keys, the
-    // samples of one place share waves; "mixfine" -- the same with a frame batch's finer
-    // 21-bit task / 4-bit-distance shadow keys; "frame" -- the sample index above the key bits
-    // like a frame batch (RT_SPP_KEYS, A/B)
+    // queue keys of a sample batch: "mix" -- no sample index in the keys, the samples of one
+    // place share waves; "mixfine" (default) -- the same with a frame batch's finer 21-bit
+    // task / 4-bit-distance shadow keys; "frame" -- the sample index above the key bits like
+    // a frame batch (RT_SPP_KEYS, A/B)
     // (frame batches: RT_FRAME_KEYS, default "frame")
     const char* sk = std::getenv(spp_batch ? "RT_SPP_KEYS" : "RT_FRAME_KEYS");
-    const int key_default = spp_batch ? 0 : 2;
+    // measured (config 5, 4 passes of 4K x 64 samples in batches of 4): mix 1021, mixfine
+    // 1058, frame 1023 Msamples/s; one pass per sample 788
+    const int key_default = spp_batch ? 1 : 2;
     const int spp_keys = !sk ? key_default
                              : (std::strcmp(sk, "mixfine") == 0 ? 1
                                                                 : (std::strcmp(sk, "frame") == 0 ? 2
@@ -2292,6 +2307,26 @@ rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t de
     if (!s || !cam || !rgb || spp == 0) return RT_ERR_INVALID_ARG;
     if (opts && opts->device >= 0 && opts->device != s->device) return RT_ERR_INVALID_ARG;
     if (s->multi) return rt_multi_render(s, cam, depth, spp, seed, opts, rgb, rgb8);
+    // One frame as S band shares of this device, rendered side by side on S streams (each
+    // its own scene clone and workspace), exchanged by device copies and un-permuted: the
+    // latency-bound tails of one share's levels overlap the other's work.  RT_SEAM_SPLIT
+    // (default 2; 1 = one pass), RT_SEAM_BAND_ROWS (default 8).  Config 3, 1080p, one MI355X:
+    // 3.76 ms of device time against 4.11 for one pass (4 shares: 5.08).
+    const int split = seam_split();
+    if (split > 1 && !use_megakernel() && cam->y_res >= 16u * (uint32_t)split) {
+        if (s->split_n != split) {
+            if (s->split) rt_multi_free(s->split);
+            s->split = nullptr;
+            s->split_n = 0;
+            std::vector<int32_t> devs((size_t)split, s->device);
+            rt_status st = rt_multi_build(s, devs.data(), (uint32_t)split, false, &s->split);
+            if (st != RT_OK) return st;
+            s->split_n = split;
+            const char* br = std::getenv("RT_SEAM_BAND_ROWS");
+            rt_multi_set_band_rows(s->split, br ? (uint32_t)std::atoi(br) : 8u);
+        }
+        return rt_multi_render_state(s->split, cam, depth, spp, seed, opts, rgb, rgb8);
+    }
     HIP_TRY(hipSetDevice(s->device));
     size_t n = (size_t)cam->x_res * cam->y_res * 3;
     // one band share holding every row: its buffer has the padded row count (the pass
@@ -2539,6 +2574,10 @@ rt_status rt_scene_set_material(rt_scene* s, uint32_t index, const rt_material* 
     rt_status r = mat_rec(*m, M, s->normal_max);
     if (r != RT_OK) return r;
     HIP_TRY(hipMemcpy(const_cast<MatRec*>(s->S.mats) + index, &M, sizeof(M), hipMemcpyHostToDevice));
+    if (s->split) {
+        rt_status e = rt_multi_each(s->split, [&](rt_scene* c) { return rt_scene_set_material(c, index, m); });
+        if (e != RT_OK) return e;
+    }
     if (s->multi) return rt_multi_each(s->multi, [&](rt_scene* c) { return rt_scene_set_material(c, index, m); });
     return RT_OK;
 }

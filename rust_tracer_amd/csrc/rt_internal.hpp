@@ -14,6 +14,13 @@ int rt_scene_device_of(const rt_scene* s);
 // rt_render_spp on a multi-device scene (rt_multi.cpp).
 rt_status rt_multi_render(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
                           const rt_render_opts* opts, float* rgb, uint8_t* rgb8);
+rt_status rt_multi_render_state(rt_multi_state* m, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
+                                const rt_render_opts* opts, float* rgb, uint8_t* rgb8);
+// A multi-device state around the primary handle s0 (not owned): clones of s0 on
+// devices[1..], a stream per rank; RCCL when the devices are distinct and allow_rccl.
+rt_status rt_multi_build(rt_scene* s0, const int32_t* devices, uint32_t n_devices, bool allow_rccl,
+                         rt_multi_state** out);
+void rt_multi_set_band_rows(rt_multi_state* m, uint32_t band_rows);
 // Applies `f` to every clone (devices[1..]) of a multi-device scene; first error wins.
 rt_status rt_multi_each(rt_multi_state* m, const std::function<rt_status(rt_scene*)>& f);
 void rt_multi_free(rt_multi_state* m);

@@ -88,6 +88,7 @@ struct rt_multi_state {
     bool rccl = false;
     Rccl lib;
     std::vector<ncclComm_t> comms;
+    uint32_t band_rows = 8;                  // rows per band (block-cyclic over the ranks)
 };
 
 rt_status rt_multi_each(rt_multi_state* m, const std::function<rt_status(rt_scene*)>& f) {
@@ -161,9 +162,13 @@ static rt_status ensure_buffers(rt_multi_state* m, size_t band_floats, size_t fr
 
 rt_status rt_multi_render(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
                           const rt_render_opts* opts, float* rgb, uint8_t* rgb8) {
-    rt_multi_state* m = rt_scene_multi(s);
+    return rt_multi_render_state(rt_scene_multi(s), cam, depth, spp, seed, opts, rgb, rgb8);
+}
+
+rt_status rt_multi_render_state(rt_multi_state* m, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
+                                const rt_render_opts* opts, float* rgb, uint8_t* rgb8) {
     if (!cam || cam->x_res == 0 || cam->y_res == 0) return RT_ERR_INVALID_ARG;
-    const uint32_t world = (uint32_t)m->ranks.size(), band_rows = 8;
+    const uint32_t world = (uint32_t)m->ranks.size(), band_rows = m->band_rows;
     const uint32_t rpr = rt_band_rows_per_rank(cam->y_res, band_rows, world);
     const size_t bf = (size_t)rpr * cam->x_res * 3u, ff = (size_t)cam->y_res * cam->x_res * 3u;
     rt_status st = ensure_buffers(m, bf, ff, rgb8 != nullptr);
@@ -265,6 +270,60 @@ rt_status rt_multi_render(rt_scene* s, const rt_camera* cam, uint32_t depth, uin
     return RT_OK;
 }
 
+rt_status rt_multi_build(rt_scene* s0, const int32_t* devices, uint32_t n_devices, bool allow_rccl,
+                         rt_multi_state** out) {
+    rt_status st = RT_OK;
+    rt_multi_state* m = new (std::nothrow) rt_multi_state();
+    if (!m) return RT_ERR_OUT_OF_MEMORY;
+    m->devices.assign(devices, devices + n_devices);
+    m->ranks.assign(n_devices, nullptr);
+    m->ranks[0] = s0;
+    m->streams.assign(n_devices, nullptr);
+    m->done.assign(n_devices, nullptr);
+    m->band.assign(n_devices, nullptr);
+    m->band8.assign(n_devices, nullptr);
+    m->counters.assign(n_devices, nullptr);
+    auto fail = [&](rt_status e) {
+        rt_multi_free(m);
+        return e;
+    };
+    for (uint32_t r = 0; r < n_devices; r++) {
+        if (r > 0 && (st = rt_scene_clone(s0, devices[r], &m->ranks[r])) != RT_OK) return fail(st);
+        if (hipSetDevice(devices[r]) != hipSuccess ||
+            hipStreamCreateWithFlags(&m->streams[r], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&m->done[r], hipEventDisableTiming) != hipSuccess ||
+            hipMalloc(&m->counters[r], 3 * sizeof(unsigned long long)) != hipSuccess)
+            return fail(RT_ERR_HIP);
+    }
+    if (hipSetDevice(devices[0]) != hipSuccess || hipEventCreate(&m->ev0) != hipSuccess ||
+        hipEventCreate(&m->ev1) != hipSuccess)
+        return fail(RT_ERR_HIP);
+    std::vector<int> sorted(m->devices);
+    std::sort(sorted.begin(), sorted.end());
+    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    if (distinct && allow_rccl) {
+        if (!load_rccl(m->lib)) {
+            std::fprintf(stderr, "rt_multi.cpp: librccl.so.1 not loadable: %s\n", dlerror());
+            return fail(RT_ERR_UNSUPPORTED);
+        }
+        m->comms.assign(n_devices, nullptr);
+        ncclResult_t e = m->lib.init_all(m->comms.data(), (int)n_devices, m->devices.data());
+        if (e != ncclSuccess) {
+            std::fprintf(stderr, "rt_multi.cpp: ncclCommInitAll: %s\n", m->lib.error_string(e));
+            m->comms.clear();
+            return fail(RT_ERR_HIP);
+        }
+        m->rccl = true;
+    }
+    (void)hipSetDevice(devices[0]);
+    *out = m;
+    return RT_OK;
+}
+
+void rt_multi_set_band_rows(rt_multi_state* m, uint32_t band_rows) {
+    if (m && band_rows > 0) m->band_rows = band_rows;
+}
+
 extern "C" {
 
 rt_status rt_scene_create_multi(const rt_scene_desc* desc, const int32_t* devices, uint32_t n_devices,
@@ -284,52 +343,13 @@ rt_status rt_scene_create_multi(const rt_scene_desc* desc, const int32_t* device
         *out = s0;
         return st;
     }
-    rt_multi_state* m = new (std::nothrow) rt_multi_state();
-    if (!m) {
+    rt_multi_state* m = nullptr;
+    st = rt_multi_build(s0, devices, n_devices, true, &m);
+    if (st != RT_OK) {
         rt_scene_destroy(s0);
-        return RT_ERR_OUT_OF_MEMORY;
+        return st;
     }
     rt_scene_multi(s0) = m;  // rt_scene_destroy(s0) frees m from here on
-    m->devices.assign(devices, devices + n_devices);
-    m->ranks.assign(n_devices, nullptr);
-    m->ranks[0] = s0;
-    m->streams.assign(n_devices, nullptr);
-    m->done.assign(n_devices, nullptr);
-    m->band.assign(n_devices, nullptr);
-    m->band8.assign(n_devices, nullptr);
-    m->counters.assign(n_devices, nullptr);
-    auto fail = [&](rt_status e) {
-        rt_scene_destroy(s0);
-        return e;
-    };
-    for (uint32_t r = 0; r < n_devices; r++) {
-        if (r > 0 && (st = rt_scene_clone(s0, devices[r], &m->ranks[r])) != RT_OK) return fail(st);
-        if (hipSetDevice(devices[r]) != hipSuccess ||
-            hipStreamCreateWithFlags(&m->streams[r], hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&m->done[r], hipEventDisableTiming) != hipSuccess ||
-            hipMalloc(&m->counters[r], 3 * sizeof(unsigned long long)) != hipSuccess)
-            return fail(RT_ERR_HIP);
-    }
-    if (hipSetDevice(devices[0]) != hipSuccess || hipEventCreate(&m->ev0) != hipSuccess ||
-        hipEventCreate(&m->ev1) != hipSuccess)
-        return fail(RT_ERR_HIP);
-    std::vector<int> sorted(m->devices);
-    std::sort(sorted.begin(), sorted.end());
-    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-    if (distinct) {
-        if (!load_rccl(m->lib)) {
-            std::fprintf(stderr, "rt_multi.cpp: librccl.so.1 not loadable: %s\n", dlerror());
-            return fail(RT_ERR_UNSUPPORTED);
-        }
-        m->comms.assign(n_devices, nullptr);
-        ncclResult_t e = m->lib.init_all(m->comms.data(), (int)n_devices, m->devices.data());
-        if (e != ncclSuccess) {
-            std::fprintf(stderr, "rt_multi.cpp: ncclCommInitAll: %s\n", m->lib.error_string(e));
-            m->comms.clear();
-            return fail(RT_ERR_HIP);
-        }
-        m->rccl = true;
-    }
     (void)hipSetDevice(devices[0]);
     *out = s0;
     return RT_OK;

@@ -71,6 +71,7 @@ class FrameTiler:
             self.frames = self.locals[:, :height]
         self.frame = self.frames[0] if self.frames is not None else None
         self.last = 1               # frames in the last pass
+        self.last_cams = [self.cam]  # their cameras
 
     def render_local(self, n=1, cams=None):
         """Render n (<= batch) frames of this rank's bands on the current stream; cams: their
@@ -79,6 +80,7 @@ class FrameTiler:
         self.last = n
         assert n <= self.batch
         cams = list(cams) if cams is not None else [self.cam] * n
+        self.last_cams = cams
         if self.rgb8:
             self.scene.render_bands_ex_async(cams, self.depth, self.band_rows, self.rank, self.world, 0,
                                              self.locals.data_ptr(), self.counters.data_ptr(), stream)
@@ -219,6 +221,10 @@ class FramePipeline:
         every slot's overflow status first: an incomplete frame is never returned."""
         self.sync()
         return [t.frames[b] for t in self.tilers if t.frames is not None for b in range(t.last)]
+
+    def frame_cameras(self):
+        """the rt_camera of every frame frames() returns, in the same order"""
+        return [t.last_cams[b] for t in self.tilers if t.frames is not None for b in range(t.last)]
 
     def set_material(self, index, material):
         """rt_scene_set_material on every slot's scene (slot clones are independent copies),
