@@ -61,10 +61,10 @@ def parse():
     p.add_argument("--seed", type=int, default=None, help="jitter seed (default: 3 for config 5)")
     p.add_argument("--band-rows", type=int, default=8)
     p.add_argument("--batch", type=int, default=None,
-                   help="frames per pipeline pass (rt_render_bands_batch_async, <= 8; default: the timed "
+                   help="frames per pipeline pass (rt_render_bands_batch_async, <= 16; default: the timed "
                         "frames spread evenly over the slots, q = ceil(steps / inflight) per slot in equal "
-                        "passes of up to 8 frames (a divisor of q where one is close); 1 for a share above "
-                        "1080p at N = 1 or spp > 1, and a pass stays within 4 x 1080p of pixels per rank at N > 1)")
+                        "passes of up to 16 frames (a divisor of q where one is close) within 8 x 1080p of pixels "
+                        "per pass and rank; 1 for spp > 1, whose samples are batched inside each pass)")
     p.add_argument("--inflight", type=int, default=None,
                    help="frames in flight (F scene handles / HIP streams; default 4 = the box's hardware "
                         "queues per process); 1 = one at a time")
@@ -77,10 +77,10 @@ def parse():
     p.add_argument("--check", type=int, default=1,
                    help="rank 0 compares the timed passes' assembled frames with a single-launch render "
                         "(untimed, on the device; 0 to skip)")
-    p.add_argument("--animate", type=int, default=0,
-                   help="1: every frame its own camera (an animation: the origin moves 0.01 along x per frame, "
-                        "64-frame cycle) instead of K identical frames; the frame check renders each frame's "
-                        "own camera")
+    p.add_argument("--animate", type=int, default=1,
+                   help="1 (default): every frame its own camera (an animation: the origin moves 0.01 along x per "
+                        "frame, 64-frame cycle) -- no two frames of a batch share rays; 0: K renders of one camera "
+                        "(the reference's bench -n loop); the frame check renders each frame's own camera")
     p.add_argument("--force-gather", type=int, default=0,
                    help="at N = 1 under torchrun: assemble every pass through the process group's gather "
                         "and the un-permute kernel anyway (a one-rank RCCL communicator; tests the N > 1 "
@@ -339,19 +339,16 @@ def main():
     if args.batch is None:
         # The timed K frames are spread evenly over the F slots: q = ceil(K / F) frames per
         # slot, in r = ceil(q / cap) passes of B frames -- a divisor of q when one is near
-        # ceil(q / r), so that every slot runs the same passes.  Up to 8 frames per pass
-        # (bounded workspace: <= 4 x 1080p of pixels per pass and rank; ~40 GB per slot at
-        # 8 whole 1080p frames).  ms per share-frame on one MI355X at K = 20 (tools/share_burst.py):
-        # N = 1: B = 2 / 4 / 5 / 8: 2.46 / 2.51 / 2.31 / 2.36; N = 8: 0.533 / 0.464 / 0.389 /
-        # 0.381; N = 1 at K = 160 (tools/ab_batch.sh): B = 5 / 8: 919 / 938 Mpixels/s
+        # ceil(q / r), so that every slot runs the same passes.  Up to 16 frames per pass
+        # (bounded workspace: <= 8 x 1080p of pixels per pass and rank, ~1.1 KB per pixel).
+        # Round 2, ms per share-frame on one MI355X at K = 20 (tools/share_burst.py): N = 1:
+        # B = 2 / 4 / 5 / 8: 2.46 / 2.51 / 2.31 / 2.36; N = 8: 0.533 / 0.464 / 0.389 / 0.381
         # (DESIGN.md "Frame batches")
         share = band_rows_per_rank(args.height, args.band_rows, world) * args.width
         if args.spp > 1:
             cap = 1
-        elif world == 1:
-            cap = 8 if share <= 1920 * 1088 else 1
-        else:
-            cap = max(1, min(8, (4 * 1920 * 1088) // share))
+        else:  # up to 16 frames, within 8 x 1080p of pixels per pass and rank (~18 GB of workspace)
+            cap = max(1, min(16, (8 * 1920 * 1088) // share))
         q = -(-args.steps // inflight)
         r = -(-q // cap)
         b = -(-q // r)
@@ -436,7 +433,8 @@ def main():
         # the timed passes' assembled frames of every slot (pipe.frames() first checks every
         # slot's overflow status), then a fresh single frame, against one rt_render_spp launch
         # of the whole frame -- bit for bit, compared on the device
-        frames = list(pipe.frames())
+        # copies: tiler.step() below re-renders into slot 0's buffers
+        frames = [f.clone() for f in pipe.frames()]
         fcams = pipe.frame_cameras()
         single = tiler.step()
         if rank == 0:

@@ -222,10 +222,12 @@ rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* camera,
                                 uint32_t world, float* d_rgb, uint64_t* d_counters,
                                 void* stream);
 
-/* Frame batch: n_frames (1..8) frames of one resolution, each with its own camera, in one
- * pipeline pass (the per-level launch and latency floor is paid once per batch; the frame
- * index sits above every queue-key bit, so frames stay contiguous in the sorted queues --
- * an ordering property only; level 0 is frame-uniform per wave).  d_rgb holds n_frames
+/* Frame batch: n_frames (1..16) frames of one resolution, each with its own camera, in one
+ * pipeline pass (the per-level launch and latency floor is paid once per batch).  The ray
+ * queues of a batch are ordered by ray alone -- rays of different frames that start in the
+ * same place and head the same way share waves (an ordering property only: each task
+ * carries its frame; level 0 is frame-uniform per wave); RT_FRAME_KEYS=frame keeps each
+ * frame contiguous instead (the frame index above every key bit).  d_rgb holds n_frames
  * consecutive band buffers of rt_band_rows_per_rank(y_res, band_rows, world) x x_res x 3
  * floats; each equals rt_render_bands_async of that frame's camera bit for bit.  No
  * reference counterpart: a throughput form of render() (src/render.rs:31) over frames. */
@@ -234,7 +236,7 @@ rt_status rt_render_bands_batch_async(const rt_scene* scene, const rt_camera* ca
                                       float* d_rgb, uint64_t* d_counters, void* stream);
 
 /* The general stream-ordered render (every *_async render above is a special case of it):
- * n_frames (1..8) frames of one resolution, each with its own camera, spp jittered samples
+ * n_frames (1..16) frames of one resolution, each with its own camera, spp jittered samples
  * per pixel (spp > 1 needs n_frames == 1), this rank's row bands (as rt_render_bands_async).
  *  - d_rgb:  n_frames band buffers of f32 RGB (may be NULL when spp == 1 and d_rgb8 is set:
  *            then only the bytes are written);

@@ -379,7 +379,7 @@ class DeviceScene:
               "rt_render_bands_ex_async")
 
     def render_bands_batch_async(self, cams, depth, band_rows, rank, world, d_rgb_ptr, d_counters_ptr, stream_ptr):
-        """rt_render_bands_batch_async: len(cams) frames (<= 8, one resolution) in one pipeline
+        """rt_render_bands_batch_async: len(cams) frames (<= 16, one resolution) in one pipeline
         pass into len(cams) consecutive band buffers."""
         arr = (abi.rt_camera * len(cams))(*cams)
         check(self._L.rt_render_bands_batch_async(self.h, arr, len(cams), depth, band_rows, rank, world,

@@ -1786,11 +1786,13 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     // place share waves; "mixfine" (default) -- the same with a frame batch's finer 21-bit
     // task / 4-bit-distance shadow keys; "frame" -- the sample index above the key bits like
     // a frame batch (RT_SPP_KEYS, A/B)
-    // (frame batches: RT_FRAME_KEYS, default "frame")
+    // (frame batches: RT_FRAME_KEYS, default "mixfine" as well)
     const char* sk = std::getenv(spp_batch ? "RT_SPP_KEYS" : "RT_FRAME_KEYS");
     // measured (config 5, 4 passes of 4K x 64 samples in batches of 4): mix 1021, mixfine
-    // 1058, frame 1023 Msamples/s; one pass per sample 788
-    const int key_default = spp_batch ? 1 : 2;
+    // 1058, frame 1023 Msamples/s; one pass per sample 788.  Frame batches (config 3, 4 passes
+    // of 5 frames): frame 944 / 945, mix 1023 / 1018, mixfine 1073 / 1076 Mpixels/s with one
+    // camera for every frame; with a camera per frame (an animation) frame 948, mixfine 1025
+    const int key_default = 1;
     const int spp_keys = !sk ? key_default
                              : (std::strcmp(sk, "mixfine") == 0 ? 1
                                                                 : (std::strcmp(sk, "frame") == 0 ? 2

@@ -185,7 +185,7 @@ enum : uint32_t {
 
 // frame batches (rt_render_bands_batch_async): up to RT_MAX_FRAMES frames of one
 // resolution in one pipeline pass; a task carries its frame in Task.pixel's top bits
-#define RT_MAX_FRAMES 8
+#define RT_MAX_FRAMES 16  // 4 frame bits: Task.pixel bits 28-31
 #define RT_FRAME_SHIFT 28
 struct FrameCam {
     float ox, oy, oz, x_min, y_max, x_delta, y_delta, pad;
