@@ -63,7 +63,7 @@ def parse():
     p.add_argument("--batch", type=int, default=None,
                    help="frames per pipeline pass (rt_render_bands_batch_async, <= 16; default: the timed "
                         "frames spread evenly over the slots, q = ceil(steps / inflight) per slot in equal "
-                        "passes of up to 16 frames (a divisor of q where one is close) within 8 x 1080p of pixels "
+                        "passes of up to 8 frames (a divisor of q where one is close) within 8 x 1080p of pixels "
                         "per pass and rank; 1 for spp > 1, whose samples are batched inside each pass)")
     p.add_argument("--inflight", type=int, default=None,
                    help="frames in flight (F scene handles / HIP streams; default 4 = the box's hardware "
@@ -339,7 +339,7 @@ def main():
     if args.batch is None:
         # The timed K frames are spread evenly over the F slots: q = ceil(K / F) frames per
         # slot, in r = ceil(q / cap) passes of B frames -- a divisor of q when one is near
-        # ceil(q / r), so that every slot runs the same passes.  Up to 16 frames per pass
+        # ceil(q / r), so that every slot runs the same passes.  Up to 8 frames per pass
         # (bounded workspace: <= 8 x 1080p of pixels per pass and rank, ~1.1 KB per pixel).
         # Round 2, ms per share-frame on one MI355X at K = 20 (tools/share_burst.py): N = 1:
         # B = 2 / 4 / 5 / 8: 2.46 / 2.51 / 2.31 / 2.36; N = 8: 0.533 / 0.464 / 0.389 / 0.381
@@ -347,8 +347,10 @@ def main():
         share = band_rows_per_rank(args.height, args.band_rows, world) * args.width
         if args.spp > 1:
             cap = 1
-        else:  # up to 16 frames, within 8 x 1080p of pixels per pass and rank (~18 GB of workspace)
-            cap = max(1, min(16, (8 * 1920 * 1088) // share))
+        else:  # up to 8 frames, within 8 x 1080p of pixels per pass and rank (~18 GB of workspace);
+            # bigger passes lost at K = 20 (4 x 5: 1027 / 1033, 3 x 7: 1018 / 1017, 2 x 10: 750,
+            # 1 x 16: 796 Mpixels/s -- fewer passes in flight)
+            cap = max(1, min(8, (8 * 1920 * 1088) // share))
         q = -(-args.steps // inflight)
         r = -(-q // cap)
         b = -(-q // r)
