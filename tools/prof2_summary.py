@@ -1,4 +1,4 @@
-"""Summarise a tools/prof2.sh run: per-kernel ms per frame (frames in flight and one at a
+"""Summarise a tools/prof2.sh / tools/prof3.sh run: per-kernel ms per frame (frames in flight and one at a
 time), per-kernel HBM bytes per frame (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md's
 gfx950 correction) and SQ wave-cycle shares.  Copies the evidence to profiles/TAG/.
 
@@ -84,55 +84,75 @@ def main():
             st = one(os.path.join(src, name, "**", "*kernel_stats.csv"))
             if st:
                 shutil.copy(st, os.path.join(dst, f"kernel_stats_{name}.csv"))
-    pmc_frames = 4 + 1  # steps + the slot's set-up frame (inflight 1, warmup 0)
-    fe, f_fe = pmc_table(os.path.join(src, "pmc_fetch"), "FETCH_SIZE")
-    wr, f_wr = pmc_table(os.path.join(src, "pmc_write"), "WRITE_SIZE")
-    out += ["", "## HBM bytes per frame (MB; FETCH_SIZE x 2 + WRITE_SIZE, KB counters)", "",
-            "| kernel | fetch x2 | write | total |", "|---|---|---|---|"]
-    tf = tw = 0.0
-    for k in sorted(set(fe) | set(wr), key=lambda k: -(2 * fe.get(k, 0) + wr.get(k, 0))):
-        a, b = 2 * fe.get(k, 0) / 1024 / pmc_frames, wr.get(k, 0) / 1024 / pmc_frames
-        tf += a
-        tw += b
-        out.append(f"| {k} | {a:.1f} | {b:.1f} | {a + b:.1f} |")
-    out.append(f"| **all** | {tf:.1f} | {tw:.1f} | {tf + tw:.1f} |")
-    for f, n in ((f_fe, "pmc_fetch.csv"), (f_wr, "pmc_write.csv")):
-        if f:
-            shutil.copy(f, os.path.join(dst, n))
-    sq = {}
-    f_sq = one(os.path.join(src, "pmc_sq", "**", "*counter_collection.csv"))
-    if f_sq:
-        shutil.copy(f_sq, os.path.join(dst, "pmc_sq.csv"))
-        tot = defaultdict(float)
-        for r in csv.DictReader(open(f_sq)):
-            tot[r["Counter_Name"]] += float(r["Counter_Value"])
-        sq = {k: v / pmc_frames for k, v in tot.items()}
-        wc = sq.get("SQ_WAVE_CYCLES", 0) or 1
-        out += ["", "## SQ (per frame, all render kernels)", "", "| counter | value |", "|---|---|"]
-        for k, v in sorted(sq.items()):
-            out.append(f"| {k} | {v:.4g} |")
-        out.append("")
-        out.append(f"Wave-cycle shares: VALU active {sq.get('SQ_ACTIVE_INST_VALU', 0) / wc:.3f}, "
-                   f"waiting (s_waitcnt) {sq.get('SQ_WAIT_ANY', 0) / wc:.3f}, "
-                   f"issue-stalled {sq.get('SQ_WAIT_INST_ANY', 0) / wc:.3f}.")
-    traffic = (tf + tw) * 1024 * 1024
     import subprocess
     commit = os.environ.get("PROFILE_COMMIT") or subprocess.run(
         ["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True).stdout.strip()
-    wc = sq.get("SQ_WAVE_CYCLES", 0) or 1
-    json.dump({"workload": bench["config"]["workload"], "bytes_per_launch": traffic,
-               "commit": commit, "profile": f"profiles/{tag}",
-               "sq_insts_valu_per_frame": sq.get("SQ_INSTS_VALU"),
-               "wave_cycle_shares": {"valu_active": round(sq.get("SQ_ACTIVE_INST_VALU", 0) / wc, 4),
-                                     "waiting_s_waitcnt": round(sq.get("SQ_WAIT_ANY", 0) / wc, 4),
-                                     "issue_stalled": round(sq.get("SQ_WAIT_INST_ANY", 0) / wc, 4)} if sq else None,
-               "sq_source": f"profiles/{tag}/pmc_sq.csv (one frame at a time, per frame)",
-               "launch": "one frame of the render pipeline (every kernel of the frame)",
-               "fetch_size_bytes_x2": tf * 1024 * 1024, "write_size_bytes": tw * 1024 * 1024,
-               "correction": "FETCH_SIZE x 2 per MI355X_MICROARCH.md (gfx950 tallies 128-B requests at 64 B); "
-                             "WRITE_SIZE as reported",
-               "source": f"profiles/{tag}/pmc_fetch.csv, pmc_write.csv"},
-              open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+    # PMC passes: (suffix, frames per pass, frames rendered in the run: the slot's set-up pass + steps)
+    runs = [("_b1", 1, 5), ("_b5", 5, 10)] if os.path.isdir(os.path.join(src, "pmc_fetch_b1")) else [("", 1, 5)]
+    result = {}
+    for suf, per_pass, pmc_frames in runs:
+        fe, f_fe = pmc_table(os.path.join(src, "pmc_fetch" + suf), "FETCH_SIZE")
+        wr, f_wr = pmc_table(os.path.join(src, "pmc_write" + suf), "WRITE_SIZE")
+        label = f"{per_pass} frame{'s' if per_pass > 1 else ''} per pass"
+        out += ["", f"## HBM bytes per frame, {label} (MB; FETCH_SIZE x 2 + WRITE_SIZE, KB counters)", "",
+                "| kernel | fetch x2 | write | total |", "|---|---|---|---|"]
+        tf = tw = 0.0
+        for k in sorted(set(fe) | set(wr), key=lambda k: -(2 * fe.get(k, 0) + wr.get(k, 0))):
+            a, b = 2 * fe.get(k, 0) / 1024 / pmc_frames, wr.get(k, 0) / 1024 / pmc_frames
+            tf += a
+            tw += b
+            out.append(f"| {k} | {a:.1f} | {b:.1f} | {a + b:.1f} |")
+        out.append(f"| **all** | {tf:.1f} | {tw:.1f} | {tf + tw:.1f} |")
+        for f, n in ((f_fe, f"pmc_fetch{suf}.csv"), (f_wr, f"pmc_write{suf}.csv")):
+            if f:
+                shutil.copy(f, os.path.join(dst, n))
+        sq = {}
+        per_kernel = []
+        f_sq = one(os.path.join(src, "pmc_sq" + suf, "**", "*counter_collection.csv"))
+        if f_sq:
+            shutil.copy(f_sq, os.path.join(dst, f"pmc_sq{suf}.csv"))
+            tot = defaultdict(float)
+            byk = defaultdict(lambda: defaultdict(float))
+            for r in csv.DictReader(open(f_sq)):
+                tot[r["Counter_Name"]] += float(r["Counter_Value"])
+                byk[fam(r["Kernel_Name"])][r["Counter_Name"]] += float(r["Counter_Value"])
+            sq = {k: v / pmc_frames for k, v in tot.items()}
+            wc = sq.get("SQ_WAVE_CYCLES", 0) or 1
+            out += ["", f"## SQ per frame, {label} (all render kernels)", "", "| counter | value |", "|---|---|"]
+            for k, v in sorted(sq.items()):
+                out.append(f"| {k} | {v:.4g} |")
+            out.append("")
+            out.append(f"Wave-cycle shares: VALU active {sq.get('SQ_ACTIVE_INST_VALU', 0) / wc:.3f}, "
+                       f"waiting (s_waitcnt) {sq.get('SQ_WAIT_ANY', 0) / wc:.3f}, "
+                       f"issue-stalled {sq.get('SQ_WAIT_INST_ANY', 0) / wc:.3f}.")
+            out += ["", "| kernel | wave-cycles share | VALU active | s_waitcnt | issue-stalled |", "|---|---|---|---|---|"]
+            for k, v in sorted(byk.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
+                w = v.get("SQ_WAVE_CYCLES", 0)
+                if w < 0.01 * tot.get("SQ_WAVE_CYCLES", 1):
+                    continue
+                out.append(f"| {k} | {w / tot['SQ_WAVE_CYCLES']:.3f} | {v.get('SQ_ACTIVE_INST_VALU', 0) / w:.3f} | "
+                           f"{v.get('SQ_WAIT_ANY', 0) / w:.3f} | {v.get('SQ_WAIT_INST_ANY', 0) / w:.3f} |")
+        traffic = (tf + tw) * 1024 * 1024
+        wc = sq.get("SQ_WAVE_CYCLES", 0) or 1
+        result[per_pass] = {"bytes_per_launch": traffic, "fetch_size_bytes_x2": tf * 1024 * 1024,
+                            "write_size_bytes": tw * 1024 * 1024,
+                            "sq_insts_valu_per_frame": sq.get("SQ_INSTS_VALU"),
+                            "wave_cycle_shares": {"valu_active": round(sq.get("SQ_ACTIVE_INST_VALU", 0) / wc, 4),
+                                                  "waiting_s_waitcnt": round(sq.get("SQ_WAIT_ANY", 0) / wc, 4),
+                                                  "issue_stalled": round(sq.get("SQ_WAIT_INST_ANY", 0) / wc, 4)}
+                            if sq else None,
+                            "source": f"profiles/{tag}/pmc_fetch{suf}.csv, pmc_write{suf}.csv, pmc_sq{suf}.csv"}
+    # the headline's pass size when measured, else one frame per pass
+    head = result.get(5) or result[1]
+    doc = {"workload": bench["config"]["workload"], "commit": commit, "profile": f"profiles/{tag}",
+           "launch": "one frame of the render pipeline (every kernel of the frame), per frame of a "
+                     f"{5 if 5 in result else 1}-frame pass",
+           "correction": "FETCH_SIZE x 2 per MI355X_MICROARCH.md (gfx950 tallies 128-B requests at 64 B); "
+                         "WRITE_SIZE as reported",
+           "sq_source": head["source"]}
+    doc.update(head)
+    doc["per_pass_size"] = {str(k): v for k, v in result.items()}
+    json.dump(doc, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
     open(os.path.join(dst, "summary.md"), "w").write("\n".join(out) + "\n")
     print("\n".join(out))
 
