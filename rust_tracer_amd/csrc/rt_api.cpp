@@ -1979,6 +1979,20 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
             p.shadow_fine = 19u;
             shadow_bits += 1u;
         }
+        // RT_KEY24=1 (A/B): without frame bits a batch's 3 radix passes hold 24 key bits --
+        // 18-bit Morton task keys and a 7-bit shadow distance
+        const char* k24 = std::getenv("RT_KEY24");
+        if (k24 && k24[0] == '1' && fbits == 0) {
+            if (p.task_fine == 1u) {
+                p.task_fine = 2u;
+                task_bits = 24u;
+            }
+            if (p.shadow_cell == 3u && 6ull * s->S.lb_res * s->S.lb_res * 128u < (1u << 21) && lbits + 22u <= 24u) {
+                p.shadow_cell = 4u;
+                p.shadow_fine = 22u;
+                shadow_bits = 22u + lbits;
+            }
+        }
         p.task_frame_shift = task_bits;
         p.shadow_frame_shift = shadow_bits;
         task_bits += fbits;

@@ -132,6 +132,7 @@ __device__ __forceinline__ uint32_t inside_key(const WaveParams& P, uint32_t cen
         else { face = 4u + (d.z < 0.f); u = d.x; v = d.y; }
         low = (face << 2) | ((u > 0.f ? 1u : 0u) << 1) | (v > 0.f ? 1u : 0u);
     }
+    if (P.task_fine == 2u) return (1u << 23) | (center_key << 8) | (low << 3);  // 24-bit keys
     return P.task_fine ? (1u << 20) | (center_key << 5) | low : (1u << 15) | center_key;
 }
 __device__ __forceinline__ uint32_t task_key(const WaveParams& P, V3 o, V3 d) {
@@ -149,6 +150,7 @@ __device__ __forceinline__ uint32_t task_key(const WaveParams& P, V3 o, V3 d) {
         uint32_t cu = u > 0.f ? 1u : 0u, cv = v > 0.f ? 1u : 0u;
         uint32_t dir = (face << 2) | (cu << 1) | cv;
         if (P.key_mode == 7) {  // 15 bits (20 when task_fine): the bit above marks inside rays
+            if (P.task_fine == 2u) return (dir << 18) | morton18(P.S, q);  // 24-bit keys (23 used outside)
             if (P.task_fine) return (dir << 15) | morton15(P.S, q);
             return (dir << 10) | (morton15(P.S, q) >> 5);
         }
@@ -667,10 +669,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                                 const bool lb = L.lb_base != 0xFFFFFFFFu && D <= S.lb_dmax &&
                                                 len2(raw) <= RT_LB_LMAX * RT_LB_LMAX;
                                 if (!lb) {
-                                    low = (1u << (P.shadow_fine - 1u)) | (mort >> (19u - P.shadow_fine));
+                                    low = (1u << (P.shadow_fine - 1u)) |
+                                          (P.shadow_fine >= 19u ? mort << (P.shadow_fine - 19u) : mort >> (19u - P.shadow_fine));
                                 } else if (P.shadow_cell == 2u) {  // cell | 3-bit distance from the light
                                     const float dl = sqrtf(len2(raw)) * (8.f / RT_LB_LMAX);
                                     low = (lb_cell(S.lb_res, neg(norm(raw))) << 3) | (uint32_t)fminf(dl, 7.f);
+                                } else if (P.shadow_cell == 4u) {  // cell | 7-bit distance (24-bit keys)
+                                    const float dl = sqrtf(len2(raw)) * (128.f / RT_LB_LMAX);
+                                    low = (lb_cell(S.lb_res, neg(norm(raw))) << 7) | (uint32_t)fminf(dl, 127.f);
                                 } else if (P.shadow_cell == 3u) {  // cell | 4-bit distance (frame batches)
                                     const float dl = sqrtf(len2(raw)) * (16.f / RT_LB_LMAX);
                                     low = (lb_cell(S.lb_res, neg(norm(raw))) << 4) | (uint32_t)fminf(dl, 15.f);

@@ -49,6 +49,7 @@ def main():
     out["one_pass_ms"] = round(e0.elapsed_time(e1) / 10, 4)
     ref = band[:h].cpu().numpy()
     out["rt_render_pageable_ms"] = best(lambda: s.render(w, h, depth))
+    out["rt_render_device_ms"] = round(min(s.render(w, h, depth)[2] for _ in range(5)), 4)
     hf = HostFrame(w, h)
     out["rt_render_pinned_ms"] = best(lambda: s.render(w, h, depth, out=hf.array))
     img = s.render(w, h, depth, out=hf.array)[0]
