@@ -1979,10 +1979,11 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
             p.shadow_fine = 19u;
             shadow_bits += 1u;
         }
-        // RT_KEY24=1 (A/B): without frame bits a batch's 3 radix passes hold 24 key bits --
-        // 18-bit Morton task keys and a 7-bit shadow distance
+        // without frame bits a batch's 3 radix passes hold 24 key bits: 18-bit Morton task keys
+        // and a 7-bit shadow distance (1035 / 1039 vs 1027 / 1031 Mpixels/s with the 21-bit
+        // keys; RT_KEY24=0: off, A/B)
         const char* k24 = std::getenv("RT_KEY24");
-        if (k24 && k24[0] == '1' && fbits == 0) {
+        if (!(k24 && k24[0] == '0') && fbits == 0) {
             if (p.task_fine == 1u) {
                 p.task_fine = 2u;
                 task_bits = 24u;
@@ -2326,8 +2327,9 @@ rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t de
     // One frame as S band shares of this device, rendered side by side on S streams (each
     // its own scene clone and workspace), exchanged by device copies and un-permuted: the
     // latency-bound tails of one share's levels overlap the other's work.  RT_SEAM_SPLIT
-    // (default 2; 1 = one pass), RT_SEAM_BAND_ROWS (default 8).  Config 3, 1080p, one MI355X:
-    // 3.76 ms of device time against 4.11 for one pass (4 shares: 5.08).
+    // (default 2; 1 = one pass), RT_SEAM_BAND_ROWS (default: contiguous shares).  Config 3,
+    // 1080p, one MI355X: 3.47 ms of device time against 4.09 for one pass (8-row bands: 3.69;
+    // 3 shares: 3.80, 4: 5.08).
     const int split = seam_split();
     if (split > 1 && !use_megakernel() && cam->y_res >= 16u * (uint32_t)split) {
         if (s->split_n != split) {
@@ -2338,9 +2340,13 @@ rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t de
             rt_status st = rt_multi_build(s, devs.data(), (uint32_t)split, false, &s->split);
             if (st != RT_OK) return st;
             s->split_n = split;
-            const char* br = std::getenv("RT_SEAM_BAND_ROWS");
-            rt_multi_set_band_rows(s->split, br ? (uint32_t)std::atoi(br) : 8u);
         }
+        // contiguous shares by default (top / bottom halves: 3.47 ms against 3.69 with 8-row
+        // bands dealt in turn -- shares of different content fall out of step, so one share's
+        // level tails meet the other's work)
+        const char* br = std::getenv("RT_SEAM_BAND_ROWS");
+        const uint32_t rows = ((cam->y_res + (uint32_t)split - 1u) / (uint32_t)split + 7u) / 8u * 8u;
+        rt_multi_set_band_rows(s->split, br ? (uint32_t)std::max(1, std::atoi(br)) : rows);
         return rt_multi_render_state(s->split, cam, depth, spp, seed, opts, rgb, rgb8);
     }
     HIP_TRY(hipSetDevice(s->device));

@@ -447,3 +447,36 @@ def test_torchrun_two_ranks_rgb8_gather():
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["frame_check"] is True and out["config"]["output"] == "rgb8"
+
+
+@pytest.mark.parametrize("split,rows", [(2, None), (3, None), (2, "8"), (4, "16")])
+def test_seam_split_changes_nothing(monkeypatch, split, rows):
+    """rt_render on a one-device scene renders the frame as `split` band shares side by side
+    (RT_SEAM_SPLIT, contiguous shares by default, RT_SEAM_BAND_ROWS otherwise): frames, RGB8
+    and counters equal the single pass (RT_SEAM_SPLIT=1) bit for bit, including a frame too
+    small to split and a ragged height; the share handles follow a material edit."""
+    desc = SceneDesc.synth_config(3)
+    sizes = [(320, 181), (96, 20)]
+    monkeypatch.setenv("RT_SEAM_SPLIT", "1")
+    s = DeviceScene(desc, device=0)
+    refs = [s.render(w, h, 8, want_u8=True) for w, h in sizes]
+    s.close()
+    monkeypatch.setenv("RT_SEAM_SPLIT", str(split))
+    if rows:
+        monkeypatch.setenv("RT_SEAM_BAND_ROWS", rows)
+    s = DeviceScene(desc, device=0)
+    for (w, h), (ref, rcnt, _, ref8) in zip(sizes, refs):
+        img, cnt, ms, img8 = s.render(w, h, 8, want_u8=True)
+        assert same_bits(img, ref) and np.array_equal(img8, ref8) and cnt == rcnt, (w, h)
+    # a material edit reaches every share's handle
+    from rust_tracer_amd import phong_material
+    m = phong_material((0, 0, 0), (0.9, 0.2, 0.1), (1, 1, 1), 30.0, 0.5, 0.0)
+    s.set_material(0, m)
+    img, cnt, _, _ = s.render(320, 181, 8)
+    s.close()
+    monkeypatch.setenv("RT_SEAM_SPLIT", "1")
+    one = DeviceScene(desc, device=0)
+    one.set_material(0, m)
+    ref, rcnt, _, _ = one.render(320, 181, 8)
+    one.close()
+    assert same_bits(img, ref) and cnt == rcnt
