@@ -393,15 +393,16 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    # one instrumented frame (untimed) counts the scans' tests; frames are deterministic,
-    # so every timed frame runs exactly these tests, uncounted
+    # one instrumented pass (untimed) counts the scans' tests: the timed passes' size and
+    # cameras (a batch's waves mix its frames' rays, so the tests a wave runs depend on the
+    # pass), per frame; frames are deterministic, so the timed passes run these tests, uncounted
     ops = None
     if args.count_frame:
         scene.set_scan_counting(True)
         scene.scan_ops(reset=True)
-        tiler.step()
+        tiler.render_local(batch, [anim_cam(i) for i in range(batch)] if args.animate else None)
         torch.cuda.synchronize()
-        ops = scene.scan_ops()
+        ops = {k: v / batch for k, v in scene.scan_ops().items()}
         scene.set_scan_counting(False)
     pipe.zero_counters()
 
@@ -496,8 +497,8 @@ def main():
             "kernel_ms_is": (f"timed-region HIP events / steps ({inflight} passes of {batch} frames in flight)"
                              if inflight * batch > 1 else "timed-region HIP events / steps"),
             "flops_per_launch": per_launch_flops,
-            "tests_per_launch": {k: v for k, v in ops.items() if not k.startswith("cycles")} if ops else None,
-            "cycles_per_launch": {k: v for k, v in ops.items() if k.startswith("cycles")} if ops else None,
+            "tests_per_launch": {k: round(v) for k, v in ops.items() if not k.startswith("cycles")} if ops else None,
+            "cycles_per_launch": {k: round(v) for k, v in ops.items() if k.startswith("cycles")} if ops else None,
             "culling": {"hierarchy": scene.uses_bvh,
                         "linear_scan_flops_per_launch": brute_flops,
                         "linear_scan_equivalent_TFLOPs": round(brute_flops / (kernel_ms / 1e3) / 1e12, 3)},

@@ -31,7 +31,12 @@ def main():
         rpr = band_rows_per_rank(h, 8, world)
         for b in batches:
             bufs = [torch.zeros((b, rpr, w, 3), dtype=torch.float32, device="cuda") for _ in scenes]
-            cams = [cam] * b
+            # an animation, as bench.py's default: frame i's camera origin x = 0.01 (i mod 64)
+            cams = []
+            for i in range(b):
+                c = abi.camera(w, h)
+                c.origin[0] = 0.01 * i
+                cams.append(c)
 
             def burst(k):
                 p = 0
