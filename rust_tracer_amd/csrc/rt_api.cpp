@@ -1798,6 +1798,10 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
                                                                 : (std::strcmp(sk, "frame") == 0 ? 2
                                                                                                  : (std::strcmp(sk, "mix") == 0 ? 0 : key_default)));
     p.frame_keys = spp_keys == 2 ? 1u : 0u;
+    {
+        const char* e = std::getenv("RT_L0_INTERLEAVE");  // A/B
+        p.l0_interleave = (e && e[0] == '1') ? 1u : 0u;
+    }
     p.sample = sample;
     p.seed = seed;
     p.S = s->S;
@@ -1985,7 +1989,8 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         const char* k24 = std::getenv("RT_KEY24");
         if (!(k24 && k24[0] == '0') && fbits == 0) {
             if (p.task_fine == 1u) {
-                p.task_fine = 2u;
+                const char* kd = std::getenv("RT_KEY24_DIR");  // "16": 4x4 direction cells | 16-bit Morton (A/B)
+                p.task_fine = (kd && std::strcmp(kd, "16") == 0) ? 3u : 2u;
                 task_bits = 24u;
             }
             if (p.shadow_cell == 3u && 6ull * s->S.lb_res * s->S.lb_res * 128u < (1u << 21) && lbits + 22u <= 24u) {

@@ -50,6 +50,24 @@ __device__ __forceinline__ PixelRef pixel_of(const WaveParams& P, uint32_t item)
     return r;
 }
 
+// level-0 item t of a frame batch -> (frame, item within the frame).  Frame-major by
+// default; P.l0_interleave: 64-item tiles dealt to the frames in turn (tile k of every frame
+// side by side), so that concurrent level-0 waves of a batch trace the same place
+__device__ __forceinline__ uint32_t item_frame(const WaveParams& P, uint32_t t, uint32_t& local) {
+    if (P.frames <= 1) {
+        local = t;
+        return 0u;
+    }
+    if (P.l0_interleave) {
+        const uint32_t tile = t >> 6, fr = tile % P.frames;
+        local = ((tile / P.frames) << 6) | (t & 63u);
+        return fr;
+    }
+    const uint32_t fr = t / P.frame_items;
+    local = t - fr * P.frame_items;
+    return fr;
+}
+
 // rt_render_spp's counter hash (include/rt_api.h): jitter in [0, 1) of sample k of a
 // pixel along dimension dim (0: x, 1: y); 24-bit fractions, exact in f32
 __device__ __forceinline__ uint32_t spp_mix32(uint32_t x) {
@@ -122,7 +140,19 @@ __device__ __forceinline__ uint32_t morton21(const DevScene& S, V3 p) {
 #ifndef RT_INSIDE_DIR
 #define RT_INSIDE_DIR 1
 #endif
+// cube-map face of d x 4x4 cells of the face (< 96: 7 bits)
+__device__ __forceinline__ uint32_t dir_cell16(V3 d) {
+    float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z), u, v, m;
+    uint32_t face;
+    if (ax >= ay && ax >= az) { face = d.x < 0.f; u = d.y; v = d.z; m = ax; }
+    else if (ay >= az) { face = 2u + (d.y < 0.f); u = d.x; v = d.z; m = ay; }
+    else { face = 4u + (d.z < 0.f); u = d.x; v = d.y; m = az; }
+    const uint32_t qu = (uint32_t)fminf(fmaxf((u / m + 1.f) * 2.f, 0.f), 3.f);
+    const uint32_t qv = (uint32_t)fminf(fmaxf((v / m + 1.f) * 2.f, 0.f), 3.f);
+    return (face << 4) | (qu << 2) | qv;
+}
 __device__ __forceinline__ uint32_t inside_key(const WaveParams& P, uint32_t center_key, V3 d) {
+    if (P.task_fine == 3u) return (1u << 23) | (center_key << 8) | (dir_cell16(d) << 1);  // 24-bit, 4x4 cells
     uint32_t low = 0;
     if (RT_INSIDE_DIR && P.task_fine) {
         float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z), u, v;
@@ -151,6 +181,7 @@ __device__ __forceinline__ uint32_t task_key(const WaveParams& P, V3 o, V3 d) {
         uint32_t dir = (face << 2) | (cu << 1) | cv;
         if (P.key_mode == 7) {  // 15 bits (20 when task_fine): the bit above marks inside rays
             if (P.task_fine == 2u) return (dir << 18) | morton18(P.S, q);  // 24-bit keys (23 used outside)
+            if (P.task_fine == 3u) return (dir_cell16(d) << 16) | (morton18(P.S, q) >> 2);  // 4x4 cells | 16-bit Morton
             if (P.task_fine) return (dir << 15) | morton15(P.S, q);
             return (dir << 10) | (morton15(P.S, q) >> 5);
         }
@@ -408,8 +439,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         const uint32_t n = off + ((rev && active) ? count - 1u - t : t);
         if (active) {
             if (FIRST || (!DEEP && level == 0)) {
-                const uint32_t fr = P.frames > 1 ? t / P.frame_items : 0u;
-                PixelRef px = pixel_of(P, t - fr * P.frame_items);
+                uint32_t local;
+                const uint32_t fr = item_frame(P, t, local);
+                PixelRef px = pixel_of(P, local);
                 if (!px.valid) {
                     P.node_flags[n] = NODE_NONE;
                     active = false;
@@ -889,9 +921,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_COMBINE_
         const uint32_t litmask = P.node_lit[n];
         const float4 er = P.node_ec[2u * n], et = P.node_ec[2u * n + 1u];
         // frame batches: level-0 node t belongs to frame t / frame_items
-        const uint32_t fr = (level == 0 && P.frames > 1) ? t / P.frame_items : 0u;
+        uint32_t local = t;
+        const uint32_t fr = level == 0 ? item_frame(P, t, local) : 0u;
         if (flags & NODE_NONE) {  // padding of the band buffer: defined as 0
-            PixelRef px = pixel_of(P, t - fr * P.frame_items);
+            PixelRef px = pixel_of(P, local);
             if (level == 0 && px.u < P.width && px.lr < P.rows_local) {
                 const size_t i = (size_t)px.lr * P.width + px.u;
                 if (P.out) {
@@ -932,7 +965,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_COMBINE_
             continue;  // a missed child: the trace pass wrote BLACK to its parent's slot
         }
         if (level == 0) {
-            PixelRef px = pixel_of(P, t - fr * P.frame_items);
+            PixelRef px = pixel_of(P, local);
             const size_t i = (size_t)px.lr * P.width + px.u;
             bool last = true;
             if (P.out) {  // (null: an RGB8-only pass, spp == 1)
