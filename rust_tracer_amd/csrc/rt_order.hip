@@ -95,11 +95,17 @@ __global__ __launch_bounds__(SORT_THREADS) void sort_count_kernel(SortRef r, con
     const uint32_t t = threadIdx.x;
     for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
         for (uint32_t j = 0; j < DPT; j++) h[t * DPT + j] = 0u;
+        // every key of the tile requested before the first is counted (in-bounds clamped
+        // addresses, no per-item branch): one memory round trip per tile, not SORT_ITEMS
+        uint32_t kk[SORT_ITEMS];
+#pragma unroll
+        for (uint32_t i = 0; i < SORT_ITEMS; i++) kk[i] = kin[min(tile * SORT_TILE + i * SORT_THREADS + t, n - 1u)];
         __syncthreads();
+#pragma unroll
         for (uint32_t i = 0; i < SORT_ITEMS; i++) {
             const uint32_t idx = tile * SORT_TILE + i * SORT_THREADS + t;
             const bool valid = idx < n;
-            lds_digit_add(h, valid ? (kin[idx] >> shift) & dmask : 0u, valid);
+            lds_digit_add(h, valid ? (kk[i] >> shift) & dmask : 0u, valid);
         }
         __syncthreads();
         for (uint32_t j = 0; j < DPT; j++) tile_counts[(size_t)(t * DPT + j) * max_tiles + tile] = h[t * DPT + j];
@@ -160,13 +166,30 @@ __global__ __launch_bounds__(SORT_THREADS) void sort_scatter_kernel(SortRef r, c
         uint32_t k[SORT_ITEMS], v[SORT_ITEMS], rank[SORT_ITEMS];
         // warp-striped: item i of lane l in wave w is entry w * 1024 + i * 64 + l of the tile
         const uint32_t first = tile * SORT_TILE + (t >> 6) * (64u * SORT_ITEMS) + (t & 63u);
+        // every key and value requested at once (clamped in-bounds addresses, no per-item
+        // branch between the loads); padding is patched in afterwards: it ranks after every
+        // real entry of its digit (it is last in the tile) and is never written
+        if (vals) {
+#pragma unroll
+            for (uint32_t i = 0; i < SORT_ITEMS; i++) {
+                const uint32_t idc = min(first + i * 64u, n - 1u);
+                k[i] = keys[in_off + idc];
+                v[i] = vals[in_off + idc];
+            }
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < SORT_ITEMS; i++) {
+                const uint32_t idc = min(first + i * 64u, n - 1u);
+                k[i] = keys[in_off + idc];
+                v[i] = off + idc;
+            }
+        }
+#pragma unroll
         for (uint32_t i = 0; i < SORT_ITEMS; i++) {
-            const uint32_t idx = first + i * 64u;
-            const bool valid = idx < n;
-            // padding ranks after every real entry of its digit (it is last in the tile) and is
-            // never written
-            k[i] = valid ? keys[in_off + idx] : 0xFFFFFFFFu;
-            v[i] = valid ? (vals ? vals[in_off + idx] : off + idx) : 0u;
+            if (first + i * 64u >= n) {
+                k[i] = 0xFFFFFFFFu;
+                v[i] = 0u;
+            }
         }
         unsigned int pre[DPT], cnt[DPT];
         SortRank().rank_keys(k, rank, rank_storage, [shift, dmask](const uint32_t& key) { return (key >> shift) & dmask; },
