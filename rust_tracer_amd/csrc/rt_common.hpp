@@ -181,17 +181,58 @@ struct Hit {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return make_float4(p[0], p[1], p[2], p[3]); }
 
+// Shape and material records read whole, every 16-B piece requested at once: read field by
+// field through a reference, the per-kind branches split the loads into dependent round
+// trips (several L2 latencies per hit).
+struct ShapeW {
+    float4 w[8];  // {kind, mat, centre key, pad1} {inv row 0} {inv row 1} {inv row 2} {a[0..15]}
+    __device__ __forceinline__ int32_t kind() const { return __float_as_int(w[0].x); }
+    __device__ __forceinline__ int32_t mat() const { return __float_as_int(w[0].y); }
+    __device__ __forceinline__ float a(int i) const {
+        const float4 q = w[4 + (i >> 2)];
+        const int c = i & 3;
+        return c == 0 ? q.x : (c == 1 ? q.y : (c == 2 ? q.z : q.w));
+    }
+};
+__device__ __forceinline__ ShapeW load_shape(const ShapeRec* shapes, uint32_t i) {
+    static_assert(sizeof(ShapeRec) == 128, "ShapeRec is eight float4");
+    const float4* p = reinterpret_cast<const float4*>(shapes + i);
+    ShapeW r;
+#pragma unroll
+    for (int k = 0; k < 8; k++) r.w[k] = p[k];
+    return r;
+}
+__device__ __forceinline__ MatRec load_mat(const MatRec* mats, uint32_t i) {
+    static_assert(sizeof(MatRec) == 80, "MatRec is five float4");
+    const float4* p = reinterpret_cast<const float4*>(mats + i);
+    const float4 a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
+    MatRec M;
+    M.kind = __float_as_int(a.x);
+    M.dark_zero = __float_as_int(a.y);
+    M.power = a.z;
+    M.reflectivity = a.w;
+    M.refraction_index = b.x;
+    M.pad1 = b.y;
+    M.pad2 = b.z;
+    M.pad3 = b.w;
+    M.ambient = TexRec{__float_as_int(c.x), c.y, c.z, c.w};
+    M.diffuse = TexRec{__float_as_int(d.x), d.y, d.z, d.w};
+    M.specular = TexRec{__float_as_int(e.x), e.y, e.z, e.w};
+    return M;
+}
+
 // Recompute the full Intersection of the chosen shape with the reference formulas
 // (sphere.rs:57-98, plane.rs:59-84, triangle.rs:51-94, cube.rs:89-102).
-__device__ __forceinline__ Hit hit_attrs(const DevScene& S, uint32_t key, V3 o, V3 d, bool need_sphere_tex) {
+__device__ __forceinline__ Hit hit_attrs_w(const DevScene& S, const ShapeW& R, uint32_t key, V3 o, V3 d,
+                                           bool need_sphere_tex) {
     Hit h;
-    const ShapeRec& R = S.shapes[key >> 4];
-    h.mat = R.mat;
-    float4 r0 = ld4(R.inv), r1 = ld4(R.inv + 4), r2 = ld4(R.inv + 8);
+    h.mat = R.mat();
+    const float4 r0 = R.w[1], r1 = R.w[2], r2 = R.w[3];
     h.eye = neg(norm(d));
     h.tu = 0.f;
     h.tv = 0.f;
-    if (R.kind == RT_SHAPE_SPHERE) {
+    const int32_t kind = R.kind();
+    if (kind == RT_SHAPE_SPHERE) {
         V3 to = pt_mul(r0, r1, r2, o);
         V3 td = vec3_mul(r0, r1, r2, d);
         float t = 0.f;
@@ -209,26 +250,26 @@ __device__ __forceinline__ Hit hit_attrs(const DevScene& S, uint32_t key, V3 o, 
             h.tu = (1.f + atan2f(n.z, n.x) / PI_F) * 0.5f;
             h.tv = acosf(n.y) / PI_F;
         }
-    } else if (R.kind == RT_SHAPE_PLANE) {
+    } else if (kind == RT_SHAPE_PLANE) {
         V3 to = pt_mul(r0, r1, r2, o);
         V3 td = vec3_mul(r0, r1, r2, d);
-        V3 pn = v3(R.a[0], R.a[1], R.a[2]);
-        V3 po = v3(R.a[3], R.a[4], R.a[5]);
+        V3 pn = v3(R.a(0), R.a(1), R.a(2));
+        V3 po = v3(R.a(3), R.a(4), R.a(5));
         float t = 0.f;
         plane_t(to, td, pn, po, t);
         h.t = t;
         h.entering = t >= 0.f;
         h.p = add(o, mul(d, t));
-        h.n = v3(R.a[6], R.a[7], R.a[8]);  // transform * normal, evaluated on the host
-        h.tu = dot(v3(R.a[9], R.a[10], R.a[11]), h.p);
-        h.tv = dot(v3(R.a[12], R.a[13], R.a[14]), h.p);
-    } else if (R.kind == RT_SHAPE_TRIANGLE) {
+        h.n = v3(R.a(6), R.a(7), R.a(8));  // transform * normal, evaluated on the host
+        h.tu = dot(v3(R.a(9), R.a(10), R.a(11)), h.p);
+        h.tv = dot(v3(R.a(12), R.a(13), R.a(14)), h.p);
+    } else if (kind == RT_SHAPE_TRIANGLE) {
         float t = 0.f, u = 0.f, v = 0.f, det = 0.f;
-        tri_hit(o, d, v3(R.a[0], R.a[1], R.a[2]), v3(R.a[3], R.a[4], R.a[5]), v3(R.a[6], R.a[7], R.a[8]),
+        tri_hit(o, d, v3(R.a(0), R.a(1), R.a(2)), v3(R.a(3), R.a(4), R.a(5)), v3(R.a(6), R.a(7), R.a(8)),
                 t, u, v, det);
         h.t = t;
         h.p = add(o, mul(d, t));
-        h.n = v3(R.a[9], R.a[10], R.a[11]);
+        h.n = v3(R.a(9), R.a(10), R.a(11));
         h.entering = det > 0.f;
         h.tu = u;
         h.tv = v;
@@ -246,6 +287,9 @@ __device__ __forceinline__ Hit hit_attrs(const DevScene& S, uint32_t key, V3 o, 
         h.tv = v;
     }
     return h;
+}
+__device__ __forceinline__ Hit hit_attrs(const DevScene& S, uint32_t key, V3 o, V3 d, bool need_sphere_tex) {
+    return hit_attrs_w(S, load_shape(S.shapes, key >> 4), key, o, d, need_sphere_tex);
 }
 
 // Saturating f32 -> i32 cast (Rust `as i32`: NaN -> 0)

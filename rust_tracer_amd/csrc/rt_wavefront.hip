@@ -28,6 +28,14 @@
 
 #include "rt_common.hpp"
 
+#ifndef RT_HIT_BULK
+#define RT_HIT_BULK 1  // the trace kernel reads the hit shape's and material's records whole
+#endif
+#ifndef RT_MAT_BULK
+#define RT_MAT_BULK 1  // the combine reads a node's material whole (rt_common.hpp load_mat)
+#endif
+
+
 namespace rtdev {
 
 #define RT_SHADOW_COUNT(P) ((P).levels[2 * (RT_MAX_DEPTH + 1)])
@@ -535,8 +543,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 }
             } else {
                 hit = true;
+#if RT_HIT_BULK
+                // the hit shape's record whole, then its material whole: two round trips
+                const ShapeW SR = load_shape(S.shapes, bk >> 4);
+                const MatRec M = load_mat(S.mats, (uint32_t)SR.mat());
+                Hit h = hit_attrs_w(S, SR, bk, ro, rd, M.kind == RT_MAT_TEXTURE_PHONG);
+#else
                 const MatRec& M = S.mats[S.shapes[bk >> 4].mat];
                 Hit h = hit_attrs(S, bk, ro, rd, M.kind == RT_MAT_TEXTURE_PHONG);
+#endif
                 float ri = M.refraction_index;
                 float n1 = h.entering ? 1.f : ri;
                 float n2 = h.entering ? ri : 1.f;
@@ -833,35 +848,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
     bc_flush(ops_slot(S), P.ray_counters);
 }
 
-// A material record (80 B) in five 16-B loads issued together: read field by field
-// through a reference, the texture-kind branches of the shading split the loads into
-// dependent round trips
-#ifndef RT_MAT_BULK
-#define RT_MAT_BULK 1
-#endif
-__device__ __forceinline__ MatRec load_mat(const MatRec* mats, uint32_t i) {
-#if RT_MAT_BULK
-    static_assert(sizeof(MatRec) == 80, "MatRec is five float4");
-    const float4* p = reinterpret_cast<const float4*>(mats + i);
-    const float4 a = p[0], b = p[1], c = p[2], d = p[3], e = p[4];
-    MatRec M;
-    M.kind = __float_as_int(a.x);
-    M.dark_zero = __float_as_int(a.y);
-    M.power = a.z;
-    M.reflectivity = a.w;
-    M.refraction_index = b.x;
-    M.pad1 = b.y;
-    M.pad2 = b.z;
-    M.pad3 = b.w;
-    M.ambient = TexRec{__float_as_int(c.x), c.y, c.z, c.w};
-    M.diffuse = TexRec{__float_as_int(d.x), d.y, d.z, d.w};
-    M.specular = TexRec{__float_as_int(e.x), e.y, e.z, e.w};
-    return M;
-#else
-    return mats[i];
-#endif
-}
-
 // The stored part of a hit node (rt_device.hpp) and what the shading passes derive from it:
 // eye_dir = -norm(ray direction) (the Intersection's eye_dir, sphere.rs:81 etc.), n1 / n2
 // from `entering` (render.rs:51-55), the material's textures at (u, v).
@@ -972,7 +958,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_COMBINE_
         V3 c = v3(0.f, 0.f, 0.f);
         uint32_t parent = 0;
         if (flags & NODE_HIT) {
+#if RT_MAT_BULK
             const MatRec M = load_mat(S.mats, flags >> F_MAT_SHIFT);
+#else
+            const MatRec& M = S.mats[flags >> F_MAT_SHIFT];
+#endif
             const NodeIn q = node_in(qa, qb, qc, flags, M);
             parent = q.parent;
             const V3 ka = tex_eval(M.ambient, q.h.tu, q.h.tv);
