@@ -160,6 +160,8 @@ static rt_status ensure_buffers(rt_multi_state* m, size_t band_floats, size_t fr
     return RT_OK;
 }
 
+static rt_status multi_finish(rt_multi_state* m, const rt_render_opts* opts);
+
 rt_status rt_multi_render(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
                           const rt_render_opts* opts, float* rgb, uint8_t* rgb8) {
     return rt_multi_render_state(rt_scene_multi(s), cam, depth, spp, seed, opts, rgb, rgb8);
@@ -177,6 +179,59 @@ rt_status rt_multi_render_state(rt_multi_state* m, const rt_camera* cam, uint32_
     std::vector<char> redo(world, 1);  // ranks whose bands (re-)render in this attempt
     MHIP(hipSetDevice(m->devices[0]));
     MHIP(hipEventRecord(m->ev0, s0));
+    if (!m->rccl && band_rows >= rpr) {
+        // Every rank holds ONE band: rows [r band_rows, (r + 1) band_rows) of the frame, row
+        // major -- its band buffer is already that slice of the frame.  No gather and no
+        // un-permute: each rank's slice goes from its own stream straight to the caller's
+        // buffers, so the first share's copy runs while the other shares still render
+        // (rt_render's seam split on one device).
+        for (int attempt = 0;; attempt++) {
+            for (uint32_t r = 0; r < world; r++) {
+                if (!redo[r]) continue;
+                MHIP(hipSetDevice(m->devices[r]));
+                MHIP(hipMemsetAsync(m->counters[r], 0, 3 * sizeof(unsigned long long), m->streams[r]));
+                st = rt_render_bands_ex_async(m->ranks[r], cam, 1, depth, spp, seed, band_rows, r, world, m->band[r],
+                                              rgb8 ? m->band8[r] : nullptr, (uint64_t*)m->counters[r], m->streams[r]);
+                if (st != RT_OK) return st;
+                MHIP(hipEventRecord(m->done[r], m->streams[r]));
+            }
+            // the render's span on device 0's clock: from ev0 to the last share's end
+            MHIP(hipSetDevice(m->devices[0]));
+            for (uint32_t r = 0; r < world; r++) MHIP(hipStreamWaitEvent(s0, m->done[r], 0));
+            MHIP(hipEventRecord(m->ev1, s0));
+            // every render is enqueued before the first copy: a copy into pageable memory
+            // may hold this thread until it is done
+            for (uint32_t r = 0; r < world; r++) {
+                if (!redo[r]) continue;
+                const uint32_t y0 = r * band_rows;
+                const uint32_t rows = y0 < cam->y_res ? std::min(band_rows, cam->y_res - y0) : 0u;
+                const size_t off = (size_t)y0 * cam->x_res * 3u, len = (size_t)rows * cam->x_res * 3u;
+                if (!len) continue;
+                MHIP(hipSetDevice(m->devices[r]));
+                MHIP(hipMemcpyAsync(rgb + off, m->band[r], len * sizeof(float), hipMemcpyDeviceToHost, m->streams[r]));
+                if (rgb8)
+                    MHIP(hipMemcpyAsync(rgb8 + off, m->band8[r], len, hipMemcpyDeviceToHost, m->streams[r]));
+            }
+            for (uint32_t r = 0; r < world; r++) {
+                MHIP(hipSetDevice(m->devices[r]));
+                MHIP(hipStreamSynchronize(m->streams[r]));
+            }
+            // a rank whose queues overflowed renders (and copies) its slice again with a
+            // grown pool; the other slices are final
+            bool overflow = false;
+            for (uint32_t r = 0; r < world; r++) {
+                st = rt_scene_sync_status(m->ranks[r]);
+                redo[r] = st == RT_ERR_CAPACITY;
+                if (redo[r])
+                    overflow = true;
+                else if (st != RT_OK)
+                    return st;
+            }
+            if (!overflow) break;
+            if (attempt >= 8) return RT_ERR_CAPACITY;
+        }
+        return multi_finish(m, opts);
+    }
     for (int attempt = 0;; attempt++) {
         for (uint32_t r = 0; r < world; r++) {
             if (!redo[r]) continue;
@@ -248,6 +303,12 @@ rt_status rt_multi_render_state(rt_multi_state* m, const rt_camera* cam, uint32_
     MHIP(hipMemcpyAsync(rgb, m->frame, ff * sizeof(float), hipMemcpyDeviceToHost, s0));
     if (rgb8) MHIP(hipMemcpyAsync(rgb8, m->frame8, ff, hipMemcpyDeviceToHost, s0));
     MHIP(hipStreamSynchronize(s0));
+    return multi_finish(m, opts);
+}
+
+// the render's counters (summed over the ranks) and span, for rt_render_opts
+static rt_status multi_finish(rt_multi_state* m, const rt_render_opts* opts) {
+    const uint32_t world = (uint32_t)m->ranks.size();
     if (opts && opts->counters) {
         rt_counters c{0, 0, 0, 0};
         for (uint32_t r = 0; r < world; r++) {

@@ -1,11 +1,13 @@
 #!/bin/bash
-# GPU suite + default bench + every BASELINE config (frame checks)
+# round-3 check 4: rt_render's seam split copies each share's rows straight to the caller
+# (no gather / un-permute): seam tests, whole frames, then the seam timings
 set -o pipefail
-TAG=${1:-r3e}
 mkdir -p gpurun_out
-timeout -k 10 1000 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/$TAG.tests.log 2>&1
-rc=$?
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc $rc"; exit 1; fi
-timeout -k 10 400 python bench.py > gpurun_out/$TAG.bench.json 2> gpurun_out/$TAG.bench.err || exit 2
-bash tools/configs_run.sh $TAG.configs || exit 3
-echo "done (pytest rc $rc)"
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
+  tests/test_gpu_seam.py tests/test_gpu_fullframe.py tests/test_gpu_parity.py > gpurun_out/r3c4_tests.txt 2>&1 || exit 1
+O=gpurun_out/r3c4_seam.jsonl
+: > $O
+for v in "RT_X=0" "RT_X=0"; do
+  env $v timeout -k 10 200 python tools/seam_time.py >> $O 2>> gpurun_out/seam.err || exit 2
+done
+echo done
