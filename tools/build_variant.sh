@@ -1,16 +1,20 @@
 #!/bin/bash
-# Builds an A/B variant of the product library with extra device-compile flags on the
-# wavefront and ordering kernels: tools/build_variant.sh NAME "-DFOO=1 ..." -> rust_tracer_amd/librt_hip_NAME.so
-# (the other objects are the product's own; run `make` first).  Use with RT_LIB=... .
+# Builds an A/B variant of the product library with extra compile flags:
+#   tools/build_variant.sh NAME "-DRT_SWITCH=0 ..."  -> rust_tracer_amd/librt_hip_NAME.so
+# (load it with RT_LIB=rust_tracer_amd/librt_hip_NAME.so; tools/ab_env.sh takes RT_LIB=...)
 set -e
-NAME=$1; shift
-cd "$(dirname "$0")/../rust_tracer_amd/csrc"
-make -s
-T=/tmp/rt_variant_$NAME
-mkdir -p $T
-F="-O3 -std=c++17 -fPIC -ffp-contract=off -Wall --offload-arch=gfx950 -munsafe-fp-atomics"
-/opt/rocm/bin/hipcc $F "$@" -c -o $T/rt_wavefront.o rt_wavefront.hip
-/opt/rocm/bin/hipcc $F "$@" -c -o $T/rt_order.o rt_order.hip
-/opt/rocm/bin/hipcc $F -shared -o ../librt_hip_$NAME.so build/rt_kernels.o $T/rt_wavefront.o \
-    $T/rt_order.o build/rt_api.o build/rt_multi.o build/rt_bvh.o build/scene.o build/image_io.o
+NAME=$1; FLAGS=$2
+R=$(cd "$(dirname "$0")/.." && pwd)
+C=$R/rust_tracer_amd/csrc
+B=/tmp/rt_variant_$NAME
+mkdir -p $B
+HF="-O3 -std=c++17 -fPIC -ffp-contract=off -Wall --offload-arch=gfx950 -munsafe-fp-atomics $FLAGS"
+CF="-O3 -std=c++17 -fPIC -ffp-contract=off -Wall $FLAGS"
+for f in rt_kernels rt_wavefront rt_order; do /opt/rocm/bin/hipcc $HF -c -o $B/$f.o $C/$f.hip & done
+for f in rt_api rt_multi; do /opt/rocm/bin/hipcc $HF -c -o $B/$f.o $C/$f.cpp & done
+/opt/rocm/bin/hipcc $CF -x c++ -c -o $B/rt_bvh.o $C/rt_bvh.cpp &
+/opt/rocm/bin/hipcc $CF -x c++ -c -o $B/image_io.o $C/host/image_io.cpp &
+/opt/rocm/bin/hipcc $CF -x c++ -c -o $B/scene.o $C/host/scene.cpp &
+wait
+/opt/rocm/bin/hipcc $HF -shared -o $R/rust_tracer_amd/librt_hip_$NAME.so $B/*.o -ldl
 echo built rust_tracer_amd/librt_hip_$NAME.so
