@@ -1160,6 +1160,7 @@ struct rt_scene {
     rt_multi_state* multi = nullptr;  // rt_scene_create_multi: the other devices' clones (rt_multi.cpp)
     rt_multi_state* split = nullptr;  // rt_render's band shares on this one device (seam_split)
     int split_n = 0;
+    uint32_t seam_rows = 0, seam_y = 0;  // the two shares' meeting row (adapted per render) for y_res seam_y
 };
 
 rt_multi_state*& rt_scene_multi(rt_scene* s) { return s->multi; }
@@ -2350,9 +2351,57 @@ rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t de
         // bands dealt in turn -- shares of different content fall out of step, so one share's
         // level tails meet the other's work)
         const char* br = std::getenv("RT_SEAM_BAND_ROWS");
-        const uint32_t rows = ((cam->y_res + (uint32_t)split - 1u) / (uint32_t)split + 7u) / 8u * 8u;
-        rt_multi_set_band_rows(s->split, br ? (uint32_t)std::max(1, std::atoi(br)) : rows);
-        return rt_multi_render_state(s->split, cam, depth, spp, seed, opts, rgb, rgb8);
+        const uint32_t even = ((cam->y_res + (uint32_t)split - 1u) / (uint32_t)split + 7u) / 8u * 8u;
+        // Two shares meet where they finish together: after each render the row moves 8 rows
+        // toward the share that finished last (within [half, 3/4] of the frame: share 0 holds
+        // one band only down to half the rows).  Config 3: share 0 (the top) is the cheaper
+        // half; fixed rows 544 / 576 / 608 measured 3.38 / 3.35 / 3.37 ms (RT_SEAM_BAND_ROWS
+        // pins the row, RT_SEAM_ADAPT=0 keeps the even split)
+        const char* ad = std::getenv("RT_SEAM_ADAPT");
+        const bool adapt = !br && split == 2 && !(ad && ad[0] == '0');
+        const uint32_t hi = std::max(even, (cam->y_res * 3u / 4u) / 8u * 8u);
+        if (s->seam_y != cam->y_res || s->seam_rows < even || s->seam_rows > hi) {
+            s->seam_rows = even;
+            s->seam_y = cam->y_res;
+            if (adapt) {  // every share's node pool sized once for the largest share it can get
+                const uint64_t floor = std::min<uint64_t>((uint64_t)hi * cam->x_res * node_factor(), pool_cap_limit(s));
+                auto raise = [&](rt_scene* c) {
+                    c->pool_floor = std::max<uint32_t>(c->pool_floor, (uint32_t)floor);
+                    return RT_OK;
+                };
+                (void)raise(s);
+                (void)rt_multi_each(s->split, raise);
+            }
+        }
+        const uint32_t rows = br ? (uint32_t)std::max(1, std::atoi(br)) : (adapt ? s->seam_rows : even);
+        rt_multi_set_band_rows(s->split, rows);
+        // the shares' persistent grids at RT_SEAM_GRID_PCT % of the chip (default 80: two
+        // concurrent full-chip grids leave more blocks waiting for a slot; 100 / 90 / 80 at
+        // the 576-row meeting: 3.35 / 3.31 - 3.34 / 3.30 - 3.31 ms), or the scene's own
+        // share if that is smaller; restored afterwards
+        const char* gp = std::getenv("RT_SEAM_GRID_PCT");
+        const int pct = std::min(s->grid_pct, gp ? std::max(1, std::min(100, std::atoi(gp))) : 80);
+        const int saved = s->grid_pct;
+        auto set_pct = [&](int v) {
+            s->grid_pct = v;
+            (void)rt_multi_each(s->split, [&](rt_scene* c) {
+                c->grid_pct = v;
+                return RT_OK;
+            });
+        };
+        set_pct(pct);
+        rt_status st = rt_multi_render_state(s->split, cam, depth, spp, seed, opts, rgb, rgb8);
+        set_pct(saved);
+        if (st == RT_OK && adapt) {
+            float t[2] = {0.f, 0.f};
+            if (rt_multi_share_ms(s->split, t, 2) == RT_OK && t[0] > 0.f && t[1] > 0.f) {
+                if (t[0] < 0.97f * t[1] && s->seam_rows + 8u <= hi)
+                    s->seam_rows += 8u;
+                else if (t[1] < 0.97f * t[0] && s->seam_rows >= even + 8u)
+                    s->seam_rows -= 8u;
+            }
+        }
+        return st;
     }
     HIP_TRY(hipSetDevice(s->device));
     size_t n = (size_t)cam->x_res * cam->y_res * 3;

@@ -23,4 +23,7 @@ rt_status rt_multi_build(rt_scene* s0, const int32_t* devices, uint32_t n_device
 void rt_multi_set_band_rows(rt_multi_state* m, uint32_t band_rows);
 // Applies `f` to every clone (devices[1..]) of a multi-device scene; first error wins.
 rt_status rt_multi_each(rt_multi_state* m, const std::function<rt_status(rt_scene*)>& f);
+// the last render's per-rank finish times (ms after its start) on one device's copy
+// exchange; RT_ERR_UNSUPPORTED when it did not run that way
+rt_status rt_multi_share_ms(rt_multi_state* m, float* ms, uint32_t n);
 void rt_multi_free(rt_multi_state* m);

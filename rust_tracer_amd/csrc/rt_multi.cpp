@@ -89,6 +89,7 @@ struct rt_multi_state {
     Rccl lib;
     std::vector<ncclComm_t> comms;
     uint32_t band_rows = 8;                  // rows per band (block-cyclic over the ranks)
+    bool direct = false;                     // the last render copied each rank's one band straight out
 };
 
 rt_status rt_multi_each(rt_multi_state* m, const std::function<rt_status(rt_scene*)>& f) {
@@ -138,6 +139,7 @@ void rt_multi_free(rt_multi_state* m) {
     delete m;  // the RCCL library stays loaded (another communicator may use it)
 }
 
+// frame_floats == 0: band buffers only (the direct copy-out needs no gather / frame buffers)
 static rt_status ensure_buffers(rt_multi_state* m, size_t band_floats, size_t frame_floats, bool want8) {
     if (band_floats <= m->band_floats && frame_floats <= m->frame_floats && (!want8 || m->have8)) return RT_OK;
     free_buffers(m);
@@ -148,11 +150,13 @@ static rt_status ensure_buffers(rt_multi_state* m, size_t band_floats, size_t fr
         if (want8) MHIP(hipMalloc(&m->band8[r], band_floats));
     }
     MHIP(hipSetDevice(m->devices[0]));
-    MHIP(hipMalloc(&m->gathered, world * band_floats * sizeof(float)));
-    MHIP(hipMalloc(&m->frame, frame_floats * sizeof(float)));
-    if (want8) {
-        MHIP(hipMalloc(&m->gathered8, world * band_floats));
-        MHIP(hipMalloc(&m->frame8, frame_floats));
+    if (frame_floats) {
+        MHIP(hipMalloc(&m->gathered, world * band_floats * sizeof(float)));
+        MHIP(hipMalloc(&m->frame, frame_floats * sizeof(float)));
+        if (want8) {
+            MHIP(hipMalloc(&m->gathered8, world * band_floats));
+            MHIP(hipMalloc(&m->frame8, frame_floats));
+        }
     }
     m->band_floats = band_floats;
     m->frame_floats = frame_floats;
@@ -161,6 +165,14 @@ static rt_status ensure_buffers(rt_multi_state* m, size_t band_floats, size_t fr
 }
 
 static rt_status multi_finish(rt_multi_state* m, const rt_render_opts* opts);
+
+rt_status rt_multi_share_ms(rt_multi_state* m, float* ms, uint32_t n) {
+    if (!m || !ms || n > m->ranks.size() || m->rccl || !m->direct) return RT_ERR_UNSUPPORTED;
+    if (hipSetDevice(m->devices[0]) != hipSuccess) return RT_ERR_HIP;
+    for (uint32_t r = 0; r < n; r++)
+        if (hipEventElapsedTime(&ms[r], m->ev0, m->done[r]) != hipSuccess) return RT_ERR_HIP;
+    return RT_OK;
+}
 
 rt_status rt_multi_render(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
                           const rt_render_opts* opts, float* rgb, uint8_t* rgb8) {
@@ -173,13 +185,18 @@ rt_status rt_multi_render_state(rt_multi_state* m, const rt_camera* cam, uint32_
     const uint32_t world = (uint32_t)m->ranks.size(), band_rows = m->band_rows;
     const uint32_t rpr = rt_band_rows_per_rank(cam->y_res, band_rows, world);
     const size_t bf = (size_t)rpr * cam->x_res * 3u, ff = (size_t)cam->y_res * cam->x_res * 3u;
-    rt_status st = ensure_buffers(m, bf, ff, rgb8 != nullptr);
+    // one band per rank on one device's copy exchange: each band goes straight to the caller
+    // (below); its buffers are sized for a whole frame once, so a moving meeting row never
+    // reallocates them
+    const bool direct = !m->rccl && band_rows >= rpr;
+    rt_status st = direct ? ensure_buffers(m, ff, 0, rgb8 != nullptr) : ensure_buffers(m, bf, ff, rgb8 != nullptr);
     if (st != RT_OK) return st;
     hipStream_t s0 = m->streams[0];
     std::vector<char> redo(world, 1);  // ranks whose bands (re-)render in this attempt
     MHIP(hipSetDevice(m->devices[0]));
     MHIP(hipEventRecord(m->ev0, s0));
-    if (!m->rccl && band_rows >= rpr) {
+    m->direct = direct;
+    if (direct) {
         // Every rank holds ONE band: rows [r band_rows, (r + 1) band_rows) of the frame, row
         // major -- its band buffer is already that slice of the frame.  No gather and no
         // un-permute: each rank's slice goes from its own stream straight to the caller's
@@ -352,7 +369,7 @@ rt_status rt_multi_build(rt_scene* s0, const int32_t* devices, uint32_t n_device
         if (r > 0 && (st = rt_scene_clone(s0, devices[r], &m->ranks[r])) != RT_OK) return fail(st);
         if (hipSetDevice(devices[r]) != hipSuccess ||
             hipStreamCreateWithFlags(&m->streams[r], hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&m->done[r], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreate(&m->done[r]) != hipSuccess ||
             hipMalloc(&m->counters[r], 3 * sizeof(unsigned long long)) != hipSuccess)
             return fail(RT_ERR_HIP);
     }

@@ -480,3 +480,25 @@ def test_seam_split_changes_nothing(monkeypatch, split, rows):
     ref, rcnt, _, _ = one.render(320, 181, 8)
     one.close()
     assert same_bits(img, ref) and cnt == rcnt
+
+
+def test_adaptive_seam_split_changes_nothing(monkeypatch):
+    """rt_render's two band shares meet at a row that follows their finish times (moved 8 rows
+    per render within [half, 3/4] of the frame, RT_SEAM_ADAPT) and run their grids at a
+    reduced share of the chip (RT_SEAM_GRID_PCT): every one of a run of renders -- whatever
+    row the shares meet at -- equals the single pass bit for bit, RGB8 and counters too."""
+    desc = SceneDesc.synth_config(3)
+    w, h = 640, 361
+    monkeypatch.setenv("RT_SEAM_SPLIT", "1")
+    s = DeviceScene(desc, device=0)
+    ref, rcnt, _, ref8 = s.render(w, h, 8, want_u8=True)
+    s.close()
+    monkeypatch.setenv("RT_SEAM_SPLIT", "2")
+    monkeypatch.delenv("RT_SEAM_BAND_ROWS", raising=False)
+    monkeypatch.delenv("RT_SEAM_ADAPT", raising=False)
+    monkeypatch.setenv("RT_SEAM_GRID_PCT", "60")
+    s = DeviceScene(desc, device=0)
+    for _ in range(12):
+        img, cnt, _, img8 = s.render(w, h, 8, want_u8=True)
+        assert same_bits(img, ref) and np.array_equal(img8, ref8) and cnt == rcnt
+    s.close()
