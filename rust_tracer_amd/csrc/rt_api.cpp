@@ -2352,13 +2352,16 @@ rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t de
         // level tails meet the other's work)
         const char* br = std::getenv("RT_SEAM_BAND_ROWS");
         const uint32_t even = ((cam->y_res + (uint32_t)split - 1u) / (uint32_t)split + 7u) / 8u * 8u;
-        // Two shares meet where they finish together: after each render the row moves 8 rows
-        // toward the share that finished last (within [half, 3/4] of the frame: share 0 holds
+        // Two shares meet where share 1 finishes as share 0's rows reach the caller (share 0's
+        // copy then runs under share 1's tail): after each render the row moves 8 rows toward
+        // the share that is late on that mark (within [half, 3/4] of the frame: share 0 holds
         // one band only down to half the rows).  Config 3: share 0 (the top) is the cheaper
-        // half; fixed rows 544 / 576 / 608 measured 3.38 / 3.35 / 3.37 ms (RT_SEAM_BAND_ROWS
-        // pins the row, RT_SEAM_ADAPT=0 keeps the even split)
+        // half; fixed rows 544 / 576 / 608 measured 3.38 / 3.35 / 3.37 ms of device time
+        // (RT_SEAM_BAND_ROWS pins the row, RT_SEAM_ADAPT=0 keeps the even split,
+        // RT_SEAM_ADAPT=device balances the finish times alone)
         const char* ad = std::getenv("RT_SEAM_ADAPT");
         const bool adapt = !br && split == 2 && !(ad && ad[0] == '0');
+        const bool adapt_copy = !(ad && std::strcmp(ad, "device") == 0);
         const uint32_t hi = std::max(even, (cam->y_res * 3u / 4u) / 8u * 8u);
         if (s->seam_y != cam->y_res || s->seam_rows < even || s->seam_rows > hi) {
             s->seam_rows = even;
@@ -2393,11 +2396,14 @@ rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t de
         rt_status st = rt_multi_render_state(s->split, cam, depth, spp, seed, opts, rgb, rgb8);
         set_pct(saved);
         if (st == RT_OK && adapt) {
-            float t[2] = {0.f, 0.f};
-            if (rt_multi_share_ms(s->split, t, 2) == RT_OK && t[0] > 0.f && t[1] > 0.f) {
-                if (t[0] < 0.97f * t[1] && s->seam_rows + 8u <= hi)
+            float t[2] = {0.f, 0.f}, c[2] = {0.f, 0.f};
+            if (rt_multi_share_ms(s->split, t, 2) == RT_OK && t[0] > 0.f && t[1] > 0.f &&
+                (!adapt_copy || rt_multi_copy_ms(s->split, c, 2) == RT_OK)) {
+                // > 0: share 1 ends after share 0's rows are out -- share 0 can take more rows
+                const float late = t[1] - (t[0] + c[0]), band = 0.03f * t[1];
+                if (late > band && s->seam_rows + 8u <= hi)
                     s->seam_rows += 8u;
-                else if (t[1] < 0.97f * t[0] && s->seam_rows >= even + 8u)
+                else if (late < -band && s->seam_rows >= even + 8u)
                     s->seam_rows -= 8u;
             }
         }

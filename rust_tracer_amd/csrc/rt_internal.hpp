@@ -26,4 +26,6 @@ rt_status rt_multi_each(rt_multi_state* m, const std::function<rt_status(rt_scen
 // the last render's per-rank finish times (ms after its start) on one device's copy
 // exchange; RT_ERR_UNSUPPORTED when it did not run that way
 rt_status rt_multi_share_ms(rt_multi_state* m, float* ms, uint32_t n);
+// ... and each rank's copy-out time (from its finish to its band in the caller's buffers)
+rt_status rt_multi_copy_ms(rt_multi_state* m, float* ms, uint32_t n);
 void rt_multi_free(rt_multi_state* m);

@@ -74,6 +74,7 @@ struct rt_multi_state {
     std::vector<rt_scene*> ranks;            // ranks[0] = the primary handle (not owned here)
     std::vector<hipStream_t> streams;        // one per rank, on its device
     std::vector<hipEvent_t> done;            // per rank: its band is rendered (copy exchange)
+    std::vector<hipEvent_t> copied;          // per rank: its band is in the caller's buffers (direct copy-out)
     hipEvent_t ev0 = nullptr, ev1 = nullptr; // device 0: the render's span
     std::vector<float*> band;                // per rank: rows_per_rank x x_res x 3 floats
     std::vector<uint8_t*> band8;             // per rank: ... bytes (when RGB8 is asked for)
@@ -128,6 +129,7 @@ void rt_multi_free(rt_multi_state* m) {
         (void)hipSetDevice(m->devices[r]);
         if (r < m->counters.size() && m->counters[r]) (void)hipFree(m->counters[r]);
         if (r < m->done.size() && m->done[r]) (void)hipEventDestroy(m->done[r]);
+        if (r < m->copied.size() && m->copied[r]) (void)hipEventDestroy(m->copied[r]);
         if (r < m->streams.size() && m->streams[r]) (void)hipStreamDestroy(m->streams[r]);
         if (r > 0 && m->ranks[r]) (void)rt_scene_destroy(m->ranks[r]);
     }
@@ -171,6 +173,14 @@ rt_status rt_multi_share_ms(rt_multi_state* m, float* ms, uint32_t n) {
     if (hipSetDevice(m->devices[0]) != hipSuccess) return RT_ERR_HIP;
     for (uint32_t r = 0; r < n; r++)
         if (hipEventElapsedTime(&ms[r], m->ev0, m->done[r]) != hipSuccess) return RT_ERR_HIP;
+    return RT_OK;
+}
+
+rt_status rt_multi_copy_ms(rt_multi_state* m, float* ms, uint32_t n) {
+    if (!m || !ms || n > m->ranks.size() || m->rccl || !m->direct) return RT_ERR_UNSUPPORTED;
+    if (hipSetDevice(m->devices[0]) != hipSuccess) return RT_ERR_HIP;
+    for (uint32_t r = 0; r < n; r++)
+        if (hipEventElapsedTime(&ms[r], m->done[r], m->copied[r]) != hipSuccess) return RT_ERR_HIP;
     return RT_OK;
 }
 
@@ -228,6 +238,7 @@ rt_status rt_multi_render_state(rt_multi_state* m, const rt_camera* cam, uint32_
                 MHIP(hipMemcpyAsync(rgb + off, m->band[r], len * sizeof(float), hipMemcpyDeviceToHost, m->streams[r]));
                 if (rgb8)
                     MHIP(hipMemcpyAsync(rgb8 + off, m->band8[r], len, hipMemcpyDeviceToHost, m->streams[r]));
+                MHIP(hipEventRecord(m->copied[r], m->streams[r]));
             }
             for (uint32_t r = 0; r < world; r++) {
                 MHIP(hipSetDevice(m->devices[r]));
@@ -358,6 +369,7 @@ rt_status rt_multi_build(rt_scene* s0, const int32_t* devices, uint32_t n_device
     m->ranks[0] = s0;
     m->streams.assign(n_devices, nullptr);
     m->done.assign(n_devices, nullptr);
+    m->copied.assign(n_devices, nullptr);
     m->band.assign(n_devices, nullptr);
     m->band8.assign(n_devices, nullptr);
     m->counters.assign(n_devices, nullptr);
@@ -369,7 +381,7 @@ rt_status rt_multi_build(rt_scene* s0, const int32_t* devices, uint32_t n_device
         if (r > 0 && (st = rt_scene_clone(s0, devices[r], &m->ranks[r])) != RT_OK) return fail(st);
         if (hipSetDevice(devices[r]) != hipSuccess ||
             hipStreamCreateWithFlags(&m->streams[r], hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreate(&m->done[r]) != hipSuccess ||
+            hipEventCreate(&m->done[r]) != hipSuccess || hipEventCreate(&m->copied[r]) != hipSuccess ||
             hipMalloc(&m->counters[r], 3 * sizeof(unsigned long long)) != hipSuccess)
             return fail(RT_ERR_HIP);
     }
