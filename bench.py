@@ -67,7 +67,7 @@ def parse():
                         "per pass and rank; 1 for spp > 1, whose samples are batched inside each pass)")
     p.add_argument("--inflight", type=int, default=None,
                    help="frames in flight (F scene handles / HIP streams; default 4 = the box's hardware "
-                        "queues per process); 1 = one at a time")
+                        "queues per process, 3 from 4 ranks up); 1 = one at a time")
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU oracle timing")
     p.add_argument("--cpu-threads", type=int, default=None,
                    help="threads of the multi-core CPU baseline (default: every core in the affinity mask)")
@@ -335,7 +335,11 @@ def main():
     t_sc = time.perf_counter()
     scene = DeviceScene(desc, device=dev.index)   # host build (hierarchy, light buffers) + upload
     scene_create_ms = (time.perf_counter() - t_sc) * 1e3
-    inflight = max(1, args.inflight or 4)
+    # 4 passes in flight; 3 from N = 4 up, where a rank's share of a frame is small and fewer,
+    # bigger passes amortise each level's fixed latency (one rank's share of a K = 20 burst on
+    # one MI355X, tools/r3_share2.sh: N = 8: 0.310 vs 0.326 ms per share-frame, N = 4: 0.543 vs
+    # 0.554; N = 1: 3 x 7 1018 / 1017 vs 4 x 5 1027 / 1033 Mpixels/s)
+    inflight = max(1, args.inflight or (3 if world >= 4 else 4))
     if args.batch is None:
         # The timed K frames are spread evenly over the F slots: q = ceil(K / F) frames per
         # slot, in r = ceil(q / cap) passes of B frames -- a divisor of q when one is near
