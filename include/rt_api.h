@@ -204,7 +204,12 @@ int32_t rt_scene_uses_rccl(const rt_scene* scene);
 
 /* render.rs:31-38: fill `rgb` (h*w*3 float, row-major [v][u][c]) with
  * trace_ray(get_ray(u, v), depth) for every pixel.  `rgb8` (optional, may be NULL)
- * receives Color::as_u8 (color.rs:43-46) of every pixel, row-major RGB8. */
+ * receives Color::as_u8 (color.rs:43-46) of every pixel, row-major RGB8.
+ * On a one-device scene the frame is rendered as two contiguous row shares side by side on
+ * two streams (RT_SEAM_SPLIT, default 2; 1 = one pass), each copied from its own stream
+ * straight into `rgb` / `rgb8`; the row where the shares meet follows their finish times
+ * from call to call (RT_SEAM_ADAPT; RT_SEAM_BAND_ROWS pins it) and their persistent grids
+ * take RT_SEAM_GRID_PCT (default 80) % of the chip.  None of this changes a pixel. */
 rt_status rt_render(const rt_scene* scene, const rt_camera* camera, uint32_t depth,
                     const rt_render_opts* opts, float* rgb, uint8_t* rgb8);
 
