@@ -51,7 +51,10 @@ OP_FLOPS = {"node_pairs": 24, "dsph_pairs": 2 * 57, "gsph": 57, "tri_pairs": 2 *
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
+    # K = 64 timed frames by default: every slot runs 2 passes of 8 frames, the steady state
+    # of frames in flight (K = 20 is one pass of 5 per slot, its fill and drain included:
+    # 1051 - 1062 vs 1089 - 1095 Mpixels/s at K = 64 / 96, tools/r3_steps.sh)
+    p.add_argument("--steps", type=int, default=64)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", type=int, default=3, help="BASELINE config (2..5 synth scenes)")
     p.add_argument("--width", type=int, default=None, help="default: the config's (1920 / 3840)")
