@@ -51,9 +51,9 @@ OP_FLOPS = {"node_pairs": 24, "dsph_pairs": 2 * 57, "gsph": 57, "tri_pairs": 2 *
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    # K = 64 timed frames by default: every slot runs 2 passes of 8 frames, the steady state
-    # of frames in flight (K = 20 is one pass of 5 per slot, its fill and drain included:
-    # 1051 - 1062 vs 1089 - 1095 Mpixels/s at K = 64 / 96, tools/r3_steps.sh)
+    # K = 64 timed frames by default: every slot runs a pass of 16 frames (K = 20 is one pass
+    # of 5 per slot: 1051 - 1062 Mpixels/s; 2 passes of 8 per slot at K = 64: 1077 - 1095;
+    # tools/r3_steps.sh, tools/r3_steps2.sh)
     p.add_argument("--steps", type=int, default=64)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", type=int, default=3, help="BASELINE config (2..5 synth scenes)")
@@ -66,7 +66,7 @@ def parse():
     p.add_argument("--batch", type=int, default=None,
                    help="frames per pipeline pass (rt_render_bands_batch_async, <= 16; default: the timed "
                         "frames spread evenly over the slots, q = ceil(steps / inflight) per slot in equal "
-                        "passes of up to 8 frames (a divisor of q where one is close) within 8 x 1080p of pixels "
+                        "passes of up to 16 frames (a divisor of q where one is close) within 16 x 1080p of pixels "
                         "per pass and rank; 1 for spp > 1, whose samples are batched inside each pass)")
     p.add_argument("--inflight", type=int, default=None,
                    help="frames in flight (F scene handles / HIP streams; default 4 = the box's hardware "
@@ -346,18 +346,20 @@ def main():
     if args.batch is None:
         # The timed K frames are spread evenly over the F slots: q = ceil(K / F) frames per
         # slot, in r = ceil(q / cap) passes of B frames -- a divisor of q when one is near
-        # ceil(q / r), so that every slot runs the same passes.  Up to 8 frames per pass
-        # (bounded workspace: <= 8 x 1080p of pixels per pass and rank, ~1.1 KB per pixel).
+        # ceil(q / r), so that every slot runs the same passes.  Up to 16 frames per pass
+        # (bounded workspace: <= 16 x 1080p of pixels per pass and rank, ~1.1 KB per pixel).
         # Round 2, ms per share-frame on one MI355X at K = 20 (tools/share_burst.py): N = 1:
         # B = 2 / 4 / 5 / 8: 2.46 / 2.51 / 2.31 / 2.36; N = 8: 0.533 / 0.464 / 0.389 / 0.381
         # (DESIGN.md "Frame batches")
         share = band_rows_per_rank(args.height, args.band_rows, world) * args.width
         if args.spp > 1:
             cap = 1
-        else:  # up to 8 frames, within 8 x 1080p of pixels per pass and rank (~18 GB of workspace);
-            # bigger passes lost at K = 20 (4 x 5: 1027 / 1033, 3 x 7: 1018 / 1017, 2 x 10: 750,
-            # 1 x 16: 796 Mpixels/s -- fewer passes in flight)
-            cap = max(1, min(8, (8 * 1920 * 1088) // share))
+        else:  # up to 16 frames (RT_MAX_FRAMES), within 16 x 1080p of pixels per pass and rank
+            # (~37 GB of workspace per slot, ~150 GB for 4 slots of the 288 GB): at K = 64, 4 x 16
+            # 1118 - 1126 vs 4 x 8 1077 - 1084 Mpixels/s (tools/r3_steps2.sh).  Passes in flight
+            # come first: at K = 20 bigger passes lost (4 x 5: 1027 / 1033, 3 x 7: 1018 / 1017,
+            # 2 x 10: 750, 1 x 16: 796)
+            cap = max(1, min(16, (16 * 1920 * 1088) // share))
         q = -(-args.steps // inflight)
         r = -(-q // cap)
         b = -(-q // r)
