@@ -70,7 +70,8 @@ def main():
     # trace runs: warmup + slot set-up + steps frames; divide by all frames rendered
     f4 = bench["config"]["frames_in_flight"]
     # slot set-up (inflight x batch frames) + warm-up + timed frames
-    t4, f_t4, _ = trace_table(os.path.join(src, "trace"), 20 + 4 + f4)  # tools/prof2.sh: --steps 20 --warmup 4
+    # the trace run repeats bench.json's own arguments (tools/prof3.sh)
+    t4, f_t4, _ = trace_table(os.path.join(src, "trace"), bench["steps"] + bench["warmup"] + f4)
     t1, f_t1, _ = trace_table(os.path.join(src, "trace1"), 6 + 1 + 1)
     out += ["## rocprofv3 --kernel-trace (ms of kernel time per frame)", "",
             f"| kernel | {f4} frames in flight ({bench['config']['passes_in_flight']} passes x "
@@ -88,7 +89,10 @@ def main():
     commit = os.environ.get("PROFILE_COMMIT") or subprocess.run(
         ["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True).stdout.strip()
     # PMC passes: (suffix, frames per pass, frames rendered in the run: the slot's set-up pass + steps)
-    runs = [("_b1", 1, 5), ("_b5", 5, 10)] if os.path.isdir(os.path.join(src, "pmc_fetch_b1")) else [("", 1, 5)]
+    # (b1: --steps 4 after a 1-frame set-up pass; bN: --steps N after an N-frame set-up pass)
+    sizes = sorted(int(d[len("pmc_fetch_b"):]) for d in os.listdir(src)
+                   if d.startswith("pmc_fetch_b") and d[len("pmc_fetch_b"):].isdigit())
+    runs = [(f"_b{n}", n, 5 if n == 1 else 2 * n) for n in sizes] if sizes else [("", 1, 5)]
     result = {}
     for suf, per_pass, pmc_frames in runs:
         fe, f_fe = pmc_table(os.path.join(src, "pmc_fetch" + suf), "FETCH_SIZE")
@@ -143,10 +147,11 @@ def main():
                             if sq else None,
                             "source": f"profiles/{tag}/pmc_fetch{suf}.csv, pmc_write{suf}.csv, pmc_sq{suf}.csv"}
     # the headline's pass size when measured, else one frame per pass
-    head = result.get(5) or result[1]
+    big = max(result)
+    head = result[big]
     doc = {"workload": bench["config"]["workload"], "commit": commit, "profile": f"profiles/{tag}",
            "launch": "one frame of the render pipeline (every kernel of the frame), per frame of a "
-                     f"{5 if 5 in result else 1}-frame pass",
+                     f"{big}-frame pass",
            "correction": "FETCH_SIZE x 2 per MI355X_MICROARCH.md (gfx950 tallies 128-B requests at 64 B); "
                          "WRITE_SIZE as reported",
            "sq_source": head["source"]}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU side of a round-3 profile: bench lines, kernel traces (bench defaults and one frame at
 # a time) and PMC passes (HBM FETCH / WRITE, SQ), each its own run; the PMC passes once for
-# one frame per pass and once for a 5-frame pass (the headline's pass size).
+# one frame per pass and once for a BIG-frame pass (default 16, the headline pass size).
 # usage: tools/prof3.sh TAG   -> gpurun_out/TAG/
 set -o pipefail
 TAG=${1:-r3p}
@@ -11,15 +11,17 @@ export TMPDIR=/tmp
 B="--cpu-baseline 0 --seam-stats 0 --check 0"
 cat /sys/fs/cgroup/cpu.max > $OUT/cpu_max.txt 2>/dev/null
 git rev-parse --short=12 HEAD > $OUT/commit.txt 2>/dev/null
-timeout -k 10 300 python bench.py --steps 20 --warmup 4 --cpu-baseline 0 --seam-stats 0 > $OUT/bench.json 2> $OUT/bench.err || exit 1
+# the bench defaults (K = 64, passes of up to 16 frames) and a PMC pass of that size
+BIG=${BIG:-16}
+timeout -k 10 300 python bench.py --warmup 4 --cpu-baseline 0 --seam-stats 0 > $OUT/bench.json 2> $OUT/bench.err || exit 1
 timeout -k 10 300 python bench.py --steps 10 --warmup 2 --inflight 1 --batch 1 $B > $OUT/bench1.json 2> $OUT/bench1.err || exit 2
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-    python bench.py --steps 20 --warmup 4 $B --count-frame 0 > $OUT/trace.log 2>&1 || exit 3
+    python bench.py --warmup 4 $B --count-frame 0 > $OUT/trace.log 2>&1 || exit 3
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace1 -o run -- \
     python bench.py --steps 6 --warmup 1 --inflight 1 --batch 1 $B --count-frame 0 > $OUT/trace1.log 2>&1 || exit 4
 P1="--steps 4 --warmup 0 --inflight 1 --batch 1 $B --count-frame 0"
-P5="--steps 5 --warmup 0 --inflight 1 --batch 5 $B --count-frame 0"
-for cfg in "1:$P1" "5:$P5"; do
+PB="--steps $BIG --warmup 0 --inflight 1 --batch $BIG $B --count-frame 0"
+for cfg in "1:$P1" "$BIG:$PB"; do
   n=${cfg%%:*}; args=${cfg#*:}
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_b$n -o run -- \
       python bench.py $args > $OUT/pmc_fetch_b$n.log 2>&1 || exit 5
