@@ -383,6 +383,8 @@ rt_status rt_scene_set_material(rt_scene* scene, uint32_t index, const rt_materi
 
 const char* rt_status_str(rt_status status);
 int32_t rt_api_version(void);
+/* The most frames one pipeline pass takes (rt_render_bands_batch_async's n_frames). */
+uint32_t rt_max_frames(void);
 
 #ifdef __cplusplus
 }

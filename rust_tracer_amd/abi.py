@@ -171,6 +171,7 @@ def lib():
     L.rt_status_str.argtypes = [C.c_int32]
     L.rt_status_str.restype = C.c_char_p
     L.rt_api_version.restype = C.c_int32
+    L.rt_max_frames.restype = C.c_uint32
     # scene builders (include/rt_scenes.h)
     L.rt_desc_my_scene.argtypes = [P(P(rt_scene_desc))]
     L.rt_desc_bench_128.argtypes = [P(P(rt_scene_desc))]

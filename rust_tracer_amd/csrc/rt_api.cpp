@@ -1276,6 +1276,7 @@ void free_workspace(Workspace& w) {
 extern "C" {
 
 int32_t rt_api_version(void) { return RT_API_VERSION; }
+uint32_t rt_max_frames(void) { return RT_MAX_FRAMES; }
 
 const char* rt_status_str(rt_status s) {
     switch (s) {

@@ -185,8 +185,14 @@ enum : uint32_t {
 
 // frame batches (rt_render_bands_batch_async): up to RT_MAX_FRAMES frames of one
 // resolution in one pipeline pass; a task carries its frame in Task.pixel's top bits
+#ifndef RT_MAX_FRAMES
 #define RT_MAX_FRAMES 16  // 4 frame bits: Task.pixel bits 28-31
+#endif
+#if RT_MAX_FRAMES > 16
+#define RT_FRAME_SHIFT 27  // 32 frames: bits 27-31 (frames of < 2^27 pixels)
+#else
 #define RT_FRAME_SHIFT 28
+#endif
 struct FrameCam {
     float ox, oy, oz, x_min, y_max, x_delta, y_delta, pad;
 };

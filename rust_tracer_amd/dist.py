@@ -53,7 +53,7 @@ class FrameTiler:
         self.rpr = band_rows_per_rank(height, band_rows, world)
         assert self.rpr == band_rows_per_rank_py(height, band_rows, world)
         # frames per pipeline pass (rt_render_bands_batch_async; 1 = rt_render_bands_async)
-        self.batch = max(1, min(int(batch), 16))
+        self.batch = max(1, min(int(batch), int(abi.lib().rt_max_frames())))
         if spp > 1:
             self.batch = 1
         self.cam = abi.camera(width, height)
