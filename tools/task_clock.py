@@ -53,6 +53,16 @@ def main():
             print(f"  level {lv}: iters {len(t):6d}  ticks med {q(0.5):7.0f} p90 {q(0.9):7.0f} p99 {q(0.99):7.0f} "
                   f"max {t[-1]:7.0f}  first start {st.min() - t0:8d}  last start {st.max() - t0:8d}  "
                   f"last end {en.max() - t0:8d}", flush=True)
+            # where the slow tasks sit in the sorted queue: mean ticks per decile of the queue
+            # position, and the deciles of the slowest 1% (inside rays sort last)
+            b = r[:, 1].astype(np.float64)
+            pos = (b - b.min()) / max(1.0, float(b.max() - b.min()) + 64.0)
+            dec = np.minimum((pos * 10).astype(int), 9)
+            tk = r[:, 2].astype(np.float64)
+            means = [tk[dec == d].mean() if np.any(dec == d) else 0.0 for d in range(10)]
+            slow = dec[tk >= np.quantile(tk, 0.99)]
+            print("    mean ticks per queue decile: " + " ".join(f"{m:6.0f}" for m in means) +
+                  "   slowest 1% by decile: " + " ".join(str(int(np.sum(slow == d))) for d in range(10)), flush=True)
             t0 = int(en.max())
     s.close()
 
