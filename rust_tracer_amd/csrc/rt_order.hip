@@ -150,6 +150,7 @@ __global__ __launch_bounds__(SORT_THREADS) void sort_scatter_kernel(SortRef r, c
     uint32_t off;
     const uint32_t n = sort_extent(r, off);
     const uint32_t tiles = (n + SORT_TILE - 1) / SORT_TILE;
+    if (blockIdx.x >= tiles) return;  // a block without a tile (the grid is sized for the queue's capacity)
     const uint32_t t = threadIdx.x;
     // thread t: digits t * DPT ..; their global bases (exclusive scan over every digit)
     uint32_t dtot[DPT], dsum = 0;
