@@ -338,11 +338,13 @@ def main():
     t_sc = time.perf_counter()
     scene = DeviceScene(desc, device=dev.index)   # host build (hierarchy, light buffers) + upload
     scene_create_ms = (time.perf_counter() - t_sc) * 1e3
-    # 4 passes in flight; 3 from N = 4 up, where a rank's share of a frame is small and fewer,
-    # bigger passes amortise each level's fixed latency (one rank's share of a K = 20 burst on
-    # one MI355X, tools/r3_share2.sh: N = 8: 0.310 vs 0.326 ms per share-frame, N = 4: 0.543 vs
-    # 0.554; N = 1: 3 x 7 1018 / 1017 vs 4 x 5 1027 / 1033 Mpixels/s)
-    inflight = max(1, args.inflight or (3 if world >= 4 else 4))
+    # 4 passes in flight.  A short burst at N >= 4 (fewer than 8 frames per slot) takes 3, so
+    # that each pass is bigger: a rank's share of a frame is small there and bigger passes
+    # amortise each level's fixed latency (one rank's share on one MI355X, K = 20,
+    # tools/r3_share2.sh: N = 8: 3 x 7 0.310 vs 4 x 5 0.326 ms per share-frame, N = 4: 0.543 vs
+    # 0.554).  With 16 frames per slot 4 x 16 wins at every N (K = 64, tools/r3_share5.sh:
+    # N = 8: 0.251 vs 0.270 for 3 x 11, N = 4: 0.487 vs 0.508)
+    inflight = max(1, args.inflight or (3 if world >= 4 and -(-args.steps // 4) < 8 else 4))
     if args.batch is None:
         # The timed K frames are spread evenly over the F slots: q = ceil(K / F) frames per
         # slot, in r = ceil(q / cap) passes of B frames -- a divisor of q when one is near
