@@ -1801,8 +1801,11 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
                                                                                                  : (std::strcmp(sk, "mix") == 0 ? 0 : key_default)));
     p.frame_keys = spp_keys == 2 ? 1u : 0u;
     {
-        const char* e = std::getenv("RT_L0_INTERLEAVE");  // A/B
-        p.l0_interleave = (e && e[0] == '1') ? 1u : 0u;
+        // level-0 tiles dealt to a pass's frames in turn (default since the 16-frame passes:
+        // 1124 - 1133 vs 1116 - 1122 Mpixels/s in 7 alternating pairs, tools/r3_ab23.sh /
+        // r3_ab24.sh; at 5-frame passes it was noise); RT_L0_INTERLEAVE=0: frame-major (A/B)
+        const char* e = std::getenv("RT_L0_INTERLEAVE");
+        p.l0_interleave = (e && e[0] == '0') ? 0u : 1u;
     }
     p.sample = sample;
     p.seed = seed;

@@ -254,7 +254,7 @@ struct WaveParams {
     // own buffer (out + f x frame_floats) and spp_accumulate_kernel sums them in sample order
     uint32_t spp_batch;
     uint32_t frame_keys;               // frames > 1: the frame index sits above the queue keys' bits
-    uint32_t l0_interleave;            // frames > 1: level-0 tiles dealt to the frames in turn (A/B)
+    uint32_t l0_interleave;            // frames > 1: level-0 tiles dealt to the frames in turn (default; RT_L0_INTERLEAVE=0 off)
     uint32_t self_shadow;              // trace decides shadow rays its own shape settles (A/B: RT_SELF_SHADOW=0)
     uint32_t inline_levels;            // trace levels < this trace their own shadow rays (RT_INLINE_SHADOW)
     uint32_t sched;                    // work distribution of trace / shadow launches (rt_wavefront.hip sched_base)

@@ -61,9 +61,9 @@ __device__ __forceinline__ PixelRef pixel_of(const WaveParams& P, uint32_t item)
     return r;
 }
 
-// level-0 item t of a frame batch -> (frame, item within the frame).  Frame-major by
-// default; P.l0_interleave: 64-item tiles dealt to the frames in turn (tile k of every frame
-// side by side), so that concurrent level-0 waves of a batch trace the same place
+// level-0 item t of a frame batch -> (frame, item within the frame).  P.l0_interleave (the
+// default): 64-item tiles dealt to the frames in turn (tile k of every frame side by side),
+// so that concurrent level-0 waves of a batch trace the same place; else frame-major
 __device__ __forceinline__ uint32_t item_frame(const WaveParams& P, uint32_t t, uint32_t& local) {
     if (P.frames <= 1) {
         local = t;
