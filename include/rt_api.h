@@ -227,6 +227,22 @@ rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* camera,
                                 uint32_t world, float* d_rgb, uint64_t* d_counters,
                                 void* stream);
 
+/* render.rs:31-38 in stream order: the whole frame, row-major, into device memory (`d_rgb`:
+ * y_res*x_res*3 floats; `d_rgb8` optional, Color::as_u8 bytes; `d_counters` optional, 3
+ * uint64 the kernels ADD node_rays, shadow_rays, pixels into), enqueued on `stream` without
+ * a host round trip.  rt_render's seam split on a one-device scene: two contiguous row
+ * shares render side by side on rt_render's two internal streams (the scene and one clone,
+ * each with its own workspace), forked from and joined back into `stream`; RT_SEAM_SPLIT=1
+ * or y_res < 32: one pass on `stream`.  Bit-identical to rt_render.  A queue overflow is
+ * reported by rt_scene_sync_status (the frame is then incomplete; render it again), also
+ * when an rt_render on the same scene ran in between.  Pass a created stream: on the legacy
+ * null stream the fork and join serialise with the process's other streams (measured 5.4
+ * instead of 3.4 ms per 1080p frame).  One-device scenes
+ * only (RT_ERR_UNSUPPORTED on rt_scene_create_multi's).  No reference counterpart beyond
+ * render() itself: the device-resident form of the seam. */
+rt_status rt_render_frame_async(const rt_scene* scene, const rt_camera* camera, uint32_t depth,
+                                float* d_rgb, uint8_t* d_rgb8, uint64_t* d_counters, void* stream);
+
 /* Frame batch: n_frames (1..16) frames of one resolution, each with its own camera, in one
  * pipeline pass (the per-level launch and latency floor is paid once per batch).  The ray
  * queues of a batch are ordered by ray alone -- rays of different frames that start in the

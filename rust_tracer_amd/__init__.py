@@ -367,6 +367,12 @@ class DeviceScene:
                                                 C.c_void_p(d_rgb_ptr), C.c_void_p(d_counters_ptr),
                                                 C.c_void_p(stream_ptr)), "rt_render_bands_spp_async")
 
+    def render_frame_async(self, cam, depth, d_rgb_ptr, d_counters_ptr, stream_ptr, d_rgb8_ptr=0):
+        """rt_render_frame_async: the whole frame, row-major, into device memory on `stream_ptr`
+        (rt_render's two band shares side by side, forked from and joined into that stream)."""
+        check(self._L.rt_render_frame_async(self.h, C.byref(cam), depth, C.c_void_p(d_rgb_ptr),
+                                             C.c_void_p(d_rgb8_ptr or None), C.c_void_p(d_counters_ptr or None),
+                                             C.c_void_p(stream_ptr)), "rt_render_frame_async")
 
     def render_bands_ex_async(self, cams, depth, band_rows, rank, world, d_rgb_ptr, d_rgb8_ptr, d_counters_ptr,
                               stream_ptr, spp=1, seed=0):

@@ -129,6 +129,7 @@ def lib():
                                               C.c_uint32, vp, vp, vp]
     L.rt_render_bands_ex_async.argtypes = [vp, P(rt_camera), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                            C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp]
+    L.rt_render_frame_async.argtypes = [vp, P(rt_camera), C.c_uint32, vp, vp, vp, vp]
     L.rt_scene_sync_status.argtypes = [vp]
     L.rt_scene_clone.argtypes = [vp, C.c_int32, P(vp)]
     L.rt_scene_create_multi.argtypes = [P(rt_scene_desc), P(C.c_int32), C.c_uint32, P(vp)]

@@ -1161,6 +1161,12 @@ struct rt_scene {
     rt_multi_state* split = nullptr;  // rt_render's band shares on this one device (seam_split)
     int split_n = 0;
     uint32_t seam_rows = 0, seam_y = 0;  // the two shares' meeting row (adapted per render) for y_res seam_y
+    // rt_render_frame_async (on `split`, rt_render's shares): its meeting row for y_res
+    // split_dev_y, whether a render awaits rt_scene_sync_status, and an overflow of such a
+    // render that rt_render's own status check found first (reported by the next
+    // rt_scene_sync_status)
+    uint32_t split_dev_rows = 0, split_dev_y = 0;
+    bool split_dev_pending = false, split_dev_overflow = false;
 };
 
 rt_multi_state*& rt_scene_multi(rt_scene* s) { return s->multi; }
@@ -2223,7 +2229,125 @@ rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* cam, uin
     return rt_render_bands_spp_async(scene, cam, depth, 1, 0, band_rows, rank, world, d_rgb, d_counters, stream);
 }
 
+// rt_render's band shares on this device: s->split with n ranks (s itself and n - 1 clones,
+// each rank its own stream); built on first use, rebuilt when n changes
+static rt_status ensure_split(rt_scene* s, int n) {
+    if (s->split_n == n && s->split) return RT_OK;
+    if (s->split) rt_multi_free(s->split);
+    s->split = nullptr;
+    s->split_n = 0;
+    s->split_dev_pending = false;
+    std::vector<int32_t> devs((size_t)n, s->device);
+    rt_status st = rt_multi_build(s, devs.data(), (uint32_t)n, false, &s->split);
+    if (st != RT_OK) return st;
+    const bool count = s->count_ops;
+    (void)rt_multi_each(s->split, [&](rt_scene* c) { return rt_scene_set_scan_counting(c, count); });
+    s->split_n = n;
+    s->split_dev_y = 0;
+    return RT_OK;
+}
+
+// rt_render's seam split in stream order (rt_multi.cpp rt_multi_render_frame_async): the
+// frame's top rows [0, rows) and the rest render side by side as two band shares of this
+// device -- rt_render's shares (s->split: this handle and one clone, each share on the
+// state's own stream; the same two streams as rt_render, since streams created later may
+// share a hardware queue: 5.4 vs 3.4 ms for a frame when they did) -- forked from and
+// joined back into `stream`.  The meeting row starts at the
+// even split and, whenever the previous call's share spans have already completed when the
+// next call is enqueued, moves 8 rows toward the share that finished first (within [half,
+// 3/4] of the frame); the shares' persistent grids take RT_SEAM_GRID_PCT (default 80) % of
+// the chip, or the scene's own share if smaller.  RT_SEAM_SPLIT=1 (or frames under 32 rows):
+// one pass on `stream`.  No pixel depends on any of it.
+rt_status rt_render_frame_async(const rt_scene* scene, const rt_camera* cam, uint32_t depth, float* d_rgb,
+                                uint8_t* d_rgb8, uint64_t* d_counters, void* stream) {
+    rt_scene* s = const_cast<rt_scene*>(scene);
+    if (!s || !cam || !d_rgb || cam->x_res == 0 || cam->y_res == 0) return RT_ERR_INVALID_ARG;
+    if (s->multi) return RT_ERR_UNSUPPORTED;  // a multi-device scene renders through rt_render
+    if (depth > RT_MAX_DEPTH) return RT_ERR_UNSUPPORTED;
+    if ((uint64_t)cam->x_res * cam->y_res * 3 >= (1ull << 32)) return RT_ERR_UNSUPPORTED;
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t hs = (hipStream_t)stream;
+    const uint32_t y = cam->y_res;
+    if (seam_split() != 2 || use_megakernel() || y < 32u) {
+        // one pass: one band of 8-row tiles holding every row, padded to a multiple of 8
+        const size_t n = (size_t)cam->x_res * y * 3;
+        const size_t n_pad = (size_t)cam->x_res * rt_band_rows_per_rank(y, 8, 1) * 3;
+        if (n_pad == n)
+            return rt_render_bands_ex_async(s, cam, 1, depth, 1, 0, 8, 0, 1, d_rgb, d_rgb8, d_counters, stream);
+        rt_status st = ensure_ws(s, n_pad, d_rgb8 ? n_pad : 0);
+        if (st != RT_OK) return st;
+        st = rt_render_bands_ex_async(s, cam, 1, depth, 1, 0, 8, 0, 1, s->ws.out, d_rgb8 ? s->ws.out8 : nullptr,
+                                      d_counters, stream);
+        if (st != RT_OK) return st;
+        HIP_TRY(hipMemcpyAsync(d_rgb, s->ws.out, n * sizeof(float), hipMemcpyDeviceToDevice, hs));
+        if (d_rgb8) HIP_TRY(hipMemcpyAsync(d_rgb8, s->ws.out8, n, hipMemcpyDeviceToDevice, hs));
+        return RT_OK;
+    }
+    rt_status st0 = ensure_split(s, 2);
+    if (st0 != RT_OK) return st0;
+    const uint32_t even = ((y + 1u) / 2u + 7u) / 8u * 8u;
+    const uint32_t hi = std::max(even, (y * 3u / 4u) / 8u * 8u);
+    if (s->split_dev_y != y || s->split_dev_rows < even || s->split_dev_rows > hi) {
+        s->split_dev_rows = even;
+        s->split_dev_y = y;
+        // both shares' node pools sized once for the largest share they can get (unless the
+        // RT_NODE_CAP test knob pins them)
+        const uint64_t floor = std::min<uint64_t>((uint64_t)hi * cam->x_res * node_factor(), pool_cap_limit(s));
+        if (!std::getenv("RT_NODE_CAP"))
+            (void)rt_multi_each_rank(s->split, [&](rt_scene* c) {
+                c->pool_floor = std::max<uint32_t>(c->pool_floor, (uint32_t)floor);
+                return RT_OK;
+            });
+    } else {
+        float t[2] = {0.f, 0.f};
+        if (rt_multi_async_share_ms(s->split, t, 2) == RT_OK && t[0] > 0.f && t[1] > 0.f) {
+            const float late = t[1] - t[0], band = 0.03f * t[1];  // > 0: share 0 can take more rows
+            if (late > band && s->split_dev_rows + 8u <= hi)
+                s->split_dev_rows += 8u;
+            else if (late < -band && s->split_dev_rows >= even + 8u)
+                s->split_dev_rows -= 8u;
+        }
+    }
+    const char* gp = std::getenv("RT_SEAM_GRID_PCT");
+    const int pct = std::min(s->grid_pct, gp ? std::max(1, std::min(100, std::atoi(gp))) : 80);
+    const int saved = s->grid_pct;  // read when the passes are enqueued: restored right after
+    auto set_pct = [&](int v) {
+        s->grid_pct = v;
+        (void)rt_multi_each(s->split, [&](rt_scene* c) {
+            c->grid_pct = v;
+            return RT_OK;
+        });
+    };
+    set_pct(pct);
+    rt_status st = rt_multi_render_frame_async(s->split, cam, depth, s->split_dev_rows, d_rgb, d_rgb8, d_counters, hs);
+    set_pct(saved);
+    if (st != RT_OK) return st;
+    s->split_dev_pending = true;
+    return RT_OK;
+}
+
 rt_status rt_scene_sync_status(rt_scene* s) {
+    if (!s) return RT_ERR_INVALID_ARG;
+    rt_status st = rt_scene_sync_own(s);
+    if (st != RT_OK && st != RT_ERR_CAPACITY) return st;
+    bool ovf = st == RT_ERR_CAPACITY || s->split_dev_overflow;
+    s->split_dev_overflow = false;
+    if (s->split && s->split_dev_pending) {  // rt_render_frame_async's other share
+        s->split_dev_pending = false;
+        rt_status e = rt_multi_each(s->split, [&](rt_scene* c) -> rt_status {
+            rt_status r = rt_scene_sync_own(c);
+            if (r == RT_ERR_CAPACITY) {
+                ovf = true;
+                return RT_OK;
+            }
+            return r;
+        });
+        if (e != RT_OK) return e;
+    }
+    return ovf ? RT_ERR_CAPACITY : RT_OK;
+}
+
+rt_status rt_scene_sync_own(rt_scene* s) {
     if (!s) return RT_ERR_INVALID_ARG;
     HIP_TRY(hipSetDevice(s->device));
     for (auto& se : s->ev_streams) HIP_TRY(hipEventSynchronize(se.second));
@@ -2342,15 +2466,18 @@ rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t de
     // 3 shares: 3.80, 4: 5.08).
     const int split = seam_split();
     if (split > 1 && !use_megakernel() && cam->y_res >= 16u * (uint32_t)split) {
-        if (s->split_n != split) {
-            if (s->split) rt_multi_free(s->split);
-            s->split = nullptr;
-            s->split_n = 0;
-            std::vector<int32_t> devs((size_t)split, s->device);
-            rt_status st = rt_multi_build(s, devs.data(), (uint32_t)split, false, &s->split);
-            if (st != RT_OK) return st;
-            s->split_n = split;
+        if (s->split_dev_pending) {
+            // a stream-ordered rt_render_frame_async on these shares is not reported yet: keep
+            // its overflow for the caller's rt_scene_sync_status (this render's own status
+            // checks below would otherwise consume it)
+            rt_status ps = rt_scene_sync_status(s);
+            if (ps == RT_ERR_CAPACITY)
+                s->split_dev_overflow = true;
+            else if (ps != RT_OK)
+                return ps;
         }
+        rt_status es = ensure_split(s, split);
+        if (es != RT_OK) return es;
         // contiguous shares by default (top / bottom halves: 3.47 ms against 3.69 with 8-row
         // bands dealt in turn -- shares of different content fall out of step, so one share's
         // level tails meet the other's work)
@@ -2654,6 +2781,7 @@ rt_status rt_scene_set_material(rt_scene* s, uint32_t index, const rt_material* 
     MatRec cur;
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    for (auto& se : s->ev_streams) HIP_TRY(hipEventSynchronize(se.second));  // renders on other streams
     HIP_TRY(hipMemcpy(&cur, s->S.mats + index, sizeof(cur), hipMemcpyDeviceToHost));
     if (m->kind != cur.kind) return RT_ERR_INVALID_ARG;  // the same kind, as the GUI's edits
     MatRec M;

@@ -3,6 +3,8 @@
 #pragma once
 #include <functional>
 
+#include <hip/hip_runtime.h>
+
 #include "../../include/rt_api.h"
 
 struct rt_multi_state;
@@ -29,3 +31,14 @@ rt_status rt_multi_share_ms(rt_multi_state* m, float* ms, uint32_t n);
 // ... and each rank's copy-out time (from its finish to its band in the caller's buffers)
 rt_status rt_multi_copy_ms(rt_multi_state* m, float* ms, uint32_t n);
 void rt_multi_free(rt_multi_state* m);
+// Every rank of a multi-device state, ranks[0] included.
+rt_status rt_multi_each_rank(rt_multi_state* m, const std::function<rt_status(rt_scene*)>& f);
+// rt_render_frame_async's two band shares on one device (rt_multi.cpp): share 0 = rows
+// [0, rows) straight into d_rgb, share 1 = rows [rows, y_res) through its band buffer;
+// fork from and join back into `stream`.  y_res / 2 <= rows < y_res.
+rt_status rt_multi_render_frame_async(rt_multi_state* m, const rt_camera* cam, uint32_t depth, uint32_t rows,
+                                      float* d_rgb, uint8_t* d_rgb8, uint64_t* d_counters, hipStream_t stream);
+// the previous rt_multi_render_frame_async's share spans once complete (never waits)
+rt_status rt_multi_async_share_ms(rt_multi_state* m, float* ms, uint32_t n);
+// rt_scene_sync_status of this handle's own workspace only (not its split shares)
+extern "C" rt_status rt_scene_sync_own(rt_scene* s);

@@ -248,7 +248,7 @@ rt_status rt_multi_render_state(rt_multi_state* m, const rt_camera* cam, uint32_
             // grown pool; the other slices are final
             bool overflow = false;
             for (uint32_t r = 0; r < world; r++) {
-                st = rt_scene_sync_status(m->ranks[r]);
+                st = rt_scene_sync_own(m->ranks[r]);
                 redo[r] = st == RT_ERR_CAPACITY;
                 if (redo[r])
                     overflow = true;
@@ -317,7 +317,7 @@ rt_status rt_multi_render_state(rt_multi_state* m, const rt_camera* cam, uint32_
         // exchange (a collective: every rank takes part) runs once more
         bool overflow = false;
         for (uint32_t r = 0; r < world; r++) {
-            st = rt_scene_sync_status(m->ranks[r]);
+            st = rt_scene_sync_own(m->ranks[r]);
             redo[r] = st == RT_ERR_CAPACITY;
             if (redo[r])
                 overflow = true;
@@ -332,6 +332,80 @@ rt_status rt_multi_render_state(rt_multi_state* m, const rt_camera* cam, uint32_
     if (rgb8) MHIP(hipMemcpyAsync(rgb8, m->frame8, ff, hipMemcpyDeviceToHost, s0));
     MHIP(hipStreamSynchronize(s0));
     return multi_finish(m, opts);
+}
+
+// rt_render_frame_async: the seam split, stream-ordered.  Two band shares of one device
+// (ranks[0], ranks[1]: rows [0, rows) and [rows, y_res)) fork from `stream`, render side by
+// side on their own streams and join back into it.  Share 0's band buffer IS the top of the
+// caller's frame (one band of `rows` rows, no padding: rows < y_res), so it renders straight
+// into d_rgb; share 1's last band is padded past y_res, so it renders into its own buffer and
+// one device copy moves its valid rows into place.  Counters of both shares add into
+// d_counters.  Nothing here waits on the host; the last call's share spans (ev0 -> done[r])
+// are read by the next call through rt_multi_async_share_ms once they have completed.
+rt_status rt_multi_render_frame_async(rt_multi_state* m, const rt_camera* cam, uint32_t depth, uint32_t rows,
+                                      float* d_rgb, uint8_t* d_rgb8, uint64_t* d_counters, hipStream_t stream) {
+    if (!m || m->rccl || m->ranks.size() != 2 || !cam || !d_rgb || rows == 0 || rows >= cam->y_res ||
+        2ull * rows < cam->y_res)
+        return RT_ERR_INVALID_ARG;
+    const uint32_t world = 2;
+    const size_t row_floats = (size_t)cam->x_res * 3u;
+    const size_t ff = (size_t)cam->y_res * row_floats;
+    rt_status st = ensure_buffers(m, ff, 0, d_rgb8 != nullptr);
+    if (st != RT_OK) return st;
+    m->band_rows = rows;
+    m->direct = true;
+    MHIP(hipSetDevice(m->devices[0]));
+    // Share 0 runs on the caller's stream itself and only share 1 forks (3.41 / 3.40 ms vs
+    // 3.52 / 3.85 with both shares forked onto the state's streams, config 3 at 1080p, on a
+    // created caller stream); RT_FRAME_FORK=streams forks both (A/B).  On the legacy null
+    // stream the fork and join measured 5.3 - 5.4 ms once other streams and rt_render's
+    // shares existed in the process: pass a created stream.
+    static const bool on_caller = [] {
+        const char* e = std::getenv("RT_FRAME_FORK");
+        return !(e && std::strcmp(e, "streams") == 0);
+    }();
+    MHIP(hipEventRecord(m->ev0, stream));
+    for (uint32_t r = 0; r < world; r++) {
+        hipStream_t rs = (r == 0 && on_caller) ? stream : m->streams[r];
+        if (rs != stream) MHIP(hipStreamWaitEvent(rs, m->ev0, 0));
+        float* out = r == 0 ? d_rgb : m->band[r];
+        uint8_t* out8 = d_rgb8 ? (r == 0 ? d_rgb8 : m->band8[r]) : nullptr;
+        st = rt_render_bands_ex_async(m->ranks[r], cam, 1, depth, 1, 0, rows, r, world, out, out8, d_counters, rs);
+        if (st != RT_OK) return st;
+        MHIP(hipEventRecord(m->done[r], rs));
+        if (r > 0) {
+            const size_t off = (size_t)rows * row_floats, len = (size_t)(cam->y_res - rows) * row_floats;
+            MHIP(hipMemcpyAsync(d_rgb + off, m->band[r], len * sizeof(float), hipMemcpyDeviceToDevice, rs));
+            if (d_rgb8) MHIP(hipMemcpyAsync(d_rgb8 + off, m->band8[r], len, hipMemcpyDeviceToDevice, rs));
+        }
+        if (rs != stream) {
+            MHIP(hipEventRecord(m->copied[r], rs));
+            MHIP(hipStreamWaitEvent(stream, m->copied[r], 0));
+        }
+    }
+    return RT_OK;
+}
+
+// The previous rt_multi_render_frame_async's share spans (ms from the fork to each share's
+// end), if they have completed; RT_ERR_UNSUPPORTED otherwise.  Never waits.
+rt_status rt_multi_async_share_ms(rt_multi_state* m, float* ms, uint32_t n) {
+    if (!m || !ms || n > m->ranks.size() || m->rccl || !m->direct) return RT_ERR_UNSUPPORTED;
+    if (hipSetDevice(m->devices[0]) != hipSuccess) return RT_ERR_HIP;
+    if (hipEventQuery(m->ev0) != hipSuccess) return RT_ERR_UNSUPPORTED;
+    for (uint32_t r = 0; r < n; r++) {
+        if (hipEventQuery(m->done[r]) != hipSuccess) return RT_ERR_UNSUPPORTED;
+        if (hipEventElapsedTime(&ms[r], m->ev0, m->done[r]) != hipSuccess) return RT_ERR_UNSUPPORTED;
+    }
+    return RT_OK;
+}
+
+// Every rank of `m` (ranks[0] included): f, first error wins.
+rt_status rt_multi_each_rank(rt_multi_state* m, const std::function<rt_status(rt_scene*)>& f) {
+    for (rt_scene* s : m->ranks) {
+        rt_status st = f(s);
+        if (st != RT_OK) return st;
+    }
+    return RT_OK;
 }
 
 // the render's counters (summed over the ranks) and span, for rt_render_opts

@@ -38,17 +38,21 @@ class FrameTiler:
     """Renders this rank's share of a frame and gathers the frame on rank 0."""
 
     def __init__(self, scene: DeviceScene, width, height, depth, band_rows=8, rank=0, world=1,
-                 device=None, spp=1, seed=0, batch=1, rgb8=False, force_gather=False):
+                 device=None, spp=1, seed=0, batch=1, rgb8=False, force_gather=False, split=False):
         """rgb8: render and gather only Color::as_u8 bytes (3 B per pixel instead of 12; the
         level-0 combine writes them, rt_render_bands_ex_async with no float buffer).
         force_gather: at world 1 too, assemble through the process group's gather and the
-        un-permute kernel (a one-rank communicator: runs the RCCL exchange on one GPU)."""
+        un-permute kernel (a one-rank communicator: runs the RCCL exchange on one GPU).
+        split: at world 1, single frames (batch 1, spp 1, f32) go through rt_render_frame_async
+        -- rt_render's two band shares side by side, stream-ordered -- instead of one pass
+        (render on a created torch stream, not the null stream: rt_api.h)."""
         self.scene = scene
         self.rgb8 = bool(rgb8) and spp == 1
         self.spp, self.seed = spp, seed
         self.w, self.h, self.depth = width, height, depth
         self.band_rows, self.rank, self.world = band_rows, rank, world
         self.gather = world > 1 or bool(force_gather)
+        self.split = bool(split) and not self.gather and spp == 1 and not self.rgb8 and int(batch) == 1
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.rpr = band_rows_per_rank(height, band_rows, world)
         assert self.rpr == band_rows_per_rank_py(height, band_rows, world)
@@ -84,6 +88,8 @@ class FrameTiler:
         if self.rgb8:
             self.scene.render_bands_ex_async(cams, self.depth, self.band_rows, self.rank, self.world, 0,
                                              self.locals.data_ptr(), self.counters.data_ptr(), stream)
+        elif n == 1 and self.split:  # the frame's rows land row-major at the buffer's start
+            self.scene.render_frame_async(cams[0], self.depth, self.local.data_ptr(), self.counters.data_ptr(), stream)
         elif n == 1:
             self.scene.render_bands_async(cams[0], self.depth, self.band_rows, self.rank, self.world,
                                           self.local.data_ptr(), self.counters.data_ptr(), stream,
