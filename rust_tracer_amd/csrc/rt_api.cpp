@@ -35,11 +35,13 @@ hipError_t launch_unpermute_u8(const uint8_t* in, uint32_t x_res, uint32_t y_res
                                uint32_t world, uint32_t rows_per_rank, uint8_t* out, hipStream_t stream,
                                uint32_t frames = 1, uint32_t rank_rows = 0);
 bool rt_cube_table_check(const float* table);
-hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_blocks, int* combine_blocks);
+hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_blocks, int* combine_blocks,
+                          int* trace_each);
 hipError_t launch_wave_shadow(const WaveParams& p, int blocks, hipStream_t stream);
 hipError_t launch_wave_init(uint32_t* levels, uint32_t n_words, uint32_t total_items, uint32_t* overflow,
                             hipStream_t stream);
-hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream);
+hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream,
+                             const int* occ_each = nullptr, int occ_min = 0);
 hipError_t launch_wave_combine(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream);
 hipError_t launch_forest_shade(const WaveParams& p, uint32_t level, int blocks, float* frame, hipStream_t stream);
 hipError_t launch_forest_mark(const uint32_t* node_key, const uint32_t* node_pixel, const uint32_t* node_flags,
@@ -1147,6 +1149,7 @@ struct rt_scene {
     int num_cus = 256;
     int occ[3] = {0, 0, 0};  // blocks per CU for the MAXF 7 / 15 / 63 variants
     int occ_trace = 0, occ_shadow = 0, occ_combine = 0;
+    int occ_trace_each[3] = {0, 0, 0};  // generic / level-0 / deep trace instantiations
     bool count_ops = false;  // rt_scene_set_scan_counting
     int grid_pct = 100;      // rt_scene_set_grid_share: % of a full chip for persistent grids
     Workspace ws;
@@ -2083,7 +2086,7 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     }
     if (s->occ_trace == 0) {
         int a = 0, b = 0, c = 0;
-        HIP_TRY(wave_occupancy(p, &a, &b, &c));
+        HIP_TRY(wave_occupancy(p, &a, &b, &c, s->occ_trace_each));
         s->occ_trace = a > 0 ? a : 1;
         s->occ_shadow = b > 0 ? b : 1;
         s->occ_combine = c > 0 ? c : 1;
@@ -2118,7 +2121,7 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     // enqueued without a host round trip (levels past the deepest non-empty one are no-ops).
     HIP_TRY(launch_wave_init(w.levels, RT_LEVEL_TABLE_WORDS, p.total_items, sample == 0 ? w.overflow : nullptr,
                              stream));
-    HIP_TRY(launch_wave_trace(p, 0, tb, stream));
+    HIP_TRY(launch_wave_trace(p, 0, tb, stream, s->occ_trace_each, s->occ_trace));
     // RT_SORT_LEVELS: bit k set = level k's queue is sorted (A/B; default every level)
     const char* sl = std::getenv("RT_SORT_LEVELS");
     const uint64_t sort_levels = sl ? std::strtoull(sl, nullptr, 0) : ~0ull;
@@ -2141,7 +2144,7 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
                                     w.perm, tile_counts, digit_totals, 4 * s->num_cus, stream, sort_digit));
             p.perm = w.perm;
         }
-        HIP_TRY(launch_wave_trace(p, k, tb, stream));
+        HIP_TRY(launch_wave_trace(p, k, tb, stream, s->occ_trace_each, s->occ_trace));
     }
     if (sort_shadow) {
         for (int r = 0; r < dup_sort; r++)

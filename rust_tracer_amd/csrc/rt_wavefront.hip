@@ -373,8 +373,11 @@ extern __shared__ float4 rt_dyn_lds[];
 #ifndef RT_DEEP_WAVES
 #define RT_DEEP_WAVES RT_TRACE_WAVES
 #endif
+#ifndef RT_FIRST_WAVES
+#define RT_FIRST_WAVES RT_TRACE_WAVES  // level 0's instantiation (A/B builds: -DRT_FIRST_WAVES=4)
+#endif
 template <bool COUNT, bool LDS, bool DEEP = false, bool FIRST = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_DEEP_WAVES : RT_TRACE_WAVES, 8))) void trace_level_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_DEEP_WAVES : (FIRST ? RT_FIRST_WAVES : RT_TRACE_WAVES), 8))) void trace_level_kernel(
     WaveParams P, uint32_t level) {
     const DevScene& S = P.S;
     if (LDS) {  // stage the hierarchy's node records in LDS
@@ -1143,7 +1146,8 @@ static bool lds_nodes_for(const WaveParams& p, const char* kernel) {
 
 // Blocks per CU of the instantiations that launch: the LDS variants at the scene's LDS
 // bytes (the persistent grids are sized from these, so that every block is resident)
-hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_blocks, int* combine_blocks) {
+hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_blocks, int* combine_blocks,
+                          int* trace_each) {
     const size_t lds = lds_bytes(p);
     const bool aware = !getenv("RT_OCC_NOLDS");  // A/B: size the grids as if no LDS were used
     // every trace instantiation launch_wave_trace may pick (generic, level 0, deep levels):
@@ -1161,6 +1165,8 @@ hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_bl
            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&tv[2], trace_level_kernel<false, false, true>, 256, 0);
     if (e != hipSuccess) return e;
     *trace_blocks = std::min(tv[0], std::min(tv[1], tv[2]));
+    if (trace_each)
+        for (int i = 0; i < 3; i++) trace_each[i] = tv[i];
     e = aware && lds_nodes_for(p, "shadow")
             ? hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<true, false>, 256, lds)
             : hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<false, false>, 256, 0);
@@ -1172,12 +1178,20 @@ hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_bl
     return e;
 }
 
-hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream) {
+// occ_each (optional): blocks per CU of the generic / level-0 / deep instantiations, occ_min
+// their least (what `blocks` was sized by): a launch of an instantiation with more resident
+// blocks per CU gets its grid scaled up to match (identical grids when they agree)
+hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream,
+                             const int* occ_each, int occ_min) {
     const size_t lds = lds_bytes(p);
     const bool use = lds_nodes_for(p, "trace");
     // the deep instantiation past level 0 and the inline shadow levels (RT_DEEP_KERNEL=0: never, A/B)
     static const bool deep_ok = !(getenv("RT_DEEP_KERNEL") && getenv("RT_DEEP_KERNEL")[0] == '0');
     const bool deep = deep_ok && level > 0 && level >= p.inline_levels && !(p.count_mask & 1u);
+    if (occ_each && occ_min > 0 && !(p.count_mask & 1u)) {
+        const int v = (level == 0 && deep_ok) ? 1 : (deep ? 2 : 0);
+        if (occ_each[v] > occ_min) blocks = (int)((long long)blocks * occ_each[v] / occ_min);
+    }
     if (p.count_mask & 1u) {
         if (use)
             hipLaunchKernelGGL((trace_level_kernel<true, true>), dim3(blocks), dim3(256), lds, stream, p, level);
