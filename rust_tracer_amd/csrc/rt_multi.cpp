@@ -91,6 +91,7 @@ struct rt_multi_state {
     std::vector<ncclComm_t> comms;
     uint32_t band_rows = 8;                  // rows per band (block-cyclic over the ranks)
     bool direct = false;                     // the last render copied each rank's one band straight out
+    bool frame_async = false;                // rt_multi_render_frame_async ran (done[0] marks its share 0)
 };
 
 rt_status rt_multi_each(rt_multi_state* m, const std::function<rt_status(rt_scene*)>& f) {
@@ -364,6 +365,10 @@ rt_status rt_multi_render_frame_async(rt_multi_state* m, const rt_camera* cam, u
         const char* e = std::getenv("RT_FRAME_FORK");
         return !(e && std::strcmp(e, "streams") == 0);
     }();
+    // share 0 renders on rank 0's workspace: after the previous call's share 0, whatever
+    // stream that call came from (share 1 is ordered by the state's own stream)
+    if (on_caller && m->frame_async) MHIP(hipStreamWaitEvent(stream, m->done[0], 0));
+    m->frame_async = true;
     MHIP(hipEventRecord(m->ev0, stream));
     for (uint32_t r = 0; r < world; r++) {
         hipStream_t rs = (r == 0 && on_caller) ? stream : m->streams[r];
