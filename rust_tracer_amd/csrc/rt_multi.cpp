@@ -356,14 +356,15 @@ rt_status rt_multi_render_frame_async(rt_multi_state* m, const rt_camera* cam, u
     m->band_rows = rows;
     m->direct = true;
     MHIP(hipSetDevice(m->devices[0]));
-    // Share 0 runs on the caller's stream itself and only share 1 forks (3.41 / 3.40 ms vs
-    // 3.52 / 3.85 with both shares forked onto the state's streams, config 3 at 1080p, on a
-    // created caller stream); RT_FRAME_FORK=streams forks both (A/B).  On the legacy null
-    // stream the fork and join measured 5.3 - 5.4 ms once other streams and rt_render's
-    // shares existed in the process: pass a created stream.
+    // Both shares fork onto the state's streams (share r always on streams[r], so calls from
+    // any caller streams stay ordered on each share's workspace).  RT_FRAME_FORK=caller (A/B):
+    // share 0 on the caller's stream itself, only share 1 forked -- 3.41 / 3.40 ms vs 3.52 /
+    // 3.85, config 3 at 1080p on a created caller stream.  On the legacy null stream the fork
+    // and join measured 5.3 - 5.4 ms once other streams and rt_render's shares existed in the
+    // process: pass a created stream.
     static const bool on_caller = [] {
         const char* e = std::getenv("RT_FRAME_FORK");
-        return !(e && std::strcmp(e, "streams") == 0);
+        return e && std::strcmp(e, "caller") == 0;
     }();
     // share 0 renders on rank 0's workspace: after the previous call's share 0, whatever
     // stream that call came from (share 1 is ordered by the state's own stream)

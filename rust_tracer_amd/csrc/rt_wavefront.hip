@@ -1179,8 +1179,8 @@ hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_bl
 }
 
 // occ_each (optional): blocks per CU of the generic / level-0 / deep instantiations, occ_min
-// their least (what `blocks` was sized by): a launch of an instantiation with more resident
-// blocks per CU gets its grid scaled up to match (identical grids when they agree)
+// their least (what `blocks` was sized by): with RT_OCC_EACH=1 a launch of an instantiation
+// with more resident blocks per CU gets its grid scaled up to match
 hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream,
                              const int* occ_each, int occ_min) {
     const size_t lds = lds_bytes(p);
@@ -1188,7 +1188,9 @@ hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hi
     // the deep instantiation past level 0 and the inline shadow levels (RT_DEEP_KERNEL=0: never, A/B)
     static const bool deep_ok = !(getenv("RT_DEEP_KERNEL") && getenv("RT_DEEP_KERNEL")[0] == '0');
     const bool deep = deep_ok && level > 0 && level >= p.inline_levels && !(p.count_mask & 1u);
-    if (occ_each && occ_min > 0 && !(p.count_mask & 1u)) {
+    // RT_OCC_EACH=1 (A/B builds whose instantiations differ in occupancy, e.g. RT_FIRST_WAVES)
+    static const bool occ_each_on = getenv("RT_OCC_EACH") && getenv("RT_OCC_EACH")[0] == '1';
+    if (occ_each_on && occ_each && occ_min > 0 && !(p.count_mask & 1u)) {
         const int v = (level == 0 && deep_ok) ? 1 : (deep ? 2 : 0);
         if (occ_each[v] > occ_min) blocks = (int)((long long)blocks * occ_each[v] / occ_min);
     }

@@ -6,6 +6,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 V=rust_tracer_amd/librt_hip_first4.so
+export RT_OCC_EACH=1
 RT_LIB=$V timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
   tests/test_gpu_fullframe.py tests/test_gpu_parity.py > gpurun_out/r3ab25_tests.txt 2>&1 || exit 1
 O=gpurun_out/r3ab25_frame.jsonl
