@@ -157,6 +157,15 @@ typedef struct rt_scene rt_scene;
  * scene build time (Matrix::inverse, Plane axes, Triangle normals, Cube triangles) and
  * uploads the scene to `device` (-1 = current). */
 rt_status rt_scene_create(const rt_scene_desc* desc, int32_t device, rt_scene** out);
+/* rt_scene_create with explicit tuning: "key=value" pairs separated by ',' (the keys of
+ * rust_tracer_amd/csrc/rt_tune.hpp, e.g. "lb_res=0,bvh=0").  Every key is exact -- it moves
+ * time, never a pixel.  A handle's tuning is the defaults, then the environment's RT_TUNE
+ * (same syntax; the library's only environment read), then `tuning`; clones copy it.  An
+ * unknown key or a bad value is RT_ERR_INVALID_ARG.  tuning == NULL is rt_scene_create. */
+rt_status rt_scene_create_tuned(const rt_scene_desc* desc, int32_t device, const char* tuning, rt_scene** out);
+/* Changes the per-pass keys of rt_tune.hpp on a handle (and its band shares / devices);
+ * scene-build keys are RT_ERR_INVALID_ARG here.  Not while a render of the handle runs. */
+rt_status rt_scene_set_tuning(rt_scene* scene, const char* tuning);
 rt_status rt_scene_destroy(rt_scene* scene);
 
 /* Page-locked host memory for a caller's frame buffer (the RenderBuffer a render() caller
@@ -178,19 +187,13 @@ rt_status rt_scene_clone(const rt_scene* src, int32_t device, rt_scene** out);
  * on devices[0] with RCCL (ncclGather over xGMI, communicators from ncclCommInitAll) and
  * un-permute them there before the copy to the caller's buffers.  The result equals the
  * one-device rt_render bit for bit (pixels are independent).  n_devices == 1 is
- * rt_scene_create, unless the environment sets RT_FORCE_RCCL=1: then the one device gets a
+ * rt_scene_create, unless the handle's tuning sets force_rccl=1 (RT_TUNE): then the one device gets a
  * one-rank RCCL communicator and renders go through the same band render, ncclGather and
  * un-permute as n > 1 (a one-GPU machine runs the RCCL exchange this way).  A device listed twice shares that GPU between two band shares, which
  * then exchange bands by device copies (RCCL puts one rank per device; a test
  * configuration).  The stream-ordered entry points act on devices[0] only. */
 rt_status rt_scene_create_multi(const rt_scene_desc* desc, const int32_t* devices, uint32_t n_devices,
                                 rt_scene** out);
-/* The specular power function of the device path (rt_powf.hpp: glibc's powf evaluation,
- * bit-identical to the libm powf the reference's f32::powf calls, material.rs:211), over
- * arrays -- verification hooks: rt_powf_batch_async on the device (d_* device pointers,
- * stream-ordered), rt_powf_batch_host the same code compiled for the host. */
-rt_status rt_powf_batch_async(const float* d_x, const float* d_y, float* d_out, uint64_t n, void* stream);
-rt_status rt_powf_batch_host(const float* x, const float* y, float* out, uint64_t n);
 
 /* Device bytes the scene's render workspace holds now (node pool, ray and shadow queues,
  * sort buffers, frame buffers of rt_render): it grows with the largest pass rendered so far
@@ -348,8 +351,8 @@ uint64_t rt_scene_device_bytes(const rt_scene* scene);
 rt_status rt_scene_scan_ops(rt_scene* scene, uint64_t* out, uint32_t n, int32_t reset);
 
 /* Counting is instrumentation: renders after rt_scene_set_scan_counting(scene, 1) run
- * the counting variants of the level-synchronous kernels (the per-pixel megakernel
- * always counts); the default (0) runs uncounted kernels.  Frames are identical. */
+ * the counting variants of the level-synchronous kernels; the default (0) runs uncounted
+ * kernels.  Frames are identical.  (bench.py's roofline: one untimed counting frame.) */
 rt_status rt_scene_set_scan_counting(rt_scene* scene, int32_t enable);
 
 /* Frames in flight: the share (percent, 1..100, default 100) of a full chip that one
@@ -358,8 +361,8 @@ rt_status rt_scene_set_scan_counting(rt_scene* scene, int32_t enable);
  * FramePipeline: 75 with 4 passes in flight).  Results do not change. */
 rt_status rt_scene_set_grid_share(rt_scene* scene, int32_t percent);
 
-/* 1 if the scene's scans walk the culling hierarchy (the default; RT_BVH=0 in the
- * environment at rt_scene_create turns it off), 0 if they test every shape. */
+/* 1 if the scene's scans walk the culling hierarchy (the default; tuning "bvh=0" at
+ * creation turns it off), 0 if they test every shape. */
 int32_t rt_scene_uses_bvh(const rt_scene* scene);
 
 /* ---- ray forest (src/render_tree.rs) -------------------------------------------------

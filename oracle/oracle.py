@@ -57,6 +57,7 @@ def lib():
     L.oracle_scene_set_material.argtypes = [vp, C.c_uint32, P(abi.rt_material)]
     L.oracle_as_u8.argtypes = [fa, C.c_uint64, P(C.c_uint8)]
     L.oracle_powf_batch.argtypes = [fa, fa, fa, C.c_uint64]
+    L.oracle_libm_batch.argtypes = [C.c_int, fa, fa, fa, C.c_uint64]
     for n in ("identity",):
         getattr(L, "oracle_matrix_" + n).argtypes = [fa]
     for n in ("scale", "translate"):
@@ -199,4 +200,18 @@ def powf(x, y):
     out = np.empty_like(x)
     fp = C.POINTER(C.c_float)
     lib().oracle_powf_batch(x.ctypes.data_as(fp), y.ctypes.data_as(fp), out.ctypes.data_as(fp), x.size)
+    return out
+
+
+LIBM_FN = {"powf": 0, "atan2f": 1, "acosf": 2, "atanf": 3}
+
+
+def libm(fn, x, y=None):
+    """The host libm's powf / atan2f(x, y) / acosf / atanf elementwise over float32 arrays
+    (the functions the reference's f32 methods call)."""
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.ascontiguousarray(y if y is not None else np.zeros_like(x), np.float32)
+    out = np.empty_like(x)
+    fp = C.POINTER(C.c_float)
+    lib().oracle_libm_batch(LIBM_FN[fn], x.ctypes.data_as(fp), y.ctypes.data_as(fp), out.ctypes.data_as(fp), x.size)
     return out

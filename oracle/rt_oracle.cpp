@@ -1107,6 +1107,13 @@ void oracle_powf_batch(const float* x, const float* y, float* out, uint64_t n) {
     for (uint64_t i = 0; i < n; i++) out[i] = powf(x[i], y[i]);
 }
 
+// the reference's other libm calls (sphere.rs:40-45: f32::atan2 / f32::acos; atanf, which
+// atan2f reduces to): fn 1 = atan2f(x[i], y[i]), 2 = acosf(x[i]), 3 = atanf(x[i])
+void oracle_libm_batch(int fn, const float* x, const float* y, float* out, uint64_t n) {
+    for (uint64_t i = 0; i < n; i++)
+        out[i] = fn == 0 ? powf(x[i], y[i]) : fn == 1 ? atan2f(x[i], y[i]) : fn == 2 ? acosf(x[i]) : atanf(x[i]);
+}
+
 void oracle_as_u8(const float* rgb, uint64_t n, uint8_t* out) {
     for (uint64_t k = 0; k < n; k++) out[k] = sat_u8(255.f * rgb[k]);
 }

@@ -238,23 +238,40 @@ class SceneDesc:
             self._owned_ptr = None
 
 
+def tuning_spec(tuning):
+    """bytes for the C ABI from None, "k=v,..." or {k: v}."""
+    if tuning is None:
+        return None
+    if isinstance(tuning, dict):
+        tuning = ",".join(f"{k}={v}" for k, v in tuning.items())
+    return tuning.encode()
+
+
 class DeviceScene:
     """An uploaded scene (rt_scene_create) on one HIP device, or -- `devices` a list --
     replicated over several (rt_scene_create_multi: render() then tiles the frame across
     them and gathers it over RCCL, from this one thread)."""
 
-    def __init__(self, desc, device=-1, devices=None, _handle=None):
+    def __init__(self, desc, device=-1, devices=None, tuning=None, _handle=None):
+        """tuning: "key=value,..." of rust_tracer_amd/csrc/rt_tune.hpp (rt_scene_create_tuned;
+        every key is exact -- it moves time, never a pixel), or a dict of them."""
         self._L = lib()
         self.h = C.c_void_p()
         self.desc = desc
         if _handle is not None:
             self.h = _handle
         elif devices is not None:
+            assert tuning is None, "multi-device scenes take their tuning from RT_TUNE"
             arr = (C.c_int32 * len(devices))(*devices)
             check(self._L.rt_scene_create_multi(desc.ptr(), arr, len(devices), C.byref(self.h)),
                   "rt_scene_create_multi")
         else:
-            check(self._L.rt_scene_create(desc.ptr(), device, C.byref(self.h)), "rt_scene_create")
+            check(self._L.rt_scene_create_tuned(desc.ptr(), device, tuning_spec(tuning), C.byref(self.h)),
+                  "rt_scene_create_tuned")
+
+    def set_tuning(self, tuning):
+        """rt_scene_set_tuning: change per-pass keys of rt_tune.hpp (string or dict)."""
+        check(self._L.rt_scene_set_tuning(self.h, tuning_spec(tuning)), "rt_scene_set_tuning")
 
     def clone(self, device=-1):
         """rt_scene_clone: another handle of this scene (own workspace and stream), copied on
@@ -459,29 +476,37 @@ class DeviceForest:
                 "p95": at(0.95), "p99": at(0.99)}
 
 
-class HostFrame:
-    """A float32 [h, w, 3] frame in page-locked host memory (rt_host_alloc): rt_render's
-    device-to-host copy into it runs at the link's DMA rate."""
+class _PinnedBuffer:
+    """rt_host_alloc'd bytes exposed through the array interface: every numpy view of it keeps
+    this object (and so the page-locked allocation) alive; the last view to go frees it."""
 
-    def __init__(self, w, h):
+    def __init__(self, nbytes):
         self._L = lib()
         self.ptr = C.c_void_p()
-        n = w * h * 3 * 4
-        check(self._L.rt_host_alloc(n, C.byref(self.ptr)), "rt_host_alloc")
-        buf = (C.c_uint8 * n).from_address(self.ptr.value)
-        self.array = np.frombuffer(buf, dtype=np.float32).reshape(h, w, 3)
-
-    def close(self):
-        if self.ptr:
-            self.array = None
-            self._L.rt_host_free(self.ptr)
-            self.ptr = C.c_void_p()
+        check(self._L.rt_host_alloc(nbytes, C.byref(self.ptr)), "rt_host_alloc")
+        self.__array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (self.ptr.value, False),
+                                    "version": 3}
 
     def __del__(self):
         try:
-            self.close()
+            if self.ptr:
+                self._L.rt_host_free(self.ptr)
+                self.ptr = C.c_void_p()
         except Exception:
             pass
+
+
+class HostFrame:
+    """A float32 [h, w, 3] frame in page-locked host memory (rt_host_alloc): rt_render's
+    device-to-host copy into it runs at the link's DMA rate.  The allocation lives as long as
+    any array view of it (``HostFrame(w, h).array`` alone is safe); close() drops this
+    object's own reference."""
+
+    def __init__(self, w, h):
+        self.array = np.asarray(_PinnedBuffer(w * h * 3 * 4)).view(np.float32).reshape(h, w, 3)
+
+    def close(self):
+        self.array = None
 
 
 def write_image(path, rgb8):

@@ -16,6 +16,8 @@ STATUS_NAMES = {
     3: "RT_ERR_UNSUPPORTED", 4: "RT_ERR_NO_DEVICE", 5: "RT_ERR_HIP",
     6: "RT_ERR_OUT_OF_MEMORY", 7: "RT_ERR_BAD_MATERIAL", 8: "RT_ERR_CAPACITY",
 }
+RT_ERR_INVALID_ARG = 1
+RT_ERR_NO_DEVICE = 4
 RT_ERR_CAPACITY = 8
 RT_MAX_DEPTH = 1024
 
@@ -116,6 +118,8 @@ def lib():
     P = C.POINTER
     vp = C.c_void_p
     L.rt_scene_create.argtypes = [P(rt_scene_desc), C.c_int32, P(vp)]
+    L.rt_scene_create_tuned.argtypes = [P(rt_scene_desc), C.c_int32, C.c_char_p, P(vp)]
+    L.rt_scene_set_tuning.argtypes = [vp, C.c_char_p]
     L.rt_scene_destroy.argtypes = [vp]
     L.rt_render.argtypes = [vp, P(rt_camera), C.c_uint32, P(rt_render_opts),
                             P(C.c_float), P(C.c_uint8)]
@@ -150,8 +154,6 @@ def lib():
     L.rt_scene_device_bytes.argtypes = [vp]
     L.rt_scene_device_bytes.restype = C.c_uint64
     L.rt_scene_workspace_bytes.argtypes = [vp]
-    L.rt_powf_batch_async.argtypes = [vp, vp, vp, C.c_uint64, vp]
-    L.rt_powf_batch_host.argtypes = [vp, vp, vp, C.c_uint64]
     L.rt_host_alloc.argtypes = [C.c_uint64, C.POINTER(vp)]
     L.rt_host_free.argtypes = [vp]
     L.rt_scene_workspace_bytes.restype = C.c_uint64

@@ -4,8 +4,9 @@
 // preprocessing the reference performs in its constructors and set_transform calls
 // (Matrix::inverse matrix.rs:99-153, Plane::new axes plane.rs:22-42, Triangle::new
 // normal triangle.rs:16-39, Cube::new triangles cube.rs:21-77), lay the result out as
-// the device runs of rt_device.hpp and upload it.  Rendering launches the megakernel of
-// rt_kernels.hip; there is no CPU fallback anywhere in this library.
+// the device runs of rt_device.hpp and upload it.  Rendering launches the level-synchronous
+// pipeline of rt_wavefront.hip (trace / shadow / combine) with the queue sorts of
+// rt_order.hip; there is no CPU fallback anywhere in this library.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -23,10 +24,9 @@
 #include "rt_bvh.hpp"
 #include "rt_device.hpp"
 #include "rt_internal.hpp"
+#include "rt_tune.hpp"
 
 namespace rtdev {
-hipError_t launch_render(const RenderParams& p, int blocks, hipStream_t stream);
-hipError_t render_occupancy(uint32_t depth, int* blocks_per_cu);
 hipError_t launch_unpermute(const float* in, uint32_t x_res, uint32_t y_res, uint32_t band_rows,
                             uint32_t world, uint32_t rows_per_rank, float* out, hipStream_t stream,
                             uint32_t frames = 1, uint32_t rank_rows = 0);
@@ -240,11 +240,6 @@ struct RunLayout {
     float c[3] = {0, 0, 0}, r = 0, g2 = 0, g1 = 0, g0 = 0, m1 = 0, m0 = 0;
 };
 
-// RT_BVH=0 turns the hierarchy off (every shape in the linear pass): A/B parity tests.
-bool bvh_enabled() {
-    const char* e = std::getenv("RT_BVH");
-    return !(e && std::strcmp(e, "0") == 0);
-}
 
 // Safety factors over the largest ratios tools/cull_bounds_check.py measures for each
 // bound (sphere 0.43, cube 1.83; triangles: the reported hit point's distance
@@ -261,12 +256,7 @@ const double FEPS = (double)std::numeric_limits<float>::epsilon();
 // rest are covered by its box grown by SAFETY_TRI eps (...) / (sin(alpha) sin(phi_T)).
 // GRAZE_K trades the grazing band's width against that growth (RT_GRAZE_K overrides).
 constexpr double GRAZE_MIN = 2e-4, GRAZE_MAX = 0.05;
-double graze_sin(double sin_a) {
-    const char* e = std::getenv("RT_GRAZE_K");
-    double k = e ? std::atof(e) : 1e-3;
-    if (!(k > 0)) k = 1e-3;
-    return std::min(GRAZE_MAX, std::max(GRAZE_MIN, k / sin_a));
-}
+double graze_sin(double sin_a, double k) { return std::min(GRAZE_MAX, std::max(GRAZE_MIN, k / sin_a)); }
 
 float down_f(double x) {
     float f = (float)x;
@@ -390,7 +380,7 @@ void emit_cube(std::vector<float>& v, const CubeIn& A, float lf, float sn) {
 static void lb_face_dir(int f, double a, double b, double out[3]);
 
 void build_graze(const std::vector<TriIn>& tris, const std::vector<char>& in_tri, const std::vector<double>& gsin,
-                 RunLayout& L) {
+                 RunLayout& L, const Tune& tn) {
     struct G {
         const TriIn* t;
         double n[3];
@@ -481,8 +471,7 @@ void build_graze(const std::vector<TriIn>& tris, const std::vector<char>& in_tri
     // a cell when a direction within the cell's angular radius rc (+1e-4) of its centre
     // can meet one of its triangles' planes at sin(phi) < 1.01 sin(phi_T): |c.n| <=
     // sin(asin(1.01 s) + rc + 1e-4).  Exact superset of the per-lane test.
-    const char* ge = std::getenv("RT_GRAZE_RES");
-    const int R = ge ? std::atoi(ge) : 64;
+    const int R = tn.graze_res;
     const size_t npairs = L.graze_pn.size() / 8;
     if (R > 0 && R <= 256 && npairs > 0 && npairs <= 256) {
         const uint32_t W = (uint32_t)((npairs + 31) / 32);
@@ -564,11 +553,9 @@ static void lb_face_dir(int f, double a, double b, double out[3]) {
     for (int i = 0; i < 3; i++) out[i] /= l;
 }
 
-void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, LightBuffers& B) {
-    const char* e = std::getenv("RT_LB_RES");  // cells per face side; 0: no light buffers (A/B)
-    const int R = e ? std::atoi(e) : 48;
-    const char* re = std::getenv("RT_LB_REACH");  // "0": runs are never cut at the reach (A/B)
-    const bool reach_cut = !(re && re[0] == '0');
+void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, LightBuffers& B, const Tune& T) {
+    const int R = T.lb_res;  // cells per face side; 0: no light buffers (A/B)
+    const bool reach_cut = T.lb_reach != 0;  // 0: runs are never cut at the reach (A/B)
     B.base.assign(lights.size(), 0xFFFFFFFFu);
     if (!L.use || R <= 0 || R > 1024 || L.lb_prims.empty()) return;
     B.res = (uint32_t)R;
@@ -716,9 +703,8 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
 // are copies of the records of every such Q (S itself included); a lane whose check passes
 // tests it instead of walking the hierarchy.  Spheres whose list would exceed 96 records
 // get no buffer.
-void build_shape_buffers(RunLayout& L, std::vector<ShapeRec>& shapes) {
-    const char* e = std::getenv("RT_SHAPE_BUF");  // "0": off (A/B)
-    if ((e && e[0] == '0') || !L.use || L.lb_prims.empty()) return;
+void build_shape_buffers(RunLayout& L, std::vector<ShapeRec>& shapes, const Tune& T) {
+    if (!T.shape_buf || !L.use || L.lb_prims.empty()) return;
     const double dmax = 3.0 * (double)L.r;
     const double hmax = ((double)L.g2 * dmax + (double)L.g1) * dmax + (double)L.g0;
     for (const LbPrim& P : L.lb_prims) {
@@ -742,8 +728,10 @@ void build_shape_buffers(RunLayout& L, std::vector<ShapeRec>& shapes) {
                 n_rec++;
             }
         }
+#if RT_DIAG
         if (std::getenv("RT_DEBUG_SHAPE_BUF"))
             std::fprintf(stderr, "shape %u r %.4f rc %.4f hmax %.5f records %zu\n", P.shape, P.r, (double)rc, hmax, n_rec);
+#endif
         if (n_rec == 0 || n_rec > 96) continue;
         uint32_t rec[8];
         auto copy = [&](std::vector<float>& run, size_t width, const std::vector<uint32_t>& recs, uint32_t* range) {
@@ -769,7 +757,8 @@ void build_shape_buffers(RunLayout& L, std::vector<ShapeRec>& shapes) {
 }
 
 void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, const std::vector<CubeIn>& cubes,
-                bool enable, RunLayout& L) {
+                const Tune& tn, RunLayout& L) {
+    const bool enable = tn.bvh != 0;
     using namespace rtbvh;
     std::vector<Prim> prims;
     std::vector<Geo> geo;
@@ -801,8 +790,7 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
             prims.push_back(p);
             geo.push_back(g);
         }
-        const char* bt_env = std::getenv("RT_BVH_TRIS");  // "0": loose triangles stay linear (A/B)
-        const bool tris_in_bvh = !(bt_env && bt_env[0] == '0');
+        const bool tris_in_bvh = tn.bvh_tris != 0;  // 0: loose triangles stay linear (A/B)
         for (size_t i = 0; i < tris.size() && tris_in_bvh; i++) {
             const TriIn& t = tris[i];
             double v[3][3] = {{t.v[0].x, t.v[0].y, t.v[0].z}, {t.v[1].x, t.v[1].y, t.v[1].z},
@@ -836,7 +824,7 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
             // the reported hit point lies within rho eps (...) / (sin(alpha) sin(phi)) of the
             // triangle and on the ray, so for sin(phi) >= sin(phi_T) the box grown by that
             // bound contains it: no t-margin needed
-            double gs = graze_sin(sin_a);
+            double gs = graze_sin(sin_a, tn.graze_k);
             double k = SAFETY_TRI * FEPS / sin_a * std::max(1.0 / gs, TRI_STEEP);
             double v0n = std::sqrt(v[0][0] * v[0][0] + v[0][1] * v[0][1] + v[0][2] * v[0][2]);
             double e = std::max(l1, l2) + v0n;
@@ -873,7 +861,7 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
             geo.push_back(g);
         }
     }
-    Tree T = build(prims);
+    Tree T = build(prims, tn.bvh_cnode, (size_t)tn.bvh_maxleaf);
     L.use = !prims.empty();
     if (L.use) {
         // scene ball (C, R) around every hierarchy primitive's ball
@@ -887,6 +875,7 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
         }
         R *= 1 + 1e-6;
         double g2 = 0, g1 = 0, g0 = 0, m1 = 0, m0 = 0;
+#if RT_DIAG
         if (const char* ss = std::getenv("RT_DEBUG_SPH_SCALE")) {  // measurement only: NOT conservative
             const double k = std::atof(ss);
             for (size_t i = 0; i < coef.size(); i++)
@@ -906,6 +895,7 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
                     coef[i].cC *= k;
                 }
         }
+#endif
         for (const Coef& c : coef) {
             g2 = std::max(g2, c.a2);
             g1 = std::max(g1, c.a1);
@@ -917,6 +907,7 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
         L.m0 = up_f(m0 * (1 + 1e-6));
         g1 += SAFETY_SLAB * 16.0 * FEPS;
         g0 += SAFETY_SLAB * 8.0 * FEPS * (3.0 * Cn + R);
+#if RT_DIAG
         if (const char* hs = std::getenv("RT_DEBUG_H_SCALE")) {  // measurement only: NOT conservative
             double k = std::atof(hs);
             g2 *= k;
@@ -927,6 +918,7 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
             L.m1 = up_f(m1);
             L.m0 = up_f(m0);
         }
+#endif
         L.r = up_f(R);
         L.g2 = up_f(g2 * (1 + 1e-6));
         L.g1 = up_f(g1 * (1 + 1e-6));
@@ -996,6 +988,7 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
             rec[7] = (uint32_t)(L.cube.size() / 16);
             L.leaves.insert(L.leaves.end(), rec, rec + 8);
         }
+#if RT_DIAG
         if (std::getenv("RT_BVH_DEBUG")) {
             size_t kinds[4] = {0, 0, 0, 0}, max_leaf = 0;
             for (const Prim& p : prims) kinds[p.kind]++;
@@ -1008,7 +1001,8 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
                          T.nodes.size(), T.leaves.size(), T.depth, max_leaf, L.c[0], L.c[1], L.c[2], L.r, L.g2,
                          L.g1, L.g0, L.m1, L.m0);
         }
-        build_graze(tris, in_tri, tri_gsin, L);
+#endif
+        build_graze(tris, in_tri, tri_gsin, L, tn);
         L.n_dsph_bvh = (int)(L.dsph.size() / 16);
         L.n_gsph_bvh = (int)(L.gsph.size() / 16);
         L.n_tri_bvh = (int)(L.tri.size() / 24);
@@ -1070,66 +1064,14 @@ struct Workspace {
     size_t spp_buf_floats = 0;
 };
 
-// RT_SORT=0 keeps the queues in production order, RT_SORT=shadow orders only the
-// shadow queue (A/B measurements).
-bool sort_enabled() {
-    const char* e = std::getenv("RT_SORT");
-    return !(e && std::strcmp(e, "0") == 0);
-}
-bool sort_tasks_enabled() {
-    const char* e = std::getenv("RT_SORT");
-    return !(e && std::strcmp(e, "shadow") == 0);
-}
-// Task ordering key (16 bits): 1 (default) = cube-map face of the direction x 2x2 cells
-// | 11-bit Morton origin; 0 = octant | 13-bit Morton; 2 = face x 4x4 | 9-bit Morton.
-// RT_TASK_KEY overrides (A/B): config 3 1080p frame 10.35 / 10.77 / 10.39 ms.
-uint32_t task_key_mode() {
-    const char* e = std::getenv("RT_TASK_KEY");
-    return e ? (uint32_t)std::atoi(e) : 7u;
-}
-// 7 (default): a ray inside a sphere or cube (the refracted child of an entering hit, the
-// reflected child of a hit from inside) is keyed by that shape's centre (1 | 15-bit Morton
-// of the centre), so a wave holds the rays trapped in one or two shapes; every other ray by
-// face x 2x2 direction cells | 10-bit Morton code of a point ahead (mode 6 with one bit less).
-// 5 / 6: face x 2x2 direction cells | 11-bit Morton code of the point
-// RT_KEY_AHEAD x (scene radius) ahead on the ray (default 0.5 / 0.25): rays that cross
-// the same region next share a key.  Config 3 (same box): mode 1 4.90 ms, 6 at 0.10 /
-// 0.15 / 0.20 / 0.25 / 0.35: 4.88 / 4.86 / 4.88 / 4.81 / 4.94, mode 5 (0.5) +1.5%.
-// 3 / 4: 24-bit keys -- task = face x 8x8 direction cells | 15-bit Morton origin (4:
-// origin-major), shadow = light | 18-bit Morton origin (3 sort passes).  Measured
-// (config 3, 1080p): 1 -> 5.78 ms, 3 -> 6.13, 4 -> 6.42: finer keys scatter the waves.
-// Own-shape shadow pre-test in the trace kernel (default on; RT_SELF_SHADOW=0: off, A/B)
-bool self_shadow_enabled() {
-    const char* e = std::getenv("RT_SELF_SHADOW");
-    return !(e && e[0] == '0');
-}
-
-// rt_render on a one-device scene: band shares rendered side by side (RT_SEAM_SPLIT)
-int seam_split() {
-    const char* e = std::getenv("RT_SEAM_SPLIT");
-    const int v = e ? std::atoi(e) : 2;
-    return v < 1 ? 1 : (v > 8 ? 8 : v);
-}
-
-// Workspace sizing: node slots per level-0 item, shadow-queue slots per node slot
-// (measured need, config 3: 3.66 node rays per pixel, 2.0 queued shadow rays per node)
-uint64_t node_factor() {
-    const char* e = std::getenv("RT_NODE_FACTOR");
-    const long v = e ? std::atol(e) : 6;
-    return v >= 2 ? (uint64_t)v : 2u;
-}
-double shadow_factor() {
-    const char* e = std::getenv("RT_SHADOW_FACTOR");
-    const double v = e ? std::atof(e) : 2.0;
-    return v >= 0.25 ? v : 0.25;
-}
-
-// Device path: "wave" (level-synchronous, default) or "mega" (per-pixel megakernel),
-// chosen with RT_PIPELINE for A/B measurement.
-bool use_megakernel() {
-    const char* e = std::getenv("RT_PIPELINE");
-    return e && std::strcmp(e, "mega") == 0;
-}
+// Task ordering key (rt_wavefront.hip task_key / inside_key; Tune::task_key): 7 (default) =
+// a ray inside a sphere or cube (the refracted child of an entering hit, the reflected child
+// of a hit from inside) is keyed by that shape's centre (1 | 15-bit Morton of the centre), so
+// a wave holds the rays trapped in one or two shapes; every other ray by face x 2x2
+// direction cells | 10-bit Morton code of a point 0.25 x (scene radius) ahead on the ray
+// (mode 6 with one bit less).  Measured alternatives (config 3, 1080p): 1 = face
+// x 2x2 cells | 11-bit Morton origin 4.90 ms, 6 at 0.10 - 0.35 ahead 4.81 - 4.94, 5 (0.5
+// ahead) +1.5%, 3 / 4 (24-bit keys) 6.13 / 6.42 vs 5.78 for mode 1.
 
 int g_num_cus(int device) {
     hipDeviceProp_t prop;
@@ -1147,11 +1089,11 @@ struct rt_scene {
     uint64_t flops_per_scan = 0;
     uint32_t n_point_lights = 0;
     int num_cus = 256;
-    int occ[3] = {0, 0, 0};  // blocks per CU for the MAXF 7 / 15 / 63 variants
     int occ_trace = 0, occ_shadow = 0, occ_combine = 0;
     int occ_trace_each[3] = {0, 0, 0};  // generic / level-0 / deep trace instantiations
     bool count_ops = false;  // rt_scene_set_scan_counting
     int grid_pct = 100;      // rt_scene_set_grid_share: % of a full chip for persistent grids
+    Tune tune;               // rt_tune.hpp: fixed scene-build keys, pass keys (rt_scene_set_tuning)
     Workspace ws;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -1174,6 +1116,7 @@ struct rt_scene {
 
 rt_multi_state*& rt_scene_multi(rt_scene* s) { return s->multi; }
 int rt_scene_device_of(const rt_scene* s) { return s->device; }
+const Tune& rt_scene_tune(const rt_scene* s) { return s->tune; }
 
 namespace {
 
@@ -1214,10 +1157,6 @@ uint32_t light_bits(const rt_scene* s) {
 // (node << 1) | slot a parent reference).
 uint64_t pool_cap_limit(const rt_scene* s) { return std::min<uint64_t>(1ull << (32 - light_bits(s)), 1ull << 30); }
 
-int variant_of(uint32_t depth) {
-    int maxf = (int)depth - 1;
-    return maxf <= 7 ? 0 : (maxf <= 15 ? 1 : 2);
-}
 
 rt_status ensure_ws(rt_scene* s, size_t out_floats, size_t out8_bytes) {
     Workspace& w = s->ws;
@@ -1310,7 +1249,14 @@ uint32_t rt_band_rows_per_rank(uint32_t y_res, uint32_t band_rows, uint32_t worl
 }
 
 rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out) {
+    return rt_scene_create_tuned(d, device, nullptr, out);
+}
+
+rt_status rt_scene_create_tuned(const rt_scene_desc* d, int32_t device, const char* tuning, rt_scene** out) {
     if (!d || !out) return RT_ERR_INVALID_ARG;
+    // the handle's tuning: defaults, the environment's RT_TUNE (A/B harness), then `tuning`
+    Tune tn;
+    if (!tune_apply(tn, std::getenv("RT_TUNE"), true) || !tune_apply(tn, tuning, true)) return RT_ERR_INVALID_ARG;
     if ((d->n_materials && !d->materials) || (d->n_shapes && !d->shapes) || (d->n_lights && !d->lights))
         return RT_ERR_INVALID_ARG;
     if (d->n_shapes >= (1u << 27)) return RT_ERR_UNSUPPORTED;
@@ -1409,7 +1355,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     }
     // ---- culling hierarchy and the run layout (leaf order first, then the linear rest)
     RunLayout lay;
-    build_runs(sph_in, tri_in, cube_in, bvh_enabled(), lay);
+    build_runs(sph_in, tri_in, cube_in, tn, lay);
     // light buffers append cell leaves and record copies to the layout (after the linear
     // rest: the scan's run counts below exclude them)
     const int n_dsph_all = (int)(lay.dsph.size() / 16), n_gsph_all = (int)(lay.gsph.size() / 16);
@@ -1434,9 +1380,9 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
         }
     }
     LightBuffers lbuf;
-    build_light_buffers(lay, lights, lbuf);
+    build_light_buffers(lay, lights, lbuf, tn);
     for (size_t i = 0; i < lights.size(); i++) lights[i].lb_base = lbuf.base[i];
-    build_shape_buffers(lay, shapes);
+    build_shape_buffers(lay, shapes, tn);
     dsph.swap(lay.dsph);
     gsph.swap(lay.gsph);
     tri.swap(lay.tri);
@@ -1479,12 +1425,17 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     if (!sc) return RT_ERR_OUT_OF_MEMORY;
     rt_status st = select_device(device, &sc->device);
     if (st != RT_OK) return st;
+    HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&sc->ev0));
+    HIP_TRY(hipEventCreate(&sc->ev1));
     HIP_TRY(hipMalloc(&sc->dmem, total));
     sc->dbytes = total;
     std::vector<uint8_t> host(total, 0);
     for (auto& s : secs)
         if (s.bytes) std::memcpy(host.data() + s.off, s.src, s.bytes);
-    HIP_TRY(hipMemcpy(sc->dmem, host.data(), total, hipMemcpyHostToDevice));
+    // on the scene's own stream, waited for (the host buffer is pageable and goes out of scope)
+    HIP_TRY(hipMemcpyAsync(sc->dmem, host.data(), total, hipMemcpyHostToDevice, sc->stream));
+    HIP_TRY(hipStreamSynchronize(sc->stream));
     auto at = [&](int k) { return (const void*)((const uint8_t*)sc->dmem + secs[k].off); };
     DevScene& S = sc->S;
     S.dsph = (const float4*)at(0);
@@ -1513,14 +1464,13 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     S.graze_mask = (const uint32_t*)at(15);
     S.graze_res = lay.graze_res;
     S.graze_words = lay.graze_words;
-    {  // RT_GRAZE_LANE=0: the wave-union grazing path (A/B)
-        const char* e = std::getenv("RT_GRAZE_LANE");
-        S.graze_lane = (e && e[0] == '0') ? 0u : 1u;
-    }
+    S.graze_lane = tn.graze_lane ? 1u : 0u;  // 0: the wave-union grazing path (A/B)
     S.lb_res = lbuf.res;
     S.lb_dmax = lbuf.dmax;
     S.n_graze_blk = (int32_t)(lay.graze_blk.size() / 32);
+#if RT_DIAG
     if (std::getenv("RT_DEBUG_NO_GRAZE")) S.n_graze_blk = 0;  // measurement only: NOT exact (the grazing pass's cost)
+#endif
     S.bvh_root = lay.root;
     S.n_bvh_nodes = (int32_t)(lay.nodes.size() / 16);
     S.use_bvh = lay.use ? 1 : 0;
@@ -1538,8 +1488,10 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     S.bvh_m1 = lay.m1;
     S.bvh_m0 = lay.m0;
     S.graze_s2 = 1.0201f;  // normals pre-divided by sin(phi_T): checked at 1.01 sin(phi_T)
+#if RT_DIAG
     if (const char* e = std::getenv("RT_DEBUG_GRAZE_S2")) S.graze_s2 = (float)std::atof(e);  // measurement only: NOT exact
-    S.dark_skip = (normals_ok && !std::getenv("RT_NO_DARK_SKIP")) ? 1 : 0;  // env: A/B
+#endif
+    S.dark_skip = (normals_ok && tn.dark_skip) ? 1 : 0;
     S.amb_r = d->ambient.r;
     S.amb_g = d->ambient.g;
     S.amb_b = d->ambient.b;
@@ -1547,9 +1499,7 @@ rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out
     sc->n_point_lights = n_point;
     sc->normal_max = nmax;
     sc->num_cus = g_num_cus(sc->device);
-    HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreate(&sc->ev0));
-    HIP_TRY(hipEventCreate(&sc->ev1));
+    sc->tune = tn;
     *out = sc.release();
     return RT_OK;
 }
@@ -1634,6 +1584,20 @@ rt_status rt_scene_set_grid_share(rt_scene* s, int32_t percent) {
     return RT_OK;
 }
 
+rt_status rt_scene_set_tuning(rt_scene* s, const char* tuning) {
+    if (!s) return RT_ERR_INVALID_ARG;
+    Tune t = s->tune;
+    if (!tune_apply(t, tuning, false)) return RT_ERR_INVALID_ARG;
+    auto set = [&](rt_scene* c) {  // clones share the scene-build keys
+        c->tune = t;
+        return RT_OK;
+    };
+    (void)set(s);
+    if (s->multi) (void)rt_multi_each(s->multi, set);
+    if (s->split) (void)rt_multi_each(s->split, set);
+    return RT_OK;
+}
+
 rt_status rt_scene_set_scan_counting(rt_scene* s, int32_t enable) {
     if (!s) return RT_ERR_INVALID_ARG;
     if (s->multi) (void)rt_multi_each(s->multi, [&](rt_scene* c) { return rt_scene_set_scan_counting(c, enable); });
@@ -1642,7 +1606,9 @@ rt_status rt_scene_set_scan_counting(rt_scene* s, int32_t enable) {
     return RT_OK;
 }
 
-static uint32_t* g_task_clock = nullptr;  // RT_TASK_CLOCK records (debug)
+#if RT_DIAG
+static uint32_t* g_task_clock = nullptr;  // RT_TASK_CLOCK records (diagnostic builds)
+#endif
 
 // Where one render pass's results go: the float frame (or band buffer), optionally its
 // Color::as_u8 bytes (fused into the level-0 combine), ray counters, and whether queue
@@ -1663,57 +1629,14 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
 static rt_status launch_bands(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
                               uint32_t band_rows, uint32_t rank, uint32_t world, const PassOut& o,
                               hipStream_t stream) {
-    float* d_rgb = o.rgb;
-    unsigned long long* d_counters = o.counters;
-    if (!s || !cam || (!d_rgb && !o.rgb8) || band_rows == 0 || world == 0 || rank >= world) return RT_ERR_INVALID_ARG;
+    if (!s || !cam || (!o.rgb && !o.rgb8) || band_rows == 0 || world == 0 || rank >= world) return RT_ERR_INVALID_ARG;
     if (spp == 0) return RT_ERR_INVALID_ARG;
     if (cam->x_res == 0 || cam->y_res == 0) return RT_ERR_INVALID_ARG;
     if (depth > RT_MAX_DEPTH) return RT_ERR_UNSUPPORTED;
     if ((uint64_t)cam->x_res * cam->y_res * 3 >= (1ull << 32)) return RT_ERR_UNSUPPORTED;
     rt_status st = ensure_ws(s, 0, 0);
     if (st != RT_OK) return st;
-    if (!use_megakernel()) return launch_bands_wave(s, cam, depth, spp, seed, band_rows, rank, world, o, stream);
-    // the per-pixel megakernel (A/B path): one sample, f32 out, a 63-frame continuation stack
-    if (spp != 1 || o.rgb8 || !d_rgb || depth > 64) return RT_ERR_UNSUPPORTED;  // the per-pixel megakernel traces one sample, f32 out
-    RenderParams p;
-    std::memset(&p, 0, sizeof(p));
-    p.S = s->S;
-    p.cam_ox = cam->origin[0];
-    p.cam_oy = cam->origin[1];
-    p.cam_oz = cam->origin[2];
-    p.x_min = cam->x_min;
-    p.y_max = cam->y_max;
-    // render.rs:179-180, evaluated once in f32 (identical on host and device)
-    p.x_delta = (cam->x_max - cam->x_min) / (float)cam->x_res;
-    p.y_delta = (cam->y_max - cam->y_min) / (float)cam->y_res;
-    p.width = cam->x_res;
-    p.height = cam->y_res;
-    p.depth = depth;
-    p.band_rows = band_rows;
-    p.rank = rank;
-    p.world = world;
-    p.rows_local = rt_band_rows_per_rank(cam->y_res, band_rows, world);
-    p.tiles_x = (cam->x_res + 7) / 8;
-    uint32_t tiles_y = (p.rows_local + 7) / 8;
-    p.total_items = p.tiles_x * tiles_y * 64u;
-    p.out = d_rgb;
-    p.ray_counters = d_counters;
-    p.iter_counter = s->ws.counters + 3;
-    p.work_counter = s->ws.work;
-
-    int var = variant_of(depth);
-    if (s->occ[var] == 0) {
-        int b = 0;
-        HIP_TRY(render_occupancy(depth, &b));
-        s->occ[var] = b > 0 ? b : 1;
-    }
-    long long blocks = (long long)s->num_cus * s->occ[var];
-    long long need = ((long long)p.total_items + 255) / 256;
-    if (blocks > need) blocks = need;
-    if (blocks < 1) blocks = 1;
-    HIP_TRY(hipMemsetAsync(s->ws.work, 0, sizeof(uint32_t), stream));
-    HIP_TRY(launch_render(p, (int)blocks, stream));
-    return RT_OK;
+    return launch_bands_wave(s, cam, depth, spp, seed, band_rows, rank, world, o, stream);
 }
 
 // Level-synchronous pipeline: trace(0..L-1), then combine(L-1..0), all on `stream`.
@@ -1726,16 +1649,12 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
                                uint32_t sample = 0, uint32_t seed = 0, uint32_t frames = 1,
                                const rt_camera* cams = nullptr, bool spp_batch = false);
 
-// Samples per pipeline pass for spp > 1: RT_SPP_BATCH, else as many (<= RT_MAX_FRAMES) as
-// keep a pass within RT_SPP_BATCH_ITEMS level-0 items (default 2^25: 4 x 3840x2160 or
+// Samples per pipeline pass for spp > 1: Tune::spp_batch, else as many (<= RT_MAX_FRAMES) as
+// keep a pass within Tune::spp_batch_items level-0 items (default 2^25: 4 x 3840x2160 or
 // 8 x 1920x1080; the pass's workspace grows with its items).
-static uint32_t spp_batch_size(uint32_t spp, uint64_t frame_items) {
-    if (const char* e = std::getenv("RT_SPP_BATCH")) {
-        const int v = std::atoi(e);
-        return (uint32_t)std::max(1, std::min(v, (int)RT_MAX_FRAMES));
-    }
-    const char* ei = std::getenv("RT_SPP_BATCH_ITEMS");
-    const uint64_t cap = ei ? std::strtoull(ei, nullptr, 0) : (1ull << 25);
+static uint32_t spp_batch_size(const Tune& tn, uint32_t spp, uint64_t frame_items) {
+    if (tn.spp_batch > 0) return (uint32_t)std::max(1, std::min(tn.spp_batch, (int)RT_MAX_FRAMES));
+    const uint64_t cap = tn.spp_batch_items;
     uint32_t b = 1;
     while (b < RT_MAX_FRAMES && b < spp && (uint64_t)(b + 1) * frame_items <= cap) b++;
     return b;
@@ -1753,7 +1672,7 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
     const uint32_t rows_local = rt_band_rows_per_rank(cam->y_res, band_rows, world);
     const uint64_t frame_items = (uint64_t)((cam->x_res + 7) / 8) * ((rows_local + 7) / 8) * 64u;
     const uint32_t sb = spp > 1 && o.rgb && (uint64_t)cam->x_res * cam->y_res < (1ull << RT_FRAME_SHIFT)
-                            ? spp_batch_size(spp, frame_items) : 1u;
+                            ? spp_batch_size(s->tune, spp, frame_items) : 1u;
     if (sb > 1) {
         Workspace& w = s->ws;
         const size_t frame_floats = (size_t)rows_local * cam->x_res * 3u;
@@ -1796,25 +1715,20 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     // queue keys of a sample batch: "mix" -- no sample index in the keys, the samples of one
     // place share waves; "mixfine" (default) -- the same with a frame batch's finer 21-bit
     // task / 4-bit-distance shadow keys; "frame" -- the sample index above the key bits like
-    // a frame batch (RT_SPP_KEYS, A/B)
-    // (frame batches: RT_FRAME_KEYS, default "mixfine" as well)
-    const char* sk = std::getenv(spp_batch ? "RT_SPP_KEYS" : "RT_FRAME_KEYS");
+    // a frame batch (Tune::spp_keys, A/B)
+    // (frame batches: Tune::frame_keys, default "mixfine" as well)
     // measured (config 5, 4 passes of 4K x 64 samples in batches of 4): mix 1021, mixfine
     // 1058, frame 1023 Msamples/s; one pass per sample 788.  Frame batches (config 3, 4 passes
     // of 5 frames): frame 944 / 945, mix 1023 / 1018, mixfine 1073 / 1076 Mpixels/s with one
     // camera for every frame; with a camera per frame (an animation) frame 948, mixfine 1025
-    const int key_default = 1;
-    const int spp_keys = !sk ? key_default
-                             : (std::strcmp(sk, "mixfine") == 0 ? 1
-                                                                : (std::strcmp(sk, "frame") == 0 ? 2
-                                                                                                 : (std::strcmp(sk, "mix") == 0 ? 0 : key_default)));
+    const Tune& tn = s->tune;
+    const int spp_keys = spp_batch ? tn.spp_keys : tn.frame_keys;
     p.frame_keys = spp_keys == 2 ? 1u : 0u;
     {
         // level-0 tiles dealt to a pass's frames in turn (default since the 16-frame passes:
         // 1124 - 1133 vs 1116 - 1122 Mpixels/s in 7 alternating pairs, tools/r3_ab23.sh /
-        // r3_ab24.sh; at 5-frame passes it was noise); RT_L0_INTERLEAVE=0: frame-major (A/B)
-        const char* e = std::getenv("RT_L0_INTERLEAVE");
-        p.l0_interleave = (e && e[0] == '0') ? 0u : 1u;
+        // r3_ab24.sh; at 5-frame passes it was noise); l0_interleave=0: frame-major (A/B)
+        p.l0_interleave = tn.l0_interleave ? 1u : 0u;
     }
     p.sample = sample;
     p.seed = seed;
@@ -1851,7 +1765,7 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     total *= frames;
     if (total >= (1ull << 30)) return RT_ERR_UNSUPPORTED;
     p.total_items = (uint32_t)total;
-    // node / task pool: RT_NODE_FACTOR (default 6) nodes per level-0 item -- config 3
+    // node / task pool: Tune::node_factor (default 6) nodes per level-0 item -- config 3
     // traces 3.66 node rays per pixel, config 4 the same scene at 4K; an overflow is
     // reported, never silently truncated, and the next pass gets twice the pool (rt_render
     // retries by itself).  A shadow entry packs (node << light_bits) | light, so nodes stay
@@ -1859,8 +1773,8 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     p.light_bits = light_bits(s);
     const uint64_t max_cap = pool_cap_limit(s);
     if (total >= max_cap) return RT_ERR_UNSUPPORTED;
-    uint64_t want = std::max<uint64_t>(total * node_factor(), 1u << 20);
-    if (const char* e = std::getenv("RT_NODE_CAP")) want = std::max<uint64_t>(total + 1, std::strtoull(e, nullptr, 0));
+    uint64_t want = std::max<uint64_t>(total * (uint64_t)tn.node_factor, 1u << 20);
+    if (tn.node_cap) want = std::max<uint64_t>(total + 1, tn.node_cap);  // test knob
     if (&w == &s->ws) want = std::max<uint64_t>(want, s->pool_floor);
     if (want > max_cap) want = max_cap;
     if (w.capacity < want) {  // grows only (rt_render may have grown it after an overflow)
@@ -1870,13 +1784,17 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     if (!w.levels) {
         HIP_TRY(hipMalloc(&w.levels, RT_LEVEL_TABLE_WORDS * sizeof(uint32_t)));
         HIP_TRY(hipMalloc(&w.overflow, 64));
-        HIP_TRY(hipMemset(w.overflow, 0, 64));
+        // stream-ordered on the pass's own stream: a hipMemset on the null stream is not
+        // ordered with the caller's non-blocking stream and could land after this pass had
+        // latched an overflow (profiles/r3y: a missed RT_ERR_CAPACITY that depended on which
+        // hardware queue the null stream shared with another slot's pass)
+        HIP_TRY(hipMemsetAsync(w.overflow, 0, 64, stream));
     }
-    // shadow queue: at most one entry per point light per hit node; RT_SHADOW_FACTOR
+    // shadow queue: at most one entry per point light per hit node; Tune::shadow_factor
     // (default 2) entries per node slot, at most the point lights (config 3 queues 2.0 per
     // traced node: the trace kernel decides the rest; overflow reported like the node pool's)
     uint64_t want_sh = std::min<uint64_t>(
-        (uint64_t)((double)w.capacity * std::min<double>(shadow_factor(), (double)s->n_point_lights)), 0x7FFFFFFFu);
+        (uint64_t)((double)w.capacity * std::min<double>(tn.shadow_factor, (double)s->n_point_lights)), 0x7FFFFFFFu);
     if (want_sh == 0) want_sh = 1;
     if (w.shadow_capacity < want_sh) {
         if (w.shadow) (void)hipFree(w.shadow);
@@ -1885,31 +1803,20 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         HIP_TRY(hipMalloc(&w.shadow, want_sh * sizeof(uint32_t)));
         w.shadow_capacity = (uint32_t)want_sh;
     }
-    const char* ss = std::getenv("RT_SORT_SHADOW");  // "0": keep production order (A/B)
-    const bool sort_on = s->S.use_bvh && sort_enabled();
-    const bool sort_tasks = sort_on && sort_tasks_enabled();
-    const bool sort_shadow = sort_on && !(ss && ss[0] == '0');
-    p.key_mode = task_key_mode();
-    {
-        const char* e = std::getenv("RT_KEY_AHEAD");
-        p.key_ahead = e ? (float)std::atof(e) : (p.key_mode == 5 ? 0.5f : 0.25f);
-    }
-    p.self_shadow = self_shadow_enabled() ? 1u : 0u;
-    {
-        const char* e = std::getenv("RT_REVERSE");  // bit mask of levels traced from the queue's end (A/B)
-        p.reverse_levels = e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
-    }
-    {
-        // primary hits are coherent (8x8 tiles): their shadow rays are traced inline by the
-        // trace kernel (config 3: -2%); deeper levels' hit points are scattered and go
-        // through the sorted shadow queue (inlining levels 0-1: +20%, all: x2.4)
-        const char* e = std::getenv("RT_INLINE_SHADOW");
-        p.inline_levels = e ? (uint32_t)std::atoi(e) : 1u;
-    }
-    {
-        const char* e = std::getenv("RT_SCHED");
-        p.sched = e ? (uint32_t)std::atoi(e) : 0u;
-    }
+    const bool sort_tasks = s->S.use_bvh && tn.sort_tasks;
+    const bool sort_shadow = s->S.use_bvh && tn.sort_shadow;
+    p.key_mode = (uint32_t)tn.task_key;
+    p.key_ahead = p.key_mode == 5 ? 0.5f : 0.25f;
+    p.self_shadow = tn.self_shadow ? 1u : 0u;
+    // tracing a level's sorted queue from its end (939 / 947 vs 944 / 945 Mpixels/s) and the
+    // dynamic per-wave work counter (6.7 vs 4.9 ms) lost: levels run in queue order, grid-stride
+    p.reverse_levels = 0u;
+    p.sched = 0u;
+    // primary hits are coherent (8x8 tiles): their shadow rays are traced inline by the
+    // trace kernel (config 3: -2%); deeper levels' hit points are scattered and go
+    // through the sorted shadow queue (inlining levels 0-1: +20%, all: x2.4)
+    p.inline_levels = (uint32_t)tn.inline_shadow;
+#if RT_DIAG
     {
         // debug: per wave-iteration wall-clock records of the trace kernel (rt_debug_task_clock)
         static uint32_t* clk = nullptr;
@@ -1924,21 +1831,19 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         p.task_clock_cap = clk_cap;
         if (p.task_clock) HIP_TRY(hipMemsetAsync(p.task_clock, 0, 16, stream));
     }
-    {
-        // RT_TASK_W = narrowest trace task width (64: fixed 64-ray tasks), RT_TASK_FILL =
-        // tasks per wave slot below which a level's tasks are narrowed
-        const char* e = std::getenv("RT_TASK_W");
-        const int w = e ? std::atoi(e) : 64;
-        p.task_w_min = (w == 16 || w == 32) ? (uint32_t)w : 64u;
-        const char* f = std::getenv("RT_TASK_FILL");
-        p.task_w_fill = f ? (float)std::atof(f) : 1.f;
-    }
-    if (s->count_ops) {  // instrumented kernels; RT_COUNT=trace|shadow: only that kernel's tests
-        const char* e = std::getenv("RT_COUNT");
-        p.count_mask = !e ? 3u : (std::strcmp(e, "trace") == 0 ? 1u : (std::strcmp(e, "shadow") == 0 ? 2u : 3u));
-    } else {
-        p.count_mask = 0u;
-    }
+#else
+    p.task_clock = nullptr;
+    p.task_clock_cap = 0;
+#endif
+    // narrowest trace task width (64: fixed 64-ray tasks) and the tasks per wave slot below
+    // which a level's tasks are narrowed
+    p.task_w_min = (uint32_t)tn.task_w;
+    p.task_w_fill = (float)tn.task_fill;
+    // instrumented kernels (counting frames): Tune::count selects the kernels that count
+    p.count_mask = s->count_ops ? (uint32_t)tn.count : 0u;
+    p.lds_mask = (uint32_t)tn.lds_nodes;
+    p.deep_kernel = (uint32_t)tn.deep_kernel;
+    p.occ_each = (uint32_t)tn.occ_each;
     // 16-bit keys: task = direction cell | coarse origin Morton (task_key); shadow =
     // light index | the Morton bits that fit (all 15 above 16 lights' worth of bits)
     uint32_t lbits = 0;
@@ -1950,10 +1855,9 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         // holds rays that test one cell's records, at similar reach; rays that walk the
         // hierarchy: light | flag | 17-bit Morton): 790 / 789 Mpixels/s vs 784 / 775 for the
         // cell alone ("cell") and 752 / 763 for light | 18-bit Morton ("18", round 1's
-        // default; round 1: 4.80 ms vs 4.93 with the 16-bit key "16"); RT_SHADOW_KEY (A/B)
-        const char* e = std::getenv("RT_SHADOW_KEY");
-        const uint32_t cell = !e ? 2u : (std::strcmp(e, "cell") == 0 ? 1u : (std::strcmp(e, "cell2") == 0 ? 2u : 0u));
-        const int v = (e && !cell) ? std::atoi(e) : 18;
+        // default; round 1: 4.80 ms vs 4.93 with the 16-bit key "16"); Tune::shadow_key (A/B)
+        const uint32_t cell = tn.shadow_key == 1 ? 1u : (tn.shadow_key == 2 ? 2u : 0u);
+        const int v = cell ? 18 : tn.shadow_key;
         p.shadow_fine = (p.key_mode == 3 || p.key_mode == 4 || v == 18) ? 18u : (v == 21 ? 21u : 0u);
         if (p.shadow_fine && p.shadow_fine + lbits > 32u) p.shadow_fine = 0u;
         // cell keys: the light-buffer cell index (x 8 distance buckets for cell2) must fit
@@ -1962,36 +1866,21 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         p.shadow_cell = (cell && p.shadow_fine == 18u && s->S.lb_res && cells < (1u << 17)) ? cell : 0u;
     }
     if (p.shadow_fine) shadow_bits = p.shadow_fine + lbits;
-    if (frames == 1 && !forest_params) {
-        // RT_FINE1=1 (A/B): one frame gets a batch's finer keys too -- 21-bit task keys and
-        // the 4-bit shadow distance (3 radix passes each)
-        const char* f1 = std::getenv("RT_FINE1");
-        if (f1 && f1[0] == '1' && p.key_mode == 7 && task_bits == 16u) {
-            p.task_fine = 1u;
-            task_bits = 21u;
-            if (p.shadow_cell == 2u && p.shadow_fine == 18u && shadow_bits + 1u <= 24u &&
-                6ull * s->S.lb_res * s->S.lb_res * 16u < (1u << 18)) {
-                p.shadow_cell = 3u;
-                p.shadow_fine = 19u;
-                shadow_bits += 1u;
-            }
-        }
-    }
+    // (one frame with a batch's finer keys -- 21-bit task keys, 4-bit shadow distance --
+    // measured 4.08 vs 4.11 ms, split 3.88 vs 3.76: not kept)
     if (frames > 1 && spp_keys != 0) {  // the frame index above every key bit: frames are contiguous in sorted queues (ordering only)
         uint32_t fbits = 0;
         while ((1u << fbits) < frames) fbits++;
         if (!p.frame_keys) fbits = 0;  // "mixfine": the finer keys without the sample index
         // a batch's task keys take 3 radix passes of 8 bits anyway: key mode 7 fills them with
-        // 5 more origin bits (RT_TASK_FINE=0: off, A/B)
-        const char* tf = std::getenv("RT_TASK_FINE");
-        if (!(tf && tf[0] == '0') && p.key_mode == 7 && task_bits == 16u && fbits <= 3) {
+        // 5 more origin bits (task_fine=0: off, A/B)
+        if (tn.task_fine && p.key_mode == 7 && task_bits == 16u && fbits <= 3) {
             p.task_fine = 1u;
             task_bits = 21u;
         }
         // ... and the shadow keys a fourth distance bit when 3 passes still hold them
-        // (RT_SHADOW_FINE=0: off, A/B)
-        const char* sf = std::getenv("RT_SHADOW_FINE");
-        if (!(sf && sf[0] == '0') && p.shadow_cell == 2u && p.shadow_fine == 18u && shadow_bits + 1u + fbits <= 24u &&
+        // (shadow_fine=0: off, A/B)
+        if (tn.shadow_fine && p.shadow_cell == 2u && p.shadow_fine == 18u && shadow_bits + 1u + fbits <= 24u &&
             6ull * s->S.lb_res * s->S.lb_res * 16u < (1u << 18)) {
             p.shadow_cell = 3u;
             p.shadow_fine = 19u;
@@ -1999,12 +1888,10 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         }
         // without frame bits a batch's 3 radix passes hold 24 key bits: 18-bit Morton task keys
         // and a 7-bit shadow distance (1035 / 1039 vs 1027 / 1031 Mpixels/s with the 21-bit
-        // keys; RT_KEY24=0: off, A/B)
-        const char* k24 = std::getenv("RT_KEY24");
-        if (!(k24 && k24[0] == '0') && fbits == 0) {
+        // keys; key24=0: off, A/B; 4x4 direction cells | 16-bit Morton instead: no gain)
+        if (tn.key24 && fbits == 0) {
             if (p.task_fine == 1u) {
-                const char* kd = std::getenv("RT_KEY24_DIR");  // "16": 4x4 direction cells | 16-bit Morton (A/B)
-                p.task_fine = (kd && std::strcmp(kd, "16") == 0) ? 3u : 2u;
+                p.task_fine = 2u;
                 task_bits = 24u;
             }
             if (p.shadow_cell == 3u && 6ull * s->S.lb_res * s->S.lb_res * 128u < (1u << 21) && lbits + 22u <= 24u) {
@@ -2057,8 +1944,7 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     // 21-bit shadow keys).  At 4 passes x 2 frames in flight: 9 (task keys in 2 passes)
     // 788 / 795 vs 791 / 790 Mpixels/s, 11 (every key in 2 passes) 751 / 750 vs 789 / 785 --
     // a wider digit's ranking and tile counts cost more than the pass it saves
-    const char* sd = std::getenv("RT_SORT_DIGIT");
-    const uint32_t sort_digit = sd ? (uint32_t)std::atoi(sd) : 8u;
+    const uint32_t sort_digit = 8u;
     p.task_keys = sort_tasks ? w.task_keys : nullptr;
     p.perm = nullptr;
     p.shadow_keys = sort_shadow ? w.shadow_keys : nullptr;
@@ -2096,35 +1982,29 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     int cb = s->num_cus * s->occ_combine;
     {
         // the persistent trace grids at grid_pct % of a full chip (rt_scene_set_grid_share;
-        // RT_GRID_PCT overrides it, A/B)
-        const char* e = std::getenv("RT_GRID_PCT");
-        const int pct = e ? std::atoi(e) : s->grid_pct;
+        // Tune::grid_pct overrides it, A/B)
+        const int pct = tn.grid_pct ? tn.grid_pct : s->grid_pct;
         // the shadow pass keeps the whole chip (measured: 937 vs 927 Mpixels/s at 75%);
-        // RT_GRID_PCT_SHADOW sets its own share (A/B)
-        const char* es = std::getenv("RT_GRID_PCT_SHADOW");
-        const int spct = es ? std::atoi(es) : 100;
+        // Tune::grid_pct_shadow sets its own share (A/B)
+        const int spct = tn.grid_pct_shadow;
         if (pct > 0 && pct < 100) tb = std::max(1, tb * pct / 100);
         if (spct > 0 && spct < 100) sb = std::max(1, sb * spct / 100);
         // the combine grids too (50% / 25%: 928 / 918, 889 / 896 vs 936 / 940 Mpixels/s);
-        // RT_GRID_PCT_COMBINE (A/B)
-        const char* ec = std::getenv("RT_GRID_PCT_COMBINE");
-        const int cpct = ec ? std::atoi(ec) : 100;
+        // Tune::grid_pct_combine (A/B)
+        const int cpct = tn.grid_pct_combine;
         if (cpct > 0 && cpct < 100) cb = std::max(1, cb * cpct / 100);
     }
     uint32_t levels = depth > 0 ? depth : 1;
-    // debug A/B (RT_DUP, letters s / h / c): launch every queue sort / the shadow pass / every
-    // combine twice -- each is idempotent -- to measure a stage's marginal cost in place
-    const char* dup = std::getenv("RT_DUP");
-    const int dup_sort = dup && std::strchr(dup, 's') ? 2 : 1, dup_shadow = dup && std::strchr(dup, 'h') ? 2 : 1,
-              dup_comb = dup && std::strchr(dup, 'c') ? 2 : 1;
+    // measurement (Tune::dup, letters s / h / c): launch every queue sort / the shadow pass /
+    // every combine twice -- each is idempotent -- to measure a stage's marginal cost in place
+    const int dup_sort = (tn.dup & 1) ? 2 : 1, dup_shadow = (tn.dup & 2) ? 2 : 1, dup_comb = (tn.dup & 4) ? 2 : 1;
     // Every launch sizes itself from the device-side level counts: the whole frame is
     // enqueued without a host round trip (levels past the deepest non-empty one are no-ops).
     HIP_TRY(launch_wave_init(w.levels, RT_LEVEL_TABLE_WORDS, p.total_items, sample == 0 ? w.overflow : nullptr,
                              stream));
     HIP_TRY(launch_wave_trace(p, 0, tb, stream, s->occ_trace_each, s->occ_trace));
-    // RT_SORT_LEVELS: bit k set = level k's queue is sorted (A/B; default every level)
-    const char* sl = std::getenv("RT_SORT_LEVELS");
-    const uint64_t sort_levels = sl ? std::strtoull(sl, nullptr, 0) : ~0ull;
+    // every level's queue is sorted (leaving any level unsorted lost: DESIGN.md)
+    const uint64_t sort_levels = ~0ull;
     for (uint32_t k = 1; k < levels; k++) {
         if (o.may_sync && levels > 16 && (k & 7u) == 0) {
             // a deep pass the caller waits for anyway: stop at the first empty level (the
@@ -2191,17 +2071,24 @@ rt_status rt_render_bands_ex_async(const rt_scene* scene, const rt_camera* cams,
     hipStream_t hs = (hipStream_t)stream;
     const PassOut o{d_rgb, d_rgb8, reinterpret_cast<unsigned long long*>(d_counters), true, false};
     if (n_frames == 1) {
-        if (use_megakernel() && !d_rgb) return RT_ERR_UNSUPPORTED;
         st = launch_bands(s, cam, depth, spp, seed, band_rows, rank, world, o, hs);
     } else {
-        if (use_megakernel()) return RT_ERR_UNSUPPORTED;
         st = wave_pipeline(s, s->ws, cam, depth, band_rows, rank, world, o, hs, nullptr, nullptr, 1, 0, 0, n_frames,
                            cams);
     }
     if (st != RT_OK) return st;
     hipEvent_t ev = nullptr;
-    for (auto& se : s->ev_streams)
+    for (size_t i = 0; i < s->ev_streams.size();) {  // drop completed renders of other streams
+        auto& se = s->ev_streams[i];
+        if (se.first != hs && hipEventQuery(se.second) == hipSuccess) {
+            (void)hipEventDestroy(se.second);
+            se = s->ev_streams.back();
+            s->ev_streams.pop_back();
+            continue;
+        }
         if (se.first == hs) ev = se.second;
+        i++;
+    }
     if (!ev) {
         HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         s->ev_streams.emplace_back(hs, ev);
@@ -2258,8 +2145,8 @@ static rt_status ensure_split(rt_scene* s, int n) {
 // joined back into `stream`.  The meeting row starts at the
 // even split and, whenever the previous call's share spans have already completed when the
 // next call is enqueued, moves 8 rows toward the share that finished first (within [half,
-// 3/4] of the frame); the shares' persistent grids take RT_SEAM_GRID_PCT (default 80) % of
-// the chip, or the scene's own share if smaller.  RT_SEAM_SPLIT=1 (or frames under 32 rows):
+// 3/4] of the frame); the shares' persistent grids take Tune::seam_grid_pct (default 80) % of
+// the chip, or the scene's own share if smaller.  seam_split=1 (or frames under 32 rows):
 // one pass on `stream`.  No pixel depends on any of it.
 rt_status rt_render_frame_async(const rt_scene* scene, const rt_camera* cam, uint32_t depth, float* d_rgb,
                                 uint8_t* d_rgb8, uint64_t* d_counters, void* stream) {
@@ -2271,7 +2158,7 @@ rt_status rt_render_frame_async(const rt_scene* scene, const rt_camera* cam, uin
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t hs = (hipStream_t)stream;
     const uint32_t y = cam->y_res;
-    if (seam_split() != 2 || use_megakernel() || y < 32u) {
+    if (s->tune.seam_split != 2 || y < 32u) {
         // one pass: one band of 8-row tiles holding every row, padded to a multiple of 8
         const size_t n = (size_t)cam->x_res * y * 3;
         const size_t n_pad = (size_t)cam->x_res * rt_band_rows_per_rank(y, 8, 1) * 3;
@@ -2294,9 +2181,10 @@ rt_status rt_render_frame_async(const rt_scene* scene, const rt_camera* cam, uin
         s->split_dev_rows = even;
         s->split_dev_y = y;
         // both shares' node pools sized once for the largest share they can get (unless the
-        // RT_NODE_CAP test knob pins them)
-        const uint64_t floor = std::min<uint64_t>((uint64_t)hi * cam->x_res * node_factor(), pool_cap_limit(s));
-        if (!std::getenv("RT_NODE_CAP"))
+        // node_cap test knob pins them)
+        const uint64_t floor = std::min<uint64_t>((uint64_t)hi * cam->x_res * (uint64_t)s->tune.node_factor,
+                                                  pool_cap_limit(s));
+        if (!s->tune.node_cap)
             (void)rt_multi_each_rank(s->split, [&](rt_scene* c) {
                 c->pool_floor = std::max<uint32_t>(c->pool_floor, (uint32_t)floor);
                 return RT_OK;
@@ -2311,8 +2199,7 @@ rt_status rt_render_frame_async(const rt_scene* scene, const rt_camera* cam, uin
                 s->split_dev_rows -= 8u;
         }
     }
-    const char* gp = std::getenv("RT_SEAM_GRID_PCT");
-    const int pct = std::min(s->grid_pct, gp ? std::max(1, std::min(100, std::atoi(gp))) : 80);
+    const int pct = std::min(s->grid_pct, s->tune.seam_grid_pct);
     const int saved = s->grid_pct;  // read when the passes are enqueued: restored right after
     auto set_pct = [&](int v) {
         s->grid_pct = v;
@@ -2353,12 +2240,20 @@ rt_status rt_scene_sync_status(rt_scene* s) {
 rt_status rt_scene_sync_own(rt_scene* s) {
     if (!s) return RT_ERR_INVALID_ARG;
     HIP_TRY(hipSetDevice(s->device));
+    // every stream-ordered render of this handle is complete after this loop, so the events
+    // are released (one per caller stream would otherwise accumulate for the process's life)
     for (auto& se : s->ev_streams) HIP_TRY(hipEventSynchronize(se.second));
+    for (auto& se : s->ev_streams) (void)hipEventDestroy(se.second);
+    s->ev_streams.clear();
     if (!s->ws.overflow) return RT_OK;
+    // read and clear the sticky word on the handle's own stream, waited for here: no null-stream
+    // operation (unordered with the callers' non-blocking streams) touches it
     uint32_t v = 0;
-    HIP_TRY(hipMemcpy(&v, s->ws.overflow + 1, sizeof(v), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(&v, s->ws.overflow + 1, sizeof(v), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
     if (!v) return RT_OK;
-    HIP_TRY(hipMemset(s->ws.overflow + 1, 0, sizeof(v)));
+    HIP_TRY(hipMemsetAsync(s->ws.overflow + 1, 0, sizeof(v), s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
     // the next pass on this scene gets a pool twice as large (up to the index limit)
     s->pool_floor = (uint32_t)std::min<uint64_t>(2ull * s->ws.capacity, pool_cap_limit(s));
     return RT_ERR_CAPACITY;
@@ -2370,14 +2265,19 @@ rt_status rt_scene_clone(const rt_scene* src, int32_t device, rt_scene** out) {
     if (!sc) return RT_ERR_OUT_OF_MEMORY;
     rt_status st = select_device(device, &sc->device);
     if (st != RT_OK) return st;
+    HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreate(&sc->ev0));
+    HIP_TRY(hipEventCreate(&sc->ev1));
     HIP_TRY(hipMalloc(&sc->dmem, src->dbytes));
     sc->dbytes = src->dbytes;
+    // on the clone's own stream and waited for: a render on any caller stream sees the copy
     if (sc->device == src->device)
-        HIP_TRY(hipMemcpy(sc->dmem, src->dmem, src->dbytes, hipMemcpyDeviceToDevice));
+        HIP_TRY(hipMemcpyAsync(sc->dmem, src->dmem, src->dbytes, hipMemcpyDeviceToDevice, sc->stream));
     else
-        HIP_TRY(hipMemcpyPeer(sc->dmem, sc->device, src->dmem, src->device, src->dbytes));
-    HIP_TRY(hipMemset((uint8_t*)sc->dmem + ((const uint8_t*)src->S.scan_ops - (const uint8_t*)src->dmem), 0,
-                      RT_OPS_SLOTS * RT_OPS_STRIDE * sizeof(unsigned long long)));
+        HIP_TRY(hipMemcpyPeerAsync(sc->dmem, sc->device, src->dmem, src->device, src->dbytes, sc->stream));
+    HIP_TRY(hipMemsetAsync((uint8_t*)sc->dmem + ((const uint8_t*)src->S.scan_ops - (const uint8_t*)src->dmem), 0,
+                           RT_OPS_SLOTS * RT_OPS_STRIDE * sizeof(unsigned long long), sc->stream));
+    HIP_TRY(hipStreamSynchronize(sc->stream));
     // the same DevScene, every pointer rebased into the new allocation
     sc->S = src->S;
     const uint8_t* from = (const uint8_t*)src->dmem;
@@ -2394,9 +2294,7 @@ rt_status rt_scene_clone(const rt_scene* src, int32_t device, rt_scene** out) {
     sc->n_point_lights = src->n_point_lights;
     sc->num_cus = g_num_cus(sc->device);
     sc->count_ops = src->count_ops;
-    HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreate(&sc->ev0));
-    HIP_TRY(hipEventCreate(&sc->ev1));
+    sc->tune = src->tune;
     *out = sc.release();
     return RT_OK;
 }
@@ -2463,12 +2361,12 @@ rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t de
     if (s->multi) return rt_multi_render(s, cam, depth, spp, seed, opts, rgb, rgb8);
     // One frame as S band shares of this device, rendered side by side on S streams (each
     // its own scene clone and workspace), exchanged by device copies and un-permuted: the
-    // latency-bound tails of one share's levels overlap the other's work.  RT_SEAM_SPLIT
-    // (default 2; 1 = one pass), RT_SEAM_BAND_ROWS (default: contiguous shares).  Config 3,
+    // latency-bound tails of one share's levels overlap the other's work.  Tune::seam_split
+    // (default 2; 1 = one pass), seam_band_rows (default: contiguous shares).  Config 3,
     // 1080p, one MI355X: 3.47 ms of device time against 4.09 for one pass (8-row bands: 3.69;
     // 3 shares: 3.80, 4: 5.08).
-    const int split = seam_split();
-    if (split > 1 && !use_megakernel() && cam->y_res >= 16u * (uint32_t)split) {
+    const int split = s->tune.seam_split;
+    if (split > 1 && cam->y_res >= 16u * (uint32_t)split) {
         if (s->split_dev_pending) {
             // a stream-ordered rt_render_frame_async on these shares is not reported yet: keep
             // its overflow for the caller's rt_scene_sync_status (this render's own status
@@ -2484,24 +2382,26 @@ rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t de
         // contiguous shares by default (top / bottom halves: 3.47 ms against 3.69 with 8-row
         // bands dealt in turn -- shares of different content fall out of step, so one share's
         // level tails meet the other's work)
-        const char* br = std::getenv("RT_SEAM_BAND_ROWS");
+        const uint32_t br = (uint32_t)s->tune.seam_band_rows;
         const uint32_t even = ((cam->y_res + (uint32_t)split - 1u) / (uint32_t)split + 7u) / 8u * 8u;
         // Two shares meet where share 1 finishes as share 0's rows reach the caller (share 0's
         // copy then runs under share 1's tail): after each render the row moves 8 rows toward
         // the share that is late on that mark (within [half, 3/4] of the frame: share 0 holds
         // one band only down to half the rows).  Config 3: share 0 (the top) is the cheaper
         // half; fixed rows 544 / 576 / 608 measured 3.38 / 3.35 / 3.37 ms of device time
-        // (RT_SEAM_BAND_ROWS pins the row, RT_SEAM_ADAPT=0 keeps the even split,
-        // RT_SEAM_ADAPT=device balances the finish times alone)
-        const char* ad = std::getenv("RT_SEAM_ADAPT");
-        const bool adapt = !br && split == 2 && !(ad && ad[0] == '0');
-        const bool adapt_copy = !(ad && std::strcmp(ad, "device") == 0);
+        // (seam_band_rows pins the row, seam_adapt=0 keeps the even split, seam_adapt=device
+        // balances the finish times alone)
+        const bool adapt = !br && split == 2 && s->tune.seam_adapt != 0;
+        const bool adapt_copy = s->tune.seam_adapt != 2;
         const uint32_t hi = std::max(even, (cam->y_res * 3u / 4u) / 8u * 8u);
         if (s->seam_y != cam->y_res || s->seam_rows < even || s->seam_rows > hi) {
             s->seam_rows = even;
             s->seam_y = cam->y_res;
-            if (adapt) {  // every share's node pool sized once for the largest share it can get
-                const uint64_t floor = std::min<uint64_t>((uint64_t)hi * cam->x_res * node_factor(), pool_cap_limit(s));
+            if (adapt && !s->tune.node_cap) {  // every share's node pool sized once for the largest
+                                                // share it can get (unless the node_cap test knob
+                                                // pins the pools)
+                const uint64_t floor = std::min<uint64_t>((uint64_t)hi * cam->x_res * (uint64_t)s->tune.node_factor,
+                                                          pool_cap_limit(s));
                 auto raise = [&](rt_scene* c) {
                     c->pool_floor = std::max<uint32_t>(c->pool_floor, (uint32_t)floor);
                     return RT_OK;
@@ -2510,14 +2410,13 @@ rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t de
                 (void)rt_multi_each(s->split, raise);
             }
         }
-        const uint32_t rows = br ? (uint32_t)std::max(1, std::atoi(br)) : (adapt ? s->seam_rows : even);
+        const uint32_t rows = br ? br : (adapt ? s->seam_rows : even);
         rt_multi_set_band_rows(s->split, rows);
-        // the shares' persistent grids at RT_SEAM_GRID_PCT % of the chip (default 80: two
+        // the shares' persistent grids at Tune::seam_grid_pct % of the chip (default 80: two
         // concurrent full-chip grids leave more blocks waiting for a slot; 100 / 90 / 80 at
         // the 576-row meeting: 3.35 / 3.31 - 3.34 / 3.30 - 3.31 ms), or the scene's own
         // share if that is smaller; restored afterwards
-        const char* gp = std::getenv("RT_SEAM_GRID_PCT");
-        const int pct = std::min(s->grid_pct, gp ? std::max(1, std::min(100, std::atoi(gp))) : 80);
+        const int pct = std::min(s->grid_pct, s->tune.seam_grid_pct);
         const int saved = s->grid_pct;
         auto set_pct = [&](int v) {
             s->grid_pct = v;
@@ -2551,16 +2450,15 @@ rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t de
     rt_status st = ensure_ws(s, n_pad, rgb8 ? n_pad : 0);
     if (st != RT_OK) return st;
     hipStream_t stream = s->stream;
-    const bool mega = use_megakernel();
     for (int attempt = 0;; attempt++) {
         HIP_TRY(hipMemsetAsync(s->ws.counters, 0, 4 * sizeof(unsigned long long), stream));
         HIP_TRY(hipEventRecord(s->ev0, stream));
         // single device: one "band" holding every row; as_u8 fused into the level-0 combine
-        const PassOut o{s->ws.out, (rgb8 && !mega) ? s->ws.out8 : nullptr, s->ws.counters, false, true};
+        const PassOut o{s->ws.out, rgb8 ? s->ws.out8 : nullptr, s->ws.counters, false, true};
         st = launch_bands(s, cam, depth, spp, seed, 8, 0, 1, o, stream);
         if (st != RT_OK) return st;
         HIP_TRY(hipEventRecord(s->ev1, stream));
-        if (mega || !s->ws.overflow) break;
+        if (!s->ws.overflow) break;
         uint32_t ovf = 0;
         HIP_TRY(hipMemcpyAsync(&ovf, s->ws.overflow, sizeof(ovf), hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
@@ -2571,7 +2469,6 @@ rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t de
         rt_status g = grow_node_pool(s->ws, (uint32_t)std::min<uint64_t>(2ull * s->ws.capacity, lim));
         if (g != RT_OK) return g;
     }
-    if (rgb8 && mega) HIP_TRY(launch_quantize(s->ws.out, n, s->ws.out8, stream));
     HIP_TRY(hipMemcpyAsync(rgb, s->ws.out, n * sizeof(float), hipMemcpyDeviceToHost, stream));
     if (rgb8) HIP_TRY(hipMemcpyAsync(rgb8, s->ws.out8, n, hipMemcpyDeviceToHost, stream));
     unsigned long long cnt[4] = {0, 0, 0, 0};
@@ -2785,12 +2682,15 @@ rt_status rt_scene_set_material(rt_scene* s, uint32_t index, const rt_material* 
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipStreamSynchronize(s->stream));
     for (auto& se : s->ev_streams) HIP_TRY(hipEventSynchronize(se.second));  // renders on other streams
-    HIP_TRY(hipMemcpy(&cur, s->S.mats + index, sizeof(cur), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(&cur, s->S.mats + index, sizeof(cur), hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
     if (m->kind != cur.kind) return RT_ERR_INVALID_ARG;  // the same kind, as the GUI's edits
     MatRec M;
     rt_status r = mat_rec(*m, M, s->normal_max);
     if (r != RT_OK) return r;
-    HIP_TRY(hipMemcpy(const_cast<MatRec*>(s->S.mats) + index, &M, sizeof(M), hipMemcpyHostToDevice));
+    // on the handle's stream, waited for: the next render on any caller stream sees the edit
+    HIP_TRY(hipMemcpyAsync(const_cast<MatRec*>(s->S.mats) + index, &M, sizeof(M), hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
     if (s->split) {
         rt_status e = rt_multi_each(s->split, [&](rt_scene* c) { return rt_scene_set_material(c, index, m); });
         if (e != RT_OK) return e;
@@ -2801,6 +2701,7 @@ rt_status rt_scene_set_material(rt_scene* s, uint32_t index, const rt_material* 
 
 }  // extern "C"
 
+#if RT_DIAG
 // debug (tools/task_clock.py): copy the trace kernel's per wave-iteration records of the
 // last RT_TASK_CLOCK render: out[0] = records written, then 4 words per record
 extern "C" int rt_debug_task_clock(uint32_t* out, uint32_t max_records) {
@@ -2811,6 +2712,7 @@ extern "C" int rt_debug_task_clock(uint32_t* out, uint32_t max_records) {
                ? 0
                : 1;
 }
+#endif
 
 // debug (tests/test_gpu_sort.py): the ray-queue radix sort on its own.  Sorts n device keys
 // (their low `bits` bits) with digits of up to max_digit bits, stably; the values (d_vals, or

@@ -18,15 +18,7 @@ constexpr int BINS = 16;
 // Retuned with light buffers and the own-shape shadow tests (the walk now serves mostly
 // trace rays): 100 / 32: 5.07; 200 / 32: 4.76; 400 / 32: 4.65; 600 / 32: 4.68;
 // 400 / 64: 4.65; 800 / 64: 4.89.
-// RT_BVH_CNODE / RT_BVH_MAXLEAF override them (A/B measurements).
-double c_node() {
-    const char* e = std::getenv("RT_BVH_CNODE");
-    return e ? std::atof(e) : 400.0;
-}
-size_t max_leaf() {
-    const char* e = std::getenv("RT_BVH_MAXLEAF");
-    return e ? (size_t)std::atoi(e) : 32;
-}
+// Tune::bvh_cnode / bvh_maxleaf override them (A/B measurements).
 
 struct Box {
     double lo[3], hi[3];
@@ -73,13 +65,14 @@ struct Cost {
 };
 
 struct Builder {
-    const double C_NODE_V = c_node();
-    const size_t MAX_LEAF_V = max_leaf();
+    const double C_NODE_V;
+    const size_t MAX_LEAF_V;
     const std::vector<Prim>& P;
     Tree& T;
     std::vector<double> cen;  // 3 per prim
 
-    Builder(const std::vector<Prim>& p, Tree& t) : P(p), T(t), cen(3 * p.size()) {
+    Builder(const std::vector<Prim>& p, Tree& t, double c_node, size_t max_leaf)
+        : C_NODE_V(c_node), MAX_LEAF_V(max_leaf), P(p), T(t), cen(3 * p.size()) {
         for (size_t i = 0; i < p.size(); i++)
             for (int k = 0; k < 3; k++) cen[3 * i + k] = 0.5 * (p[i].lo[k] + p[i].hi[k]);
     }
@@ -185,10 +178,10 @@ struct Builder {
 
 }  // namespace
 
-Tree build(const std::vector<Prim>& prims) {
+Tree build(const std::vector<Prim>& prims, double c_node, size_t max_leaf) {
     Tree T;
     if (prims.empty()) return T;
-    Builder b(prims, T);
+    Builder b(prims, T, c_node, max_leaf);
     std::vector<uint32_t> idx(prims.size());
     for (size_t i = 0; i < idx.size(); i++) idx[i] = (uint32_t)i;
     Box root;

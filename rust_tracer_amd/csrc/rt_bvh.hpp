@@ -7,6 +7,7 @@
 // own arithmetic, and the nearest hit -- including ties, broken by the shape key in
 // insertion order -- is the one Scene::intersect (scene/mod.rs:98-116) returns.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 #include <vector>
 
@@ -38,7 +39,8 @@ struct Tree {
     int depth = 0;
 };
 
-// Binned SAH (16 bins per axis) with cost model C_node + sum(area fraction * cost).
-Tree build(const std::vector<Prim>& prims);
+// Binned SAH (16 bins per axis) with cost model c_node + sum(area fraction * cost), leaves of
+// at most max_leaf primitives (Tune::bvh_cnode / bvh_maxleaf).
+Tree build(const std::vector<Prim>& prims, double c_node, std::size_t max_leaf);
 
 }  // namespace rtbvh

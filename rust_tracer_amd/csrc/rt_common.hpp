@@ -4,14 +4,15 @@
 //
 // Numerics: compiled with -ffp-contract=off, IEEE division/sqrt and f32 denormals on,
 // so every +,-,*,/,sqrt is the same correctly rounded operation the reference
-// executes, in the same order.  powf is glibc's own evaluation (rt_powf.hpp, bit-identical to
-// the reference's libm powf); atan2f / acosf (textured spheres only) come from ocml (<= 1-2 ulp).
+// executes, in the same order.  powf, atan2f and acosf are glibc's own evaluations
+// (rt_powf.hpp, rt_libmf.hpp: bit-identical to the reference's libm).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/rt_api.h"
 #include "rt_device.hpp"
+#include "rt_libmf.hpp"
 #include "rt_powf.hpp"
 // the specular power (material.rs:211): glibc's powf, bit for bit; RT_POWF_OCML=1 builds
 // ocml's powf instead (timing A/B only -- not the reference's values)
@@ -247,8 +248,9 @@ __device__ __forceinline__ Hit hit_attrs_w(const DevScene& S, const ShapeW& R, u
         h.n = n;
         if (need_sphere_tex) {  // sphere.rs:40-45
             const float PI_F = 3.14159265358979323846f;
-            h.tu = (1.f + atan2f(n.z, n.x) / PI_F) * 0.5f;
-            h.tv = acosf(n.y) / PI_F;
+            // glibc's atan2f / acosf (rt_libmf.hpp), as Rust's f32::atan2 / f32::acos call
+            h.tu = (1.f + rtlibm::atan2f_fd(n.z, n.x) / PI_F) * 0.5f;
+            h.tv = rtlibm::acosf_fd(n.y) / PI_F;
         }
     } else if (kind == RT_SHAPE_PLANE) {
         V3 to = pt_mul(r0, r1, r2, o);

@@ -1,5 +1,5 @@
 // rt_device.hpp -- device-side scene layout shared by the host builder (rt_api.cpp) and
-// the HIP kernels (rt_kernels.hip).
+// the HIP kernels (rt_wavefront.hip, rt_order.hip, rt_frame.hip).
 //
 // The scene lives in ONE device allocation, cut into per-type runs so the hot
 // nearest-hit scan walks each run with wave-uniform indices (the loads become scalar
@@ -137,20 +137,6 @@ enum : int {
 #define RT_WORK_WORD(k) (RT_LEVEL_WORDS + (k))  // k: level, or RT_MAX_DEPTH + 1: shadow pass
 #define RT_LEVEL_TABLE_WORDS (RT_LEVEL_WORDS + RT_MAX_DEPTH + 2)
 
-// Everything one launch needs.
-struct RenderParams {
-    DevScene S;
-    float cam_ox, cam_oy, cam_oz;
-    float x_min, y_max, x_delta, y_delta;   // render.rs:178-185, deltas computed on the host
-    uint32_t width, height;                 // full frame
-    uint32_t depth;
-    uint32_t band_rows, rank, world, rows_local;  // this launch's rows: see rt_render_bands_async
-    uint32_t tiles_x, total_items;          // 8x8 pixel tiles over (width x rows_local)
-    float* out;                             // rows_local * width * 3 floats
-    unsigned long long* ray_counters;       // [node, shadow, pixels], added to
-    unsigned long long* iter_counter;       // optional: wave loop iterations (lane utilisation)
-    uint32_t* work_counter;                 // zeroed before the launch
-};
 
 // ---- level-synchronous ("wavefront") pipeline, rt_wavefront.hip ----------------------
 // A ray task of tree level k >= 1 (level-0 tasks are the pixels themselves).
@@ -263,6 +249,10 @@ struct WaveParams {
     uint32_t reverse_levels;           // bit k: level k's queue is traced from its end (A/B, RT_REVERSE)
     uint32_t task_w_min;               // narrowest trace task (rays per wave iteration; 64 = never narrowed)
     float task_w_fill;                 // trace tasks are narrowed while a level has fewer than fill x wave slots of them
+    // host-side launch choices (Tune, rt_wavefront.hip's launchers): walk records staged in LDS
+    // (bit 0 trace kernels, bit 1 shadow kernel), the deep-level trace instantiation, grids
+    // per instantiation's own occupancy
+    uint32_t lds_mask, deep_kernel, occ_each;
 };
 
 // 15-bit Morton code of a point in the 32^3 grid over [c - r, c + r]^3 (clamped)

@@ -6,12 +6,15 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/rt_api.h"
+#include "rt_tune.hpp"
 
 struct rt_multi_state;
 
 // The multi-device state a primary scene handle carries (null: a one-device scene).
 rt_multi_state*& rt_scene_multi(rt_scene* s);
 int rt_scene_device_of(const rt_scene* s);
+// The handle's tuning (rt_tune.hpp).
+const Tune& rt_scene_tune(const rt_scene* s);
 
 // rt_render_spp on a multi-device scene (rt_multi.cpp).
 rt_status rt_multi_render(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,

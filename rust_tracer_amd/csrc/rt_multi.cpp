@@ -357,15 +357,12 @@ rt_status rt_multi_render_frame_async(rt_multi_state* m, const rt_camera* cam, u
     m->direct = true;
     MHIP(hipSetDevice(m->devices[0]));
     // Both shares fork onto the state's streams (share r always on streams[r], so calls from
-    // any caller streams stay ordered on each share's workspace).  RT_FRAME_FORK=caller (A/B):
+    // any caller streams stay ordered on each share's workspace).  Tune::frame_fork=caller (A/B):
     // share 0 on the caller's stream itself, only share 1 forked -- 3.41 / 3.40 ms vs 3.52 /
     // 3.85, config 3 at 1080p on a created caller stream.  On the legacy null stream the fork
     // and join measured 5.3 - 5.4 ms once other streams and rt_render's shares existed in the
     // process: pass a created stream.
-    static const bool on_caller = [] {
-        const char* e = std::getenv("RT_FRAME_FORK");
-        return e && std::strcmp(e, "caller") == 0;
-    }();
+    const bool on_caller = rt_scene_tune(m->ranks[0]).frame_fork == 1;
     // share 0 renders on rank 0's workspace: after the previous call's share 0, whatever
     // stream that call came from (share 1 is ordered by the state's own stream)
     if (on_caller && m->frame_async) MHIP(hipStreamWaitEvent(stream, m->done[0], 0));
@@ -505,10 +502,10 @@ rt_status rt_scene_create_multi(const rt_scene_desc* desc, const int32_t* device
         if (devices[r] < 0 || devices[r] >= n_visible) return RT_ERR_INVALID_ARG;
     rt_scene* s0 = nullptr;
     rt_status st = rt_scene_create(desc, devices[0], &s0);
-    // RT_FORCE_RCCL=1: one device still renders through the band render + ncclGather (a
-    // one-rank communicator) + un-permute, so a one-GPU machine executes the RCCL exchange
-    const char* force = std::getenv("RT_FORCE_RCCL");
-    const bool force_rccl = force && force[0] == '1';
+    // Tune::force_rccl (RT_TUNE="force_rccl=1"): one device still renders through the band
+    // render + ncclGather (a one-rank communicator) + un-permute, so a one-GPU machine
+    // executes the RCCL exchange
+    const bool force_rccl = st == RT_OK && rt_scene_tune(s0).force_rccl != 0;
     if (st != RT_OK || (n_devices == 1 && !force_rccl)) {
         *out = s0;
         return st;

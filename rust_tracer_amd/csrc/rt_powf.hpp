@@ -11,7 +11,13 @@
 // breaks the 1e-4 parity bound, so the device replays glibc's evaluation exactly: same
 // tables (glibc 2.35's __powf_log2_data / __exp2f_data, located in libm by
 // tools/extract_powf_tables.py), same double operations in the same order, fma where the
-// FMA build fuses.  tests/test_powf.py checks it against the host's powf bit for bit.
+// FMA build fuses.  tests/test_libm.py checks it against the host's powf bit for bit.
+//
+// Upstream: glibc's powf comes from Arm's optimized-routines (math/powf.c, powf_log2_data.c,
+// exp2f_data.c), Copyright (c) 2017-2018, Arm Limited, SPDX-License-Identifier: MIT OR
+// Apache-2.0 WITH LLVM-exception; it is distributed in glibc under the LGPL-2.1-or-later.
+// The algorithm, operation order and table values below are restated from that published
+// code (the tables read back from the system libm by value, tools/extract_powf_tables.py).
 #pragma once
 #include <stdint.h>
 #include <string.h>

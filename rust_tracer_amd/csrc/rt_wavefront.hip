@@ -15,7 +15,8 @@
 //                   colours the children reported; the result goes to the parent's slot,
 //                   level 0 writes the pixel.
 //
-// Why levels and not one per-pixel megakernel (rt_kernels.hip): per-pixel ray trees are
+// Why levels and not one per-pixel megakernel (round 1's design, 68 ms per frame; removed in
+// round 4, git history): per-pixel ray trees are
 // ragged (median 1 node, p99 31, max > 80 at depth 8 in config 3), so a lane that owns a
 // pixel serialises up to ~350 scans while the average lane has ~110: the frame becomes
 // critical-path bound.  Here every queue entry costs one scan, lanes stay full, and the
@@ -1130,17 +1131,16 @@ hipError_t launch_wave_init(uint32_t* levels, uint32_t n_words, uint32_t total_i
 // The walk kernels' LDS variant stages the hierarchy's node records, the grazing pairs'
 // normals and the hierarchy's sphere pairs when they fit in 32 KB (five 256-thread blocks
 // per CU, the trace kernel's VGPR limit; config 3 stages 22.5 KB, which leaves the shadow
-// kernel its six); RT_LDS_NODES=0: never, =trace / =shadow: only that kernel (A/B).  The
+// kernel its six); Tune::lds_nodes=0: never, =trace / =shadow: only that kernel (A/B).  The
 // hierarchy's triangle pairs staged as well (27.9 KB; records from LDS in VGPRs instead of
 // SGPRs, shadow kernel down to five blocks) lost 7.5%: 865 / 867 / 862 vs 936 / 932 / 933.
 static size_t lds_bytes(const WaveParams& p) {
     return (size_t)p.S.n_bvh_nodes * 64 + ((p.S.graze_lane && p.S.graze_res) ? (size_t)p.S.n_graze_blk * 128 : 0) +
            (size_t)p.S.n_dsph_bvh * 64;
 }
-static bool lds_nodes_for(const WaveParams& p, const char* kernel) {
+static bool lds_nodes_for(const WaveParams& p, uint32_t kernel_bit) {
     size_t lds = lds_bytes(p);
-    const char* e = getenv("RT_LDS_NODES");
-    if (e && (e[0] == '0' || (std::strcmp(e, "1") != 0 && std::strcmp(e, kernel) != 0))) return false;
+    if (!(p.lds_mask & kernel_bit)) return false;
     return p.S.use_bvh && lds > 0 && lds <= 32 * 1024;
 }
 
@@ -1149,10 +1149,10 @@ static bool lds_nodes_for(const WaveParams& p, const char* kernel) {
 hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_blocks, int* combine_blocks,
                           int* trace_each) {
     const size_t lds = lds_bytes(p);
-    const bool aware = !getenv("RT_OCC_NOLDS");  // A/B: size the grids as if no LDS were used
+    const bool aware = true;  // (grids sized as if no LDS were used: blocks waited for a slot)
     // every trace instantiation launch_wave_trace may pick (generic, level 0, deep levels):
     // the grid is sized by the least occupancy among them, so every block is resident
-    const bool tl = aware && lds_nodes_for(p, "trace");
+    const bool tl = aware && lds_nodes_for(p, 1u);
     int tv[3] = {0, 0, 0};
     hipError_t e =
         tl ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&tv[0], trace_level_kernel<false, true>, 256, lds)
@@ -1167,14 +1167,16 @@ hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_bl
     *trace_blocks = std::min(tv[0], std::min(tv[1], tv[2]));
     if (trace_each)
         for (int i = 0; i < 3; i++) trace_each[i] = tv[i];
-    e = aware && lds_nodes_for(p, "shadow")
+    e = aware && lds_nodes_for(p, 2u)
             ? hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<true, false>, 256, lds)
             : hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<false, false>, 256, 0);
     if (e != hipSuccess) return e;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(combine_blocks, combine_level_kernel, 256, 0);
+#if RT_DIAG
     if (getenv("RT_OCC_DEBUG"))
         fprintf(stderr, "rt occupancy: lds %zu B (nodes %d, graze blocks %d, sphere pairs %d, tri pairs %d); blocks per CU trace %d shadow %d combine %d\n",
                 lds, p.S.n_bvh_nodes, p.S.n_graze_blk, p.S.n_dsph_bvh, p.S.n_tri_bvh, *trace_blocks, *shadow_blocks, *combine_blocks);
+#endif
     return e;
 }
 
@@ -1184,12 +1186,12 @@ hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_bl
 hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream,
                              const int* occ_each, int occ_min) {
     const size_t lds = lds_bytes(p);
-    const bool use = lds_nodes_for(p, "trace");
-    // the deep instantiation past level 0 and the inline shadow levels (RT_DEEP_KERNEL=0: never, A/B)
-    static const bool deep_ok = !(getenv("RT_DEEP_KERNEL") && getenv("RT_DEEP_KERNEL")[0] == '0');
+    const bool use = lds_nodes_for(p, 1u);
+    // the deep instantiation past level 0 and the inline shadow levels (deep_kernel=0: never, A/B)
+    const bool deep_ok = p.deep_kernel != 0;
     const bool deep = deep_ok && level > 0 && level >= p.inline_levels && !(p.count_mask & 1u);
-    // RT_OCC_EACH=1 (A/B builds whose instantiations differ in occupancy, e.g. RT_FIRST_WAVES)
-    static const bool occ_each_on = getenv("RT_OCC_EACH") && getenv("RT_OCC_EACH")[0] == '1';
+    // occ_each=1 (A/B builds whose instantiations differ in occupancy, e.g. RT_FIRST_WAVES)
+    const bool occ_each_on = p.occ_each != 0;
     if (occ_each_on && occ_each && occ_min > 0 && !(p.count_mask & 1u)) {
         const int v = (level == 0 && deep_ok) ? 1 : (deep ? 2 : 0);
         if (occ_each[v] > occ_min) blocks = (int)((long long)blocks * occ_each[v] / occ_min);
@@ -1220,7 +1222,7 @@ hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hi
 
 hipError_t launch_wave_shadow(const WaveParams& p, int blocks, hipStream_t stream) {
     const size_t lds = lds_bytes(p);
-    const bool use = lds_nodes_for(p, "shadow");
+    const bool use = lds_nodes_for(p, 2u);
     const bool count = (p.count_mask & 2u) != 0;
     if (use && count)
         hipLaunchKernelGGL((shadow_kernel<true, true>), dim3(blocks), dim3(256), lds, stream, p);

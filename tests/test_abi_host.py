@@ -152,3 +152,24 @@ def test_multi_device_scene_needs_devices():
     assert L.rt_scene_device_count(None) == 0
     assert L.rt_status_str(abi.RT_ERR_CAPACITY) == b"RT_ERR_CAPACITY"
     assert L.rt_scene_sync_status(None) == 1
+
+
+def test_tuning_strings_are_validated_on_the_host():
+    """rt_scene_create_tuned parses its tuning string (rt_tune.hpp) before it touches a
+    device: an unknown key, a bad value or a malformed pair is RT_ERR_INVALID_ARG; a valid
+    string gets as far as the device (RT_ERR_NO_DEVICE here).  The environment's RT_TUNE is
+    parsed the same way."""
+    L = abi.lib()
+    desc = rt.SceneDesc.my_scene()
+    h = C.c_void_p()
+    gpu = L.rt_scene_create(desc.ptr(), 0, C.byref(h)) == abi.RT_OK
+    if gpu:
+        L.rt_scene_destroy(h)
+        pytest.skip("a HIP device is present: the valid strings would create scenes")
+    for bad in (b"bogus=1", b"lb_res", b"lb_res=x", b"task_w=48", b"sort=maybe", b"seam_split=0",
+                b"shadow_key=17", b"=3"):
+        assert L.rt_scene_create_tuned(desc.ptr(), 0, bad, C.byref(h)) == abi.RT_ERR_INVALID_ARG, bad
+    for good in (b"", b"lb_res=0,bvh=0", b"task_w=32 task_fill=2.5", b"sort=shadow,dup=shc",
+                 b"shadow_key=cell,frame_keys=frame,spp_keys=mix", b"lds_nodes=trace,seam_adapt=device",
+                 b"force_rccl=1,node_cap=4096", b"graze_k=3e-3,bvh_cnode=200,bvh_maxleaf=16"):
+        assert L.rt_scene_create_tuned(desc.ptr(), 0, good, C.byref(h)) == abi.RT_ERR_NO_DEVICE, good

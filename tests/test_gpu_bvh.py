@@ -1,7 +1,7 @@
 """The culling hierarchy (rt_bvh, DESIGN.md "Exact culling") must change nothing.
 
 Every frame rendered with the hierarchy (the default) is compared BIT FOR BIT, with its
-ray counters, against the same frame rendered with RT_BVH=0 (every ray tests every
+ray counters, against the same frame rendered with tuning bvh=0 (every ray tests every
 shape, the reference's Scene::intersect loop), and against the CPU oracle where the
 oracle finishes in seconds.  The scenes include the adversarial cases of the error
 bounds: rays lying in / grazing triangle planes and cube faces, far-away tiny spheres
@@ -22,12 +22,7 @@ pytestmark = pytest.mark.gpu
 
 
 def render(desc, w, h, depth, bvh=True):
-    if not bvh:
-        os.environ["RT_BVH"] = "0"
-    try:
-        s = DeviceScene(desc)
-    finally:
-        os.environ.pop("RT_BVH", None)
+    s = DeviceScene(desc, tuning=None if bvh else "bvh=0")
     try:
         assert s.uses_bvh == bvh or (bvh and desc.n_shapes == 0)
         s.set_scan_counting(True)
@@ -147,21 +142,13 @@ def test_counting_kernels_render_the_same_frame():
     assert ca == cb == cc
 
 
-def _render_env(desc, w, h, depth, **env):
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update({k: str(v) for k, v in env.items()})
+def _render_env(desc, w, h, depth, **tune):
+    """One render of a handle created with the given tuning keys (rt_tune.hpp)."""
+    s = DeviceScene(desc, tuning=tune or None)
     try:
-        s = DeviceScene(desc)
-        try:
-            img, cnt, _, _ = s.render(w, h, depth)
-        finally:
-            s.close()
+        img, cnt, _, _ = s.render(w, h, depth)
     finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        s.close()
     return img, cnt
 
 
@@ -182,19 +169,19 @@ def _lights_in_the_cluster():
 
 @pytest.mark.parametrize("scene", ["config3", "grazing", "lights_in_cluster", "random"])
 def test_shadow_shortcuts_change_nothing(scene):
-    """Light buffers at several resolutions (RT_LB_RES, 0 = off), the trace kernel's
-    own-shape shadow tests (RT_SELF_SHADOW=0 = off), inline shadow rays (RT_INLINE_SHADOW:
-    levels traced inline) and the grazing pass's direction cells (RT_GRAZE_RES, 0 = cone
-    path): bit-identical frames and counters."""
+    """Light buffers at several resolutions (lb_res, 0 = off), the trace kernel's own-shape
+    shadow tests (self_shadow=0 = off), inline shadow rays (inline_shadow: levels traced
+    inline) and the grazing pass's direction cells (graze_res, 0 = cone path): bit-identical
+    frames and counters."""
     desc = {"config3": lambda: SceneDesc.synth_config(3), "grazing": _grazing_scene,
             "lights_in_cluster": _lights_in_the_cluster,
             "random": lambda: SceneDesc.synth(31, 400, 30, 120, 0.03, 0.5)}[scene]()
     w, h, depth = 480, 270, 8
-    base, cb = _render_env(desc, w, h, depth, RT_LB_RES=0, RT_SELF_SHADOW=0)
-    for env in ({}, {"RT_LB_RES": 8}, {"RT_LB_RES": 64}, {"RT_LB_RES": 200}, {"RT_SELF_SHADOW": 0},
-                {"RT_INLINE_SHADOW": 0}, {"RT_INLINE_SHADOW": 8, "RT_LB_RES": 16}, {"RT_GRAZE_RES": 0},
-                {"RT_GRAZE_RES": 8}, {"RT_LB_REACH": 0}, {"RT_LB_REACH": 0, "RT_LB_RES": 128},
-                {"RT_TASK_W": 16, "RT_TASK_FILL": 64}):
+    base, cb = _render_env(desc, w, h, depth, lb_res=0, self_shadow=0)
+    for env in ({}, {"lb_res": 8}, {"lb_res": 64}, {"lb_res": 200}, {"self_shadow": 0},
+                {"inline_shadow": 0}, {"inline_shadow": 8, "lb_res": 16}, {"graze_res": 0},
+                {"graze_res": 8}, {"lb_reach": 0}, {"lb_reach": 0, "lb_res": 128},
+                {"task_w": 16, "task_fill": 64}):
         img, cnt = _render_env(desc, w, h, depth, **env)
         diff = np.flatnonzero(img.view(np.uint32) != base.view(np.uint32))
         assert diff.size == 0, (env, diff.size)

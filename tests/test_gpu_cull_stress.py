@@ -7,7 +7,7 @@ bounds where the benchmark scenes do not: world scales x0.01 / x100 / x1000 (wit
 reference's absolute 0.0002 offsets and absolute light-buffer radii), cameras far from the
 scene and inside it, point lights within 0.05 of a primitive (no light buffer), sliver
 triangles (sin(angle) ~ 1e-3, linear-scan candidates), anisotropic rotated spheres,
-duplicate shapes.  Each is rendered with the hierarchy and with RT_BVH=0 (every shape
+duplicate shapes.  Each is rendered with the hierarchy and with tuning bvh=0 (every shape
 tested for every ray): frames and ray counters must be identical bit for bit; and at a
 small size against the CPU oracle.
 """
@@ -113,8 +113,7 @@ def test_hierarchy_is_exact_under_stress(seed, scale, cam_mode, near, slivers, m
     assert s.uses_bvh
     img, cnt, _, _ = s.render(w, h, depth, cam=cam)
     s.close()
-    monkeypatch.setenv("RT_BVH", "0")
-    s = DeviceScene(desc, device=0)
+    s = DeviceScene(desc, device=0, tuning="bvh=0")
     assert not s.uses_bvh
     ref, rcnt, _, _ = s.render(w, h, depth, cam=cam)
     s.close()
@@ -144,7 +143,7 @@ def test_stress_scenes_match_oracle(seed, scale, cam_mode, near, slivers):
 def test_shape_buffers_change_nothing(case, monkeypatch):
     """Rays inside a sphere test its shape buffer instead of walking the hierarchy (rt_api.cpp
     build_shape_buffers): frames and counters identical to the walk (RT_SHAPE_BUF=0) and to
-    the key mode without inside rays (RT_TASK_KEY=6)."""
+    the key mode without inside rays (task_key=6)."""
     if case is None:
         desc, w, h, depth, cam = SceneDesc.synth_config(3), 480, 270, 8, None
     else:
@@ -152,12 +151,8 @@ def test_shape_buffers_change_nothing(case, monkeypatch):
         desc, w, h, depth = stress_scene(seed, scale, near, slivers), 160, 120, 8
         cam = stress_camera(w, h, scale, cam_mode)
     out = []
-    for env in ({}, {"RT_SHAPE_BUF": "0"}, {"RT_TASK_KEY": "6"}):
-        for k in ("RT_SHAPE_BUF", "RT_TASK_KEY"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        s = DeviceScene(desc, device=0)
+    for tune in (None, "shape_buf=0", "task_key=6"):
+        s = DeviceScene(desc, device=0, tuning=tune)
         out.append(s.render(w, h, depth, cam=cam)[:2])
         s.close()
     for img, cnt in out[1:]:
@@ -172,8 +167,7 @@ def test_shadow_queue_order_changes_nothing(key, monkeypatch):
     s = DeviceScene(desc, device=0)
     ref, rcnt, _, _ = s.render(320, 180, 8)
     s.close()
-    monkeypatch.setenv("RT_SHADOW_KEY", key)
-    s = DeviceScene(desc, device=0)
+    s = DeviceScene(desc, device=0, tuning=f"shadow_key={key}")
     img, cnt, _, _ = s.render(320, 180, 8)
     s.close()
     assert same_bits(img, ref) and cnt == rcnt

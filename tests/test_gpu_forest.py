@@ -124,11 +124,7 @@ def test_forest_material_edit_affects_renders_too():
 def test_forest_bvh_off_identical():
     desc = SceneDesc.synth_config(3)
     a = DeviceScene(desc).forest(200, 112, 8).render()
-    os.environ["RT_BVH"] = "0"
-    try:
-        s = DeviceScene(desc)
-    finally:
-        os.environ.pop("RT_BVH", None)
+    s = DeviceScene(desc, tuning="bvh=0")
     b = s.forest(200, 112, 8).render()
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 

@@ -105,8 +105,7 @@ def test_frame_async_overflow_is_reported(monkeypatch):
     full = DeviceScene(desc, device=0)
     ref, rcnt, _, _ = full.render(w, h, 8)
     full.close()
-    monkeypatch.setenv("RT_NODE_CAP", str(w * h // 2 + 4096))
-    s = DeviceScene(desc, device=0)
+    s = DeviceScene(desc, device=0, tuning=f"node_cap={w * h // 2 + 4096}")
     d = Dev(w, h)
     d.render(s, 8, want8=False)
     with pytest.raises(RtError) as e:

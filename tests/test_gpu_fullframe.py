@@ -80,3 +80,29 @@ def test_config4_every_fourth_row():
     assert nan_ok, msg
     assert worst <= TOL, msg
     assert exact > 0.99, msg
+
+
+def test_textured_spheres_every_pixel():
+    """Config 3 with every 5th shape that is a sphere given a checkerboard TexturePhong
+    material (a reflective one and a refractive one alternating): sphere texture coordinates
+    u = (1 + atan2(n.z, n.x) / PI) * 0.5, v = acos(n.y) / PI (sphere.rs:40-45) feed the
+    checkerboard's integer truncation (my_scene.rs:26-43), so one ulp of atan2f / acosf flips
+    a texel.  The device evaluates glibc's own atan2f / acosf (rt_libmf.hpp): every pixel
+    against the oracle (host libm), counters equal."""
+    from rust_tracer_amd.abi import RT_SHAPE_SPHERE
+    desc = SceneDesc.synth_config(3).editable()
+    mirror = desc.texture_phong((0.1, 0.1, 0.1), "checkerboard", (1.0, 1.0, 1.0), 60.0, 0.3, 0.0)
+    glass = desc.texture_phong((0.05, 0.05, 0.05), "checkerboard", (1.0, 1.0, 1.0), 200.0, 0.1, 1.5)
+    spheres = [i for i, sh in enumerate(desc.shapes) if sh.kind == RT_SHAPE_SPHERE]
+    for k, i in enumerate(spheres[::5]):
+        desc.shapes[i].material = mirror if k % 2 == 0 else glass
+    s = DeviceScene(desc, device=0)
+    img, cnt, _, _ = s.render(1920, 1080, 8)
+    s.close()
+    ref, rcnt = OracleScene(desc).render(1920, 1080, 8, threads=host_threads())
+    worst, exact, nan_ok, msg = report(img, ref)
+    print(f"textured config 3 ({len(spheres[::5])} textured spheres): {msg}; counters {cnt}")
+    assert nan_ok, msg
+    assert worst <= TOL, msg
+    assert exact > 0.99, msg
+    assert cnt == rcnt, (cnt, rcnt)

@@ -3,7 +3,7 @@
 - multi-device scenes (rt_scene_create_multi): the frame tiled over ranks, gathered and
   un-permuted, equals the one-device rt_render bit for bit -- with one GPU listed 2 / 3 times
   (band shares exchanged by device copies: the multi-rank band logic on a one-GPU box), and
-  with RT_FORCE_RCCL=1 and one device: a one-rank RCCL communicator (ncclCommInitAll), the
+  with tuning force_rccl=1 and one device: a one-rank RCCL communicator (ncclCommInitAll), the
   grouped ncclGather and the un-permute kernel really execute on the one-GPU box;
 - bench.py under torchrun --nproc-per-node 1 --backend nccl --force-gather 1: the
   process-group path's RCCL gather (torch.distributed over RCCL) with frame_check;
@@ -50,7 +50,7 @@ def test_multi_device_scene_equals_single(devices):
     single.close()
     multi = DeviceScene(desc, devices=devices)
     assert multi.device_count == len(devices)
-    # without RT_FORCE_RCCL, one device is a plain scene and a repeated device exchanges
+    # without force_rccl, one device is a plain scene and a repeated device exchanges
     # bands by device copies: no RCCL
     assert not multi.uses_rccl
     img, cnt, ms, img8 = multi.render(w, h, depth, want_u8=True)
@@ -64,7 +64,7 @@ def test_multi_device_scene_equals_single(devices):
 
 @pytest.mark.parametrize("w,h", [(320, 180), (3840, 2160)])
 def test_forced_rccl_one_rank(monkeypatch, w, h):
-    """RT_FORCE_RCCL=1 with devices=[0]: rt_scene_create_multi builds a one-rank RCCL
+    """Tuning force_rccl=1 (RT_TUNE) with devices=[0]: rt_scene_create_multi builds a one-rank RCCL
     communicator, and rt_render runs the band render, the grouped ncclGather (rt_multi.cpp)
     and the un-permute kernel.  Config 3 at 320x180 and the whole config 4 frame (3840x2160,
     depth 8) equal the one-device rt_render bit for bit (render.rs:32-37 tiled)."""
@@ -72,7 +72,7 @@ def test_forced_rccl_one_rank(monkeypatch, w, h):
     single = DeviceScene(desc, device=0)
     ref, rcnt, _, ref8 = single.render(w, h, 8, want_u8=True)
     single.close()
-    monkeypatch.setenv("RT_FORCE_RCCL", "1")
+    monkeypatch.setenv("RT_TUNE", "force_rccl=1")
     multi = DeviceScene(desc, devices=[0])
     assert multi.uses_rccl and multi.device_count == 1
     img, cnt, ms, img8 = multi.render(w, h, 8, want_u8=True)
@@ -91,8 +91,7 @@ def test_forced_rccl_overflow_rerenders(monkeypatch):
     single = DeviceScene(desc, device=0)
     ref, rcnt, _, _ = single.render(256, 144, 8)
     single.close()
-    monkeypatch.setenv("RT_FORCE_RCCL", "1")
-    monkeypatch.setenv("RT_NODE_CAP", str(256 * 144 + 4096))
+    monkeypatch.setenv("RT_TUNE", f"force_rccl=1,node_cap={256 * 144 + 4096}")
     multi = DeviceScene(desc, devices=[0])
     assert multi.uses_rccl
     img, cnt, _, _ = multi.render(256, 144, 8)
@@ -126,10 +125,18 @@ def test_pipeline_overflow_is_raised(monkeypatch):
     from rust_tracer_amd.dist import FramePipeline
     desc = SceneDesc.synth_config(3)
     w, h, depth = 192, 108, 8
-    s = DeviceScene(desc, device=0)
-    ref, _, _, _ = s.render(w, h, depth)
-    monkeypatch.setenv("RT_NODE_CAP", str(w * h + 1024))
+    ref_scene = DeviceScene(desc, device=0)
+    ref, _, _, _ = ref_scene.render(w, h, depth)
+    ref_scene.close()
+    s = DeviceScene(desc, device=0, tuning=f"node_cap={w * h + 1024}")  # the clones copy it
     pipe = FramePipeline(s, desc, w, h, depth, inflight=2, batch=1)
+    pipe.run(2)
+    torch.cuda.synchronize()
+    # every slot's pass overflowed and each reports it (rt_scene_sync_status per slot)
+    for t in pipe.tilers:
+        with pytest.raises(RtError) as e:
+            t.scene.sync_status()
+        assert e.value.status == abi.RT_ERR_CAPACITY
     pipe.run(2)
     with pytest.raises(RtError) as e:
         pipe.frames()
@@ -141,7 +148,6 @@ def test_pipeline_overflow_is_raised(monkeypatch):
             break
         except RtError as e:
             assert e.status == abi.RT_ERR_CAPACITY
-    assert attempt >= 1
     assert len(frames) == 2 and all(same_bits(f.cpu().numpy(), ref) for f in frames)
     pipe.close()
     assert s.grid_share == 100  # the caller's scene gets its grid share back
@@ -198,8 +204,7 @@ def test_overflow_is_reported_not_truncated(monkeypatch):
     full = DeviceScene(desc, device=0)
     ref, rcnt, _, _ = full.render(w, h, depth)
     full.close()
-    monkeypatch.setenv("RT_NODE_CAP", str(w * h + 4096))  # level 0 plus a sliver
-    s = DeviceScene(desc, device=0)
+    s = DeviceScene(desc, device=0, tuning=f"node_cap={w * h + 4096}")  # level 0 plus a sliver
     _band_render(s, w, h, depth, 0, 1)
     with pytest.raises(RtError) as e:
         s.sync_status()
@@ -209,7 +214,6 @@ def test_overflow_is_reported_not_truncated(monkeypatch):
     img, cnt, _, _ = s.render(w, h, depth)
     assert same_bits(img, ref) and cnt == rcnt
     s.close()
-    monkeypatch.delenv("RT_NODE_CAP")
     s = DeviceScene(desc, device=0)
     _band_render(s, w, h, depth, 0, 1)
     s.sync_status()  # default pool: no overflow
@@ -322,14 +326,13 @@ def _axis_scene():
 @pytest.mark.parametrize("name", ["config3", "my_scene", "axis"])
 def test_shadowed_light_skip_is_exact(name, monkeypatch):
     """The combine pass skips shadowed point lights (their term is exactly +-0, light_sum):
-    frames equal the full evaluation bit for bit (RT_NO_DARK_SKIP=1), NaNs included."""
+    frames equal the full evaluation bit for bit (tuning dark_skip=0), NaNs included."""
     desc = {"config3": lambda: SceneDesc.synth_config(3), "my_scene": SceneDesc.my_scene, "axis": _axis_scene}[name]()
     w, h = (256, 144) if name == "config3" else (64, 64)
     s = DeviceScene(desc, device=0)
     img, cnt, _, _ = s.render(w, h, 8)
     s.close()
-    monkeypatch.setenv("RT_NO_DARK_SKIP", "1")
-    s = DeviceScene(desc, device=0)
+    s = DeviceScene(desc, device=0, tuning="dark_skip=0")
     ref, rcnt, _, _ = s.render(w, h, 8)
     s.close()
     assert same_bits(img, ref) and cnt == rcnt
@@ -359,7 +362,7 @@ def _scaled_plane_scene():
 
 def test_scaled_plane_normal_high_power():
     """Shadowed light on a plane with |transform * n| = 2 and power 500: NaN / inf exactly as
-    the oracle and as the full evaluation (RT_NO_DARK_SKIP=1)."""
+    the oracle and as the full evaluation (tuning dark_skip=0)."""
     desc = _scaled_plane_scene()
     w, h = 96, 96
     s = DeviceScene(desc, device=0)
@@ -371,8 +374,9 @@ def test_scaled_plane_normal_high_power():
     nan_g, nan_r = np.isnan(img), np.isnan(ref)
     assert np.array_equal(nan_g, nan_r)
     eq = img.view(np.uint32) == ref.view(np.uint32)
-    d = np.abs(img.astype(np.float64) - ref.astype(np.float64))
-    d[eq | (nan_g & nan_r)] = 0.0
+    differ = ~(eq | (nan_g & nan_r))  # masked before subtracting (equal infinities: inf - inf)
+    d = np.zeros(img.shape)
+    d[differ] = np.abs(img[differ].astype(np.float64) - ref[differ].astype(np.float64))
     assert float(d.max()) <= TOL
 
 
@@ -452,19 +456,15 @@ def test_torchrun_two_ranks_rgb8_gather():
 @pytest.mark.parametrize("split,rows", [(2, None), (3, None), (2, "8"), (4, "16")])
 def test_seam_split_changes_nothing(monkeypatch, split, rows):
     """rt_render on a one-device scene renders the frame as `split` band shares side by side
-    (RT_SEAM_SPLIT, contiguous shares by default, RT_SEAM_BAND_ROWS otherwise): frames, RGB8
-    and counters equal the single pass (RT_SEAM_SPLIT=1) bit for bit, including a frame too
+    (seam_split, contiguous shares by default, seam_band_rows otherwise): frames, RGB8
+    and counters equal the single pass (seam_split=1) bit for bit, including a frame too
     small to split and a ragged height; the share handles follow a material edit."""
     desc = SceneDesc.synth_config(3)
     sizes = [(320, 181), (96, 20)]
-    monkeypatch.setenv("RT_SEAM_SPLIT", "1")
-    s = DeviceScene(desc, device=0)
+    s = DeviceScene(desc, device=0, tuning="seam_split=1")
     refs = [s.render(w, h, 8, want_u8=True) for w, h in sizes]
     s.close()
-    monkeypatch.setenv("RT_SEAM_SPLIT", str(split))
-    if rows:
-        monkeypatch.setenv("RT_SEAM_BAND_ROWS", rows)
-    s = DeviceScene(desc, device=0)
+    s = DeviceScene(desc, device=0, tuning=f"seam_split={split}" + (f",seam_band_rows={rows}" if rows else ""))
     for (w, h), (ref, rcnt, _, ref8) in zip(sizes, refs):
         img, cnt, ms, img8 = s.render(w, h, 8, want_u8=True)
         assert same_bits(img, ref) and np.array_equal(img8, ref8) and cnt == rcnt, (w, h)
@@ -474,8 +474,7 @@ def test_seam_split_changes_nothing(monkeypatch, split, rows):
     s.set_material(0, m)
     img, cnt, _, _ = s.render(320, 181, 8)
     s.close()
-    monkeypatch.setenv("RT_SEAM_SPLIT", "1")
-    one = DeviceScene(desc, device=0)
+    one = DeviceScene(desc, device=0, tuning="seam_split=1")
     one.set_material(0, m)
     ref, rcnt, _, _ = one.render(320, 181, 8)
     one.close()
@@ -484,20 +483,15 @@ def test_seam_split_changes_nothing(monkeypatch, split, rows):
 
 def test_adaptive_seam_split_changes_nothing(monkeypatch):
     """rt_render's two band shares meet at a row that follows their finish times (moved 8 rows
-    per render within [half, 3/4] of the frame, RT_SEAM_ADAPT) and run their grids at a
-    reduced share of the chip (RT_SEAM_GRID_PCT): every one of a run of renders -- whatever
+    per render within [half, 3/4] of the frame, seam_adapt) and run their grids at a
+    reduced share of the chip (seam_grid_pct): every one of a run of renders -- whatever
     row the shares meet at -- equals the single pass bit for bit, RGB8 and counters too."""
     desc = SceneDesc.synth_config(3)
     w, h = 640, 361
-    monkeypatch.setenv("RT_SEAM_SPLIT", "1")
-    s = DeviceScene(desc, device=0)
+    s = DeviceScene(desc, device=0, tuning="seam_split=1")
     ref, rcnt, _, ref8 = s.render(w, h, 8, want_u8=True)
     s.close()
-    monkeypatch.setenv("RT_SEAM_SPLIT", "2")
-    monkeypatch.delenv("RT_SEAM_BAND_ROWS", raising=False)
-    monkeypatch.delenv("RT_SEAM_ADAPT", raising=False)
-    monkeypatch.setenv("RT_SEAM_GRID_PCT", "60")
-    s = DeviceScene(desc, device=0)
+    s = DeviceScene(desc, device=0, tuning="seam_split=2,seam_grid_pct=60")
     for _ in range(12):
         img, cnt, _, img8 = s.render(w, h, 8, want_u8=True)
         assert same_bits(img, ref) and np.array_equal(img8, ref8) and cnt == rcnt

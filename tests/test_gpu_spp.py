@@ -63,18 +63,36 @@ def test_config5_4k_sampled_rows():
     compare(img[r], ref[r])
 
 
-def test_config5_64spp_sampled_rows():
-    """Config 5 as benchmarked: 3840x2160, depth 8, 64 jittered samples per pixel, seed 3 --
-    two full rows (2 x 3840 pixels x 64 samples) against the oracle."""
+def test_config5_64spp_every_64th_row():
+    """Config 5 as benchmarked: 3840x2160, depth 8, 64 jittered samples per pixel, seed 3.
+    Every 64th row (34 rows x 3840 pixels x 64 samples) against the oracle, ray counters
+    included: rank 0 of a 64-rank band split with 1-row bands is exactly rows 0, 64, 128, ...,
+    so its band render gives those rows' own counters -- and equals the whole frame's rows
+    bit for bit.  Reference per sample: render.rs:178-185 (get_ray) and :40-103."""
+    import torch
+    from rust_tracer_amd import abi, band_rows_per_rank
+    from tests.test_gpu_fullframe import host_threads
     desc = SceneDesc.synth_config(5)
+    w, h, spp, seed, world = 3840, 2160, 64, 3, 64
     s = DeviceScene(desc)
-    img, cnt, _, _ = s.render(3840, 2160, 8, spp=64, seed=3)
+    img, cnt, _, _ = s.render(w, h, 8, spp=spp, seed=seed)
+    assert cnt["pixels"] == w * h * spp
+    rpr = band_rows_per_rank(h, 1, world)
+    dev = torch.device("cuda", 0)
+    band = torch.zeros((rpr, w, 3), dtype=torch.float32, device=dev)
+    bcnt = torch.zeros(3, dtype=torch.int64, device=dev)
+    s.render_bands_async(abi.camera(w, h), 8, 1, 0, world, band.data_ptr(), bcnt.data_ptr(),
+                         torch.cuda.current_stream(dev).cuda_stream, spp=spp, seed=seed)
+    torch.cuda.synchronize()
+    s.sync_status()
     s.close()
-    assert cnt["pixels"] == 3840 * 2160 * 64
-    rows = (1080, 2160, 1000)
-    ref, _ = OracleScene(desc).render(3840, 2160, 8, rows=rows, threads=16, spp=64, seed=3)
-    r = np.arange(*rows)
-    compare(img[r], ref[r])
+    rows = np.arange(0, h, world)
+    band = band.cpu().numpy()[:len(rows)]
+    assert np.array_equal(band.view(np.uint32), img[rows].view(np.uint32))
+    ref, rcnt = OracleScene(desc).render(w, h, 8, rows=(0, h, world), threads=host_threads(), spp=spp, seed=seed)
+    compare(band, ref[rows])
+    assert rcnt["pixels"] == len(rows) * w * spp
+    assert bcnt.cpu().tolist() == [rcnt["node_rays"], rcnt["shadow_rays"], rcnt["pixels"]]
 
 
 def test_spp_bands_reassemble():
@@ -102,16 +120,10 @@ def test_spp_bands_reassemble():
     s.close()
 
 
-def test_spp_zero_rejected_and_mega_unsupported():
+def test_spp_zero_rejected():
     s = DeviceScene(SceneDesc.my_scene())
     with pytest.raises(RtError):
         s.render(8, 8, 2, spp=0)
-    os.environ["RT_PIPELINE"] = "mega"
-    try:
-        with pytest.raises(RtError):
-            s.render(8, 8, 2, spp=2)
-    finally:
-        del os.environ["RT_PIPELINE"]
     s.close()
 
 
@@ -119,17 +131,14 @@ def test_spp_zero_rejected_and_mega_unsupported():
 def test_sample_batches_change_nothing(monkeypatch, keys):
     """Samples batched B per pipeline pass (each a frame of the pass with its own jitter,
     summed in sample order by spp_accumulate_kernel) equal one pass per sample
-    (RT_SPP_BATCH=1) bit for bit, RGB8 included -- 19 samples: batches of 8, 8 and 3, so the
+    (spp_batch=1) bit for bit, RGB8 included -- 19 samples: batches of 8, 8 and 3, so the
     running sum crosses batches and the last batch is partial; every queue-key variant."""
     desc = SceneDesc.synth_config(5)
     w, h, spp = 160, 90, 19
-    monkeypatch.setenv("RT_SPP_BATCH", "1")
-    s = DeviceScene(desc, device=0)
+    s = DeviceScene(desc, device=0, tuning="spp_batch=1")
     ref, rcnt, _, ref8 = s.render(w, h, 8, spp=spp, seed=3, want_u8=True)
     s.close()
-    monkeypatch.setenv("RT_SPP_BATCH", "8")
-    monkeypatch.setenv("RT_SPP_KEYS", keys)
-    s = DeviceScene(desc, device=0)
+    s = DeviceScene(desc, device=0, tuning=f"spp_batch=8,spp_keys={keys}")
     img, cnt, _, img8 = s.render(w, h, 8, spp=spp, seed=3, want_u8=True)
     s.close()
     assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
@@ -147,8 +156,7 @@ def test_sample_batches_in_bands(monkeypatch):
     rpr = band_rows_per_rank(h, 8, world)
     outs = []
     for b in ("1", "4"):
-        monkeypatch.setenv("RT_SPP_BATCH", b)
-        s = DeviceScene(desc, device=0)
+        s = DeviceScene(desc, device=0, tuning=f"spp_batch={b}")
         out = torch.full((rpr, w, 3), -1.0, device=dev)
         cnt = torch.zeros(3, dtype=torch.int64, device=dev)
         s.render_bands_async(abi.camera(w, h), 8, 8, 1, world, out.data_ptr(), cnt.data_ptr(),

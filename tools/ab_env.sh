@@ -1,5 +1,6 @@
 #!/bin/bash
-# A/B of RT_* switches on the benchmark (GPU side): tools/ab_env.sh "ENV1=a ENV2=b" "ENV1=c" ...
+# A/B of tuning keys (rt_tune.hpp) on the benchmark (GPU side):
+#   tools/ab_env.sh "RT_TUNE=lb_res=0,task_w=32" "RT_TUNE=lb_res=64" "RT_LIB=rust_tracer_amd/librt_hip_X.so" ...
 # Each setting runs REPS times (default 2), alternating, at the bench defaults (frames in flight;
 # K timed frames, default 64 as bench.py -- round-3 logs before r3ab17 used K = 20).
 set -o pipefail

@@ -2,6 +2,8 @@
 # Builds an A/B variant of the product library with extra compile flags:
 #   tools/build_variant.sh NAME "-DRT_SWITCH=0 ..."  -> rust_tracer_amd/librt_hip_NAME.so
 # (load it with RT_LIB=rust_tracer_amd/librt_hip_NAME.so; tools/ab_env.sh takes RT_LIB=...)
+# "-DRT_DIAG=1" builds the diagnostic knobs (result-changing measurement switches, debug
+# prints, RT_TASK_CLOCK records) that the product library does not contain.
 set -e
 NAME=$1; FLAGS=$2
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -10,9 +12,10 @@ B=/tmp/rt_variant_$NAME
 mkdir -p $B
 HF="-O3 -std=c++17 -fPIC -ffp-contract=off -Wall --offload-arch=gfx950 -munsafe-fp-atomics $FLAGS"
 CF="-O3 -std=c++17 -fPIC -ffp-contract=off -Wall $FLAGS"
-for f in rt_kernels rt_wavefront rt_order; do /opt/rocm/bin/hipcc $HF -c -o $B/$f.o $C/$f.hip & done
+for f in rt_frame rt_wavefront rt_order; do /opt/rocm/bin/hipcc $HF -c -o $B/$f.o $C/$f.hip & done
 for f in rt_api rt_multi; do /opt/rocm/bin/hipcc $HF -c -o $B/$f.o $C/$f.cpp & done
 /opt/rocm/bin/hipcc $CF -x c++ -c -o $B/rt_bvh.o $C/rt_bvh.cpp &
+/opt/rocm/bin/hipcc $CF -x c++ -c -o $B/rt_tune.o $C/rt_tune.cpp &
 /opt/rocm/bin/hipcc $CF -x c++ -c -o $B/image_io.o $C/host/image_io.cpp &
 /opt/rocm/bin/hipcc $CF -x c++ -c -o $B/scene.o $C/host/scene.cpp &
 wait

@@ -1,4 +1,4 @@
-"""Per-kernel test counts: RT_COUNT=trace / shadow instrument one kernel family at a time.
+"""Per-kernel test counts: tuning count=trace / shadow instruments one kernel family at a time.
 
 usage: python tools/kernel_ops.py [config=3]
 Prints, per kernel family, the lane-weighted test counts per ray of that family and the
@@ -14,8 +14,7 @@ def main():
     config = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     depth = 4 if config == 2 else 8
     for which in ("trace", "shadow"):
-        os.environ["RT_COUNT"] = which
-        s = DeviceScene(SceneDesc.synth_config(config))
+        s = DeviceScene(SceneDesc.synth_config(config), tuning=f"count={which}")
         _, cnt, ms0, _ = s.render(1920, 1080, depth)
         s.set_scan_counting(True)
         s.scan_ops(reset=True)
@@ -29,7 +28,6 @@ def main():
                 print(f"  {k:16s} {v:.4g}  per ray {v / rays:.1f}  share {v / max(1, ops['cycles_scans']):.3f}")
             else:
                 print(f"  {k:16s} {v:.4g}  per ray {v / rays:.2f}")
-    os.environ.pop("RT_COUNT", None)
 
 
 if __name__ == "__main__":

@@ -1,14 +1,13 @@
 """Per-level cost of the trace kernel (config 3, 1080p): rays per level and the counted
 kernels' test / cycle counters, as differences between renders of depth d and d - 1
-(RT_COUNT=trace: only the trace kernels count).  python tools/level_ops.py"""
+(tuning count=trace: only the trace kernels count).  python tools/level_ops.py"""
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["RT_COUNT"] = "trace"
 from rust_tracer_amd import DeviceScene, SceneDesc  # noqa: E402
 
-s = DeviceScene(SceneDesc.synth_config(3))
+s = DeviceScene(SceneDesc.synth_config(3), tuning="count=trace")
 s.set_scan_counting(True)
 prev_ops, prev_nodes = None, 0
 keys = DeviceScene.SCAN_OPS

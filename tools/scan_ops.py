@@ -12,12 +12,7 @@ from rust_tracer_amd import DeviceScene, SceneDesc
 
 
 def run(config, w, h, depth, bvh):
-    if not bvh:
-        os.environ["RT_BVH"] = "0"
-    try:
-        s = DeviceScene(SceneDesc.synth_config(config))
-    finally:
-        os.environ.pop("RT_BVH", None)
+    s = DeviceScene(SceneDesc.synth_config(config), tuning=None if bvh else "bvh=0")
     s.render(w, h, depth)
     s.set_scan_counting(True)
     s.scan_ops(reset=True)
