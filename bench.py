@@ -38,14 +38,18 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "Mpixels/sec (primary+8 bounces) at 1920×1080; fraction of HBM roofline"
 PEAK_F32_TFLOPS = 157.3      # MI355X FP32 vector peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBPS = 8000.0       # MI355X HBM3E peak
-# Algorithmic f32 flops of each test the scans count (rt_scene_scan_ops; DESIGN.md
-# "Roofline"): reference arithmetic of the ray-primitive tests (sphere
-# 57, triangle 52, cube 12 x 52 + 33 for the ray transform, plane 49), 12 FMAs = 24 flops
-# per 2-wide child-box test, 45 flops for a cube's object-space box (its transform shared
-# with the triangles), 6 per grazing cone test and 48 per 8-normal grazing test.
-OP_FLOPS = {"node_pairs": 24, "dsph_pairs": 2 * 57, "gsph": 57, "tri_pairs": 2 * 52,
-            "cube_boxes": 33 + 12, "cubes": 12 * 52, "graze_cones": 6, "planes": 49,
-            "graze_normals": 48}
+# f32 flops of each test the scans count (rt_scene_scan_ops; DESIGN.md "Roofline").
+# Reference tests -- the ray-primitive tests Scene::intersect performs (SURVEY.md §8(d):
+# sphere 57, triangle 52, cube 33 for the ray transform + 12 x 52, plane 49):
+REF_TEST_FLOPS = {"dsph_pairs": 2 * 57, "gsph": 57, "tri_pairs": 2 * 52, "cube_boxes": 33, "cubes": 12 * 52,
+                  "planes": 49}
+# ... as the device executes them: a translate-scale sphere's pt_mul / vec3_mul drop their
+# 24 x*0 terms (57 -> 33 flops, rt_scan.hpp sph_pair); the others as the reference's
+EXEC_TEST_FLOPS = dict(REF_TEST_FLOPS, dsph_pairs=2 * 33)
+# Hierarchy work the reference never performs: 12 FMAs = 24 flops per 2-wide child-box test,
+# 12 per cube's object-space box test, 6 per grazing cone test, 48 per 8-normal grazing test
+OVERHEAD_FLOPS = {"node_pairs": 24, "cube_box_slab": 12, "graze_cones": 6, "graze_normals": 48}
+OVERHEAD_COUNTER = {"cube_box_slab": "cube_boxes"}
 
 
 def parse():
@@ -327,15 +331,26 @@ def seam_stats(args, scene, pipe, tiler, dev):
     return out
 
 
-def load_traffic(path, workload):
+def load_traffic(path, workload, frames_per_pass):
+    """The profile (tools/profile.sh -> profiles/pmc_traffic.json) of THESE sources and this
+    pass size, or (None, why not): counters measured on other code are not replayed."""
+    from rust_tracer_amd.provenance import sources_sha
     try:
         with open(path) as f:
             t = json.load(f)
-        if t.get("workload") == workload:
-            return t
-    except Exception:
-        pass
-    return None
+    except Exception as e:  # noqa: BLE001
+        return None, f"no profile ({e!r:.80})"
+    if t.get("workload") != workload:
+        return None, "the profile is of another workload"
+    sha = sources_sha()
+    if t.get("sources_sha") != sha:
+        return None, f"profile of sources {t.get('sources_sha')}, these are {sha}: stale, not replayed"
+    entry = (t.get("per_pass_size") or {}).get(str(frames_per_pass))
+    if entry is None:
+        return None, f"the profile has no {frames_per_pass}-frame pass entry"
+    return dict(entry, profile=t.get("profile"), sources_sha=sha, commit=t.get("commit"),
+                exclusive_kernel_ms_per_frame=t.get("exclusive_kernel_ms_per_frame"),
+                exclusive_source=t.get("exclusive_source")), None
 
 
 def main():
@@ -512,14 +527,23 @@ def main():
     if rank == 0:
         steps = args.steps
         mpix = args.width * args.height * steps / elapsed / 1e6
-        # rank 0's launch: the tests its scans ran (culled), at their algorithmic flops
-        per_launch_flops = sum(ops[k] * OP_FLOPS[k] for k in OP_FLOPS) if ops else None
+        # rank 0's launch: the tests its scans ran (culled) -- the reference's tests as the device
+        # executes them plus the hierarchy's own tests; beside it the reference tests at the
+        # reference's flop counts
+        flops = None
+        if ops:
+            ref_f = sum(ops[k] * REF_TEST_FLOPS[k] for k in REF_TEST_FLOPS)
+            exec_f = sum(ops[k] * EXEC_TEST_FLOPS[k] for k in EXEC_TEST_FLOPS)
+            over_f = sum(ops[OVERHEAD_COUNTER.get(k, k)] * OVERHEAD_FLOPS[k] for k in OVERHEAD_FLOPS)
+            flops = {"reference_tests_at_reference_flops": ref_f, "reference_tests_executed": exec_f,
+                     "hierarchy_tests": over_f}
+        per_launch_flops = flops["reference_tests_executed"] + flops["hierarchy_tests"] if flops else None
         achieved = per_launch_flops / (kernel_ms / 1e3) / 1e12 if ops else None
         # what the reference's linear scan would need for the same rays (F_alg per scan)
         brute_flops = local_scans * scene.flops_per_scan
         workload = (f"config{args.config}: {scene_label(args.config)}, {args.width}x{args.height}, "
                     f"depth {args.depth}" + (f", {args.spp} spp (jitter seed {args.seed})" if args.spp > 1 else ""))
-        traffic = load_traffic(args.traffic_json, workload)
+        traffic, traffic_note = load_traffic(args.traffic_json, workload, batch)
         roofline = {
             "bound": "valu",
             "achieved": round(achieved, 3) if ops else None,
@@ -533,6 +557,11 @@ def main():
             "kernel_ms_is": (f"timed-region HIP events / steps ({inflight} passes of {batch} frames in flight)"
                              if inflight * batch > 1 else "timed-region HIP events / steps"),
             "flops_per_launch": per_launch_flops,
+            "flops_is": ("the counted tests as executed: reference tests (translate-scale spheres at 33 flops, "
+                         "their x*0 terms dropped; SURVEY.md §8(d) counts otherwise) + hierarchy tests"),
+            "flops_breakdown": flops,
+            "frac_reference_tests_only": (round(flops["reference_tests_executed"] / (kernel_ms / 1e3) / 1e12 /
+                                                PEAK_F32_TFLOPS, 4) if flops else None),
             "tests_per_launch": {k: round(v) for k, v in ops.items() if not k.startswith("cycles")} if ops else None,
             "cycles_per_launch": {k: round(v) for k, v in ops.items() if k.startswith("cycles")} if ops else None,
             "culling": {"hierarchy": scene.uses_bvh,
@@ -552,7 +581,11 @@ def main():
                 "wave_cycle_shares": traffic.get("wave_cycle_shares"),
                 "source": traffic.get("sq_source"),
             } if traffic and traffic.get("sq_insts_valu_per_frame") else None),
-            "profile_commit": traffic.get("commit") if traffic else None,
+            "profile": ({"path": traffic["profile"], "sources_sha": traffic["sources_sha"],
+                         "commit": traffic["commit"], "frames_per_pass": batch} if traffic else None),
+            "traffic_note": traffic_note,
+            # exclusive per-kernel times (one frame at a time, nothing overlapping) of the profile
+            "exclusive_kernel_ms_per_frame": traffic.get("exclusive_kernel_ms_per_frame") if traffic else None,
             "hbm": {
                 "algorithmic_bytes_per_launch": args.spp * (scene.device_bytes + args.width * args.height * 12 / world),
                 "achieved_GBps": round((traffic["bytes_per_launch"] / (kernel_ms / 1e3) / 1e9), 3)

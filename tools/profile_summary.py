@@ -1,8 +1,11 @@
-"""Summarise a tools/prof2.sh / tools/prof3.sh run: per-kernel ms per frame (frames in flight and one at a
-time), per-kernel HBM bytes per frame (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md's
-gfx950 correction) and SQ wave-cycle shares.  Copies the evidence to profiles/TAG/.
+"""Summarise a tools/profile.sh run: per-kernel ms per frame (the driver's frames in flight, and
+one frame at a time -- exclusive times), per-kernel HBM bytes per frame (FETCH_SIZE x 2 +
+WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction) and SQ wave-cycle shares for passes of
+1, 5 and 16 frames.  Copies the evidence to profiles/TAG/ and writes profiles/pmc_traffic.json
+(what bench.py replays for roofline.traffic / executed_valu, keyed by the sources' hash and
+the pass size).
 
-usage: python tools/prof2_summary.py TAG [frames_in_pmc_runs]
+usage: python tools/profile_summary.py TAG
 """
 import csv
 import glob
@@ -58,24 +61,26 @@ def main():
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     bench = json.load(open(os.path.join(src, "bench.json")))
-    bench1 = json.load(open(os.path.join(src, "bench1.json")))
-    for fn in ("bench.json", "bench1.json", "cpu_max.txt"):
+    sha = open(os.path.join(src, "sources_sha.txt")).read().strip()
+    for fn in ("bench.json", "cpu_max.txt", "sources_sha.txt"):
         if os.path.exists(os.path.join(src, fn)):
             shutil.copy(os.path.join(src, fn), os.path.join(dst, fn))
-    out = [f"# Profile {tag}: {bench['config']['workload']}", ""]
-    out.append(f"bench.py: **{bench['value']} Mpixels/s** ({bench['ms_per_step']} ms/frame, "
-               f"{bench['config']['frames_in_flight']} frames in flight); one frame at a time (--inflight 1): "
-               f"{bench1['value']} Mpixels/s ({bench1['ms_per_step']} ms/frame).")
+    out = [f"# Profile {tag}: {bench['config']['workload']}", "",
+           f"Sources: `{sha}` (rust_tracer_amd/provenance.py).", ""]
+    out.append(f"bench.py --steps 20 --warmup 5 (the driver's line): **{bench['value']} Mpixels/s** "
+               f"({bench['ms_per_step']} ms/frame, {bench['config']['passes_in_flight']} passes x "
+               f"{bench['config']['frames_per_pass']} frames in flight).")
     out.append("")
-    # trace runs: warmup + slot set-up + steps frames; divide by all frames rendered
+    # trace runs: slot set-up (inflight x batch frames) + warm-up + timed frames; the trace run
+    # repeats bench.json's own arguments (tools/profile.sh)
     f4 = bench["config"]["frames_in_flight"]
-    # slot set-up (inflight x batch frames) + warm-up + timed frames
-    # the trace run repeats bench.json's own arguments (tools/prof3.sh)
     t4, f_t4, _ = trace_table(os.path.join(src, "trace"), bench["steps"] + bench["warmup"] + f4)
     t1, f_t1, _ = trace_table(os.path.join(src, "trace1"), 6 + 1 + 1)
     out += ["## rocprofv3 --kernel-trace (ms of kernel time per frame)", "",
+            "In flight the passes overlap, so those times are not exclusive (they sum to more than a "
+            "frame); one frame at a time they are.", "",
             f"| kernel | {f4} frames in flight ({bench['config']['passes_in_flight']} passes x "
-            f"{bench['config']['frames_per_pass']}) | one frame at a time |", "|---|---|---|"]
+            f"{bench['config']['frames_per_pass']}) | one frame at a time (exclusive) |", "|---|---|---|"]
     for k in sorted(set(t4) | set(t1), key=lambda k: -t1.get(k, 0)):
         out.append(f"| {k} | {t4.get(k, 0):.3f} | {t1.get(k, 0):.3f} |")
     out.append(f"| **sum** | {sum(t4.values()):.3f} | {sum(t1.values()):.3f} |")
@@ -88,11 +93,14 @@ def main():
     import subprocess
     commit = os.environ.get("PROFILE_COMMIT") or subprocess.run(
         ["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True).stdout.strip()
+    from rust_tracer_amd.provenance import sources_sha
+    if sources_sha() != sha:
+        print(f"warning: the tree's sources ({sources_sha()}) are not the profiled ones ({sha})")
     # PMC passes: (suffix, frames per pass, frames rendered in the run: the slot's set-up pass + steps)
     # (b1: --steps 4 after a 1-frame set-up pass; bN: --steps N after an N-frame set-up pass)
     sizes = sorted(int(d[len("pmc_fetch_b"):]) for d in os.listdir(src)
                    if d.startswith("pmc_fetch_b") and d[len("pmc_fetch_b"):].isdigit())
-    runs = [(f"_b{n}", n, 5 if n == 1 else 2 * n) for n in sizes] if sizes else [("", 1, 5)]
+    runs = [(f"_b{n}", n, 2 * n) for n in sizes]  # the slot's set-up pass + one timed pass
     result = {}
     for suf, per_pass, pmc_frames in runs:
         fe, f_fe = pmc_table(os.path.join(src, "pmc_fetch" + suf), "FETCH_SIZE")
@@ -146,17 +154,17 @@ def main():
                                                   "issue_stalled": round(sq.get("SQ_WAIT_INST_ANY", 0) / wc, 4)}
                             if sq else None,
                             "source": f"profiles/{tag}/pmc_fetch{suf}.csv, pmc_write{suf}.csv, pmc_sq{suf}.csv"}
-    # the headline's pass size when measured, else one frame per pass
-    big = max(result)
-    head = result[big]
-    doc = {"workload": bench["config"]["workload"], "commit": commit, "profile": f"profiles/{tag}",
-           "launch": "one frame of the render pipeline (every kernel of the frame), per frame of a "
-                     f"{big}-frame pass",
+    # bench.py picks the entry of its own pass size (the driver's K = 20: 5 frames per pass)
+    doc = {"workload": bench["config"]["workload"], "sources_sha": sha, "commit": commit,
+           "profile": f"profiles/{tag}",
+           "launch": "one frame of the render pipeline (every kernel of the frame), per frame of an "
+                     "N-frame pass (per_pass_size[N])",
            "correction": "FETCH_SIZE x 2 per MI355X_MICROARCH.md (gfx950 tallies 128-B requests at 64 B); "
                          "WRITE_SIZE as reported",
-           "sq_source": head["source"]}
-    doc.update(head)
-    doc["per_pass_size"] = {str(k): v for k, v in result.items()}
+           "exclusive_kernel_ms_per_frame": {k: round(v, 4) for k, v in sorted(t1.items(), key=lambda kv: -kv[1])},
+           "exclusive_source": f"profiles/{tag}/kernel_trace_trace1.csv (one frame at a time)",
+           "in_flight_kernel_ms_per_frame": {k: round(v, 4) for k, v in sorted(t4.items(), key=lambda kv: -kv[1])},
+           "per_pass_size": {str(k): v for k, v in result.items()}}
     json.dump(doc, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
     open(os.path.join(dst, "summary.md"), "w").write("\n".join(out) + "\n")
     print("\n".join(out))
