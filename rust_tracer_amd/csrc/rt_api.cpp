@@ -1045,6 +1045,7 @@ struct Workspace {
     uint32_t shadow_capacity = 0;
     uint32_t* levels = nullptr;      // RT_LEVEL_TABLE_WORDS words
     uint32_t* overflow = nullptr;    // [0] this pass's queue overflows, [1] sticky (rt_scene_sync_status)
+    uint64_t* ctr_save = nullptr;    // a checked pass's caller counters before it (rt_render_bands_ex_async)
     // queue ordering (rt_order.hip)
     uint32_t* task_keys = nullptr;   // [capacity] x2 buffers
     uint32_t* perm = nullptr;
@@ -1112,6 +1113,10 @@ struct rt_scene {
     // rt_scene_sync_status)
     uint32_t split_dev_rows = 0, split_dev_y = 0;
     bool split_dev_pending = false, split_dev_overflow = false;
+    // rt_render_bands_ex_async: the last pass shape checked for overflow on this handle, and an
+    // overflow of an earlier pass that such a check found latched (reported by sync_status)
+    uint64_t checked_sig = 0;
+    bool ovf_pending = false;
 };
 
 rt_multi_state*& rt_scene_multi(rt_scene* s) { return s->multi; }
@@ -1163,6 +1168,7 @@ rt_status ensure_ws(rt_scene* s, size_t out_floats, size_t out8_bytes) {
     if (!w.counters) {
         HIP_TRY(hipMalloc(&w.counters, 4 * sizeof(unsigned long long)));
         HIP_TRY(hipMalloc(&w.work, 64));
+        HIP_TRY(hipMalloc(&w.ctr_save, 64));
     }
     if (out_floats > w.out_floats) {
         if (w.out) (void)hipFree(w.out);
@@ -1214,7 +1220,7 @@ void free_workspace(Workspace& w) {
                     (void*)w.node_flags, (void*)w.levels, (void*)w.overflow, (void*)w.node_ps, (void*)w.node_n,
                     (void*)w.node_d, (void*)w.node_lit, (void*)w.node_ec, (void*)w.task_keys, (void*)w.perm,
                     (void*)w.shadow_keys, (void*)w.shadow_sorted, (void*)w.sort_tmp, (void*)w.node_dc,
-                    (void*)w.node_key, (void*)w.node_pixel, (void*)w.spp_buf})
+                    (void*)w.node_key, (void*)w.node_pixel, (void*)w.spp_buf, (void*)w.ctr_save})
         if (b) (void)hipFree(b);
     w = Workspace();
 }
@@ -2070,11 +2076,53 @@ rt_status rt_render_bands_ex_async(const rt_scene* scene, const rt_camera* cams,
     if (st != RT_OK) return st;
     hipStream_t hs = (hipStream_t)stream;
     const PassOut o{d_rgb, d_rgb8, reinterpret_cast<unsigned long long*>(d_counters), true, false};
-    if (n_frames == 1) {
-        st = launch_bands(s, cam, depth, spp, seed, band_rows, rank, world, o, hs);
-    } else {
-        st = wave_pipeline(s, s->ws, cam, depth, band_rows, rank, world, o, hs, nullptr, nullptr, 1, 0, 0, n_frames,
-                           cams);
+    // The first pass of a new shape on this handle (frame size, bands, frames, samples, depth)
+    // is checked before the call returns: the pool is sized from node_factor, which suits
+    // config-3-like trees, and a mirror- or glass-heavy scene needs more.  The call waits for
+    // that pass, and if a queue overflowed it grows the pool and renders it again (the
+    // caller's counters restored first), as rt_render does -- so a new scene or frame shape
+    // costs one synchronisation, not an incomplete frame.  Later passes of the same shape stay
+    // asynchronous: an overflow there (trees that grew with the camera) is latched and
+    // reported by rt_scene_sync_status, and the next pass gets twice the pool.  The node_cap
+    // test knob pins the pools and skips the check.
+    const uint64_t sig = (((((uint64_t)cam->x_res * 65537u + cam->y_res) * 257u + band_rows) * 65537u + rank) * 65537u +
+                          world) * 4099u + (uint64_t)n_frames * 131u + spp * 7u + depth;
+    const bool checked = !s->tune.node_cap && sig != s->checked_sig;
+    if (checked) {
+        HIP_TRY(hipStreamSynchronize(hs));
+        for (auto& se : s->ev_streams) HIP_TRY(hipEventSynchronize(se.second));
+        if (s->ws.overflow) {  // an earlier pass's unreported overflow stays reported
+            uint32_t v = 0;
+            HIP_TRY(hipMemcpyAsync(&v, s->ws.overflow + 1, sizeof(v), hipMemcpyDeviceToHost, hs));
+            HIP_TRY(hipStreamSynchronize(hs));
+            if (v) {
+                s->ovf_pending = true;
+                HIP_TRY(hipMemsetAsync(s->ws.overflow + 1, 0, sizeof(v), hs));
+            }
+        }
+        if (d_counters) HIP_TRY(hipMemcpyAsync(s->ws.ctr_save, d_counters, 3 * sizeof(uint64_t), hipMemcpyDeviceToDevice, hs));
+    }
+    for (int attempt = 0;; attempt++) {
+        if (n_frames == 1) {
+            st = launch_bands(s, cam, depth, spp, seed, band_rows, rank, world, o, hs);
+        } else {
+            st = wave_pipeline(s, s->ws, cam, depth, band_rows, rank, world, o, hs, nullptr, nullptr, 1, 0, 0,
+                               n_frames, cams);
+        }
+        if (st != RT_OK || !checked) break;
+        uint32_t ovf = 0;
+        HIP_TRY(hipMemcpyAsync(&ovf, s->ws.overflow, sizeof(ovf), hipMemcpyDeviceToHost, hs));
+        HIP_TRY(hipStreamSynchronize(hs));
+        if (!ovf) {
+            s->checked_sig = sig;
+            break;
+        }
+        const uint64_t lim = pool_cap_limit(s);
+        if (attempt >= 8 || s->ws.capacity >= lim) break;  // latched: rt_scene_sync_status reports it
+        HIP_TRY(hipMemsetAsync(s->ws.overflow + 1, 0, sizeof(uint32_t), hs));  // rendered again
+        s->pool_floor = (uint32_t)std::min<uint64_t>(2ull * s->ws.capacity, lim);
+        if (d_counters)
+            HIP_TRY(hipMemcpyAsync(d_counters, s->ws.ctr_save, 3 * sizeof(uint64_t), hipMemcpyDeviceToDevice, hs));
     }
     if (st != RT_OK) return st;
     hipEvent_t ev = nullptr;
@@ -2245,15 +2293,22 @@ rt_status rt_scene_sync_own(rt_scene* s) {
     for (auto& se : s->ev_streams) HIP_TRY(hipEventSynchronize(se.second));
     for (auto& se : s->ev_streams) (void)hipEventDestroy(se.second);
     s->ev_streams.clear();
-    if (!s->ws.overflow) return RT_OK;
-    // read and clear the sticky word on the handle's own stream, waited for here: no null-stream
-    // operation (unordered with the callers' non-blocking streams) touches it
-    uint32_t v = 0;
-    HIP_TRY(hipMemcpyAsync(&v, s->ws.overflow + 1, sizeof(v), hipMemcpyDeviceToHost, s->stream));
-    HIP_TRY(hipStreamSynchronize(s->stream));
-    if (!v) return RT_OK;
-    HIP_TRY(hipMemsetAsync(s->ws.overflow + 1, 0, sizeof(v), s->stream));
-    HIP_TRY(hipStreamSynchronize(s->stream));
+    // an overflow a checked pass found latched before it rendered (rt_render_bands_ex_async)
+    bool ovf = s->ovf_pending;
+    s->ovf_pending = false;
+    if (s->ws.overflow) {
+        // read and clear the sticky word on the handle's own stream, waited for here: no
+        // null-stream operation (unordered with the callers' non-blocking streams) touches it
+        uint32_t v = 0;
+        HIP_TRY(hipMemcpyAsync(&v, s->ws.overflow + 1, sizeof(v), hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        if (v) {
+            HIP_TRY(hipMemsetAsync(s->ws.overflow + 1, 0, sizeof(v), s->stream));
+            HIP_TRY(hipStreamSynchronize(s->stream));
+            ovf = true;
+        }
+    }
+    if (!ovf) return RT_OK;
     // the next pass on this scene gets a pool twice as large (up to the index limit)
     s->pool_floor = (uint32_t)std::min<uint64_t>(2ull * s->ws.capacity, pool_cap_limit(s));
     return RT_ERR_CAPACITY;

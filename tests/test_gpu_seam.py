@@ -496,3 +496,31 @@ def test_adaptive_seam_split_changes_nothing(monkeypatch):
         img, cnt, _, img8 = s.render(w, h, 8, want_u8=True)
         assert same_bits(img, ref) and np.array_equal(img8, ref8) and cnt == rcnt
     s.close()
+
+
+def test_pipeline_glass_heavy_scene_completes():
+    """A scene whose ray trees far outgrow the default pool (every sphere a reflective glass
+    ball: two children per hit, ~20+ nodes per pixel at depth 8 where node_factor sizes 6):
+    the first pass of each frame-in-flight slot is checked (rt_render_bands_ex_async grows the
+    pool and renders it again), so FramePipeline returns complete frames, equal to rt_render
+    bit for bit, with no overflow reported."""
+    from rust_tracer_amd.abi import RT_SHAPE_SPHERE
+    from rust_tracer_amd.dist import FramePipeline
+    desc = SceneDesc.synth_config(3).editable()
+    glass = desc.phong((0.05, 0.05, 0.05), (0.2, 0.3, 0.4), (1.0, 1.0, 1.0), 120.0, 0.8, 1.5)
+    for sh in desc.shapes:
+        if sh.kind == RT_SHAPE_SPHERE:
+            sh.material = glass
+    w, h, depth = 240, 136, 8
+    ref_scene = DeviceScene(desc, device=0)
+    ref, rcnt, _, _ = ref_scene.render(w, h, depth)
+    ref_scene.close()
+    assert rcnt["node_rays"] > 8 * w * h  # the trees really outgrow the default 6 slots per pixel
+    s = DeviceScene(desc, device=0)
+    pipe = FramePipeline(s, desc, w, h, depth, inflight=2, batch=2)
+    for _ in range(2):
+        pipe.run(4)
+        frames = pipe.frames()  # raises RtError(RT_ERR_CAPACITY) on an incomplete frame
+        assert len(frames) == 4 and all(same_bits(f.cpu().numpy(), ref) for f in frames)
+    pipe.close()
+    s.close()
