@@ -1113,9 +1113,11 @@ struct rt_scene {
     // rt_scene_sync_status)
     uint32_t split_dev_rows = 0, split_dev_y = 0;
     bool split_dev_pending = false, split_dev_overflow = false;
-    // rt_render_bands_ex_async: the last pass shape checked for overflow on this handle, and an
-    // overflow of an earlier pass that such a check found latched (reported by sync_status)
-    uint64_t checked_sig = 0;
+    // rt_render_bands_ex_async: the largest pass (level-0 items, depth) checked for overflow on
+    // this handle, and an overflow of an earlier pass that such a check found latched
+    // (reported by sync_status)
+    uint64_t checked_items = 0;
+    uint32_t checked_depth = 0;
     bool ovf_pending = false;
 };
 
@@ -2076,18 +2078,19 @@ rt_status rt_render_bands_ex_async(const rt_scene* scene, const rt_camera* cams,
     if (st != RT_OK) return st;
     hipStream_t hs = (hipStream_t)stream;
     const PassOut o{d_rgb, d_rgb8, reinterpret_cast<unsigned long long*>(d_counters), true, false};
-    // The first pass of a new shape on this handle (frame size, bands, frames, samples, depth)
-    // is checked before the call returns: the pool is sized from node_factor, which suits
-    // config-3-like trees, and a mirror- or glass-heavy scene needs more.  The call waits for
-    // that pass, and if a queue overflowed it grows the pool and renders it again (the
-    // caller's counters restored first), as rt_render does -- so a new scene or frame shape
-    // costs one synchronisation, not an incomplete frame.  Later passes of the same shape stay
+    // A pass larger (level-0 items) or deeper than any this handle has completed is checked
+    // before the call returns: the pool is sized from node_factor, which suits config-3-like
+    // trees, and a mirror- or glass-heavy scene needs more.  The call waits for that pass, and
+    // if a queue overflowed it grows the pool and renders it again (the caller's counters
+    // restored first), as rt_render does -- so a new scene or frame size costs one
+    // synchronisation, not an incomplete frame.  Passes no larger than a checked one stay
     // asynchronous: an overflow there (trees that grew with the camera) is latched and
     // reported by rt_scene_sync_status, and the next pass gets twice the pool.  The node_cap
     // test knob pins the pools and skips the check.
-    const uint64_t sig = (((((uint64_t)cam->x_res * 65537u + cam->y_res) * 257u + band_rows) * 65537u + rank) * 65537u +
-                          world) * 4099u + (uint64_t)n_frames * 131u + spp * 7u + depth;
-    const bool checked = !s->tune.node_cap && sig != s->checked_sig;
+    const uint64_t rows_local = rt_band_rows_per_rank(cam->y_res, band_rows, world);
+    const uint64_t items = (uint64_t)((cam->x_res + 7u) / 8u) * ((rows_local + 7u) / 8u) * 64u * n_frames *
+                           std::min<uint32_t>(spp, RT_MAX_FRAMES);
+    const bool checked = !s->tune.node_cap && (items > s->checked_items || depth > s->checked_depth);
     if (checked) {
         HIP_TRY(hipStreamSynchronize(hs));
         for (auto& se : s->ev_streams) HIP_TRY(hipEventSynchronize(se.second));
@@ -2114,7 +2117,8 @@ rt_status rt_render_bands_ex_async(const rt_scene* scene, const rt_camera* cams,
         HIP_TRY(hipMemcpyAsync(&ovf, s->ws.overflow, sizeof(ovf), hipMemcpyDeviceToHost, hs));
         HIP_TRY(hipStreamSynchronize(hs));
         if (!ovf) {
-            s->checked_sig = sig;
+            s->checked_items = std::max(s->checked_items, items);
+            s->checked_depth = std::max(s->checked_depth, depth);
             break;
         }
         const uint64_t lim = pool_cap_limit(s);
