@@ -454,26 +454,10 @@ rt_status rt_multi_build(rt_scene* s0, const int32_t* devices, uint32_t n_device
         rt_multi_free(m);
         return e;
     };
-    // the ranks' streams: shares of ONE device must not share a hardware queue (the process
-    // gets 4, shared round-robin by every stream it creates), or they serialise
-    const int sq = rt_scene_tune(s0).share_queues;
-    int prio_lo = 0, prio_hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    auto make_stream = [&](hipStream_t* st_out) -> hipError_t {
-        if (sq == 1) return hipStreamCreateWithPriority(st_out, hipStreamNonBlocking, prio_hi);
-        if (sq == 2) {
-            int cus = 0, dev = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-                return hipErrorInvalidValue;
-            std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xFFFFFFFFu);
-            return hipExtStreamCreateWithCUMask(st_out, (uint32_t)mask.size(), mask.data());
-        }
-        return hipStreamCreateWithFlags(st_out, hipStreamNonBlocking);
-    };
     for (uint32_t r = 0; r < n_devices; r++) {
         if (r > 0 && (st = rt_scene_clone(s0, devices[r], &m->ranks[r])) != RT_OK) return fail(st);
-        if (hipSetDevice(devices[r]) != hipSuccess || make_stream(&m->streams[r]) != hipSuccess ||
+        if (hipSetDevice(devices[r]) != hipSuccess ||
+            hipStreamCreateWithFlags(&m->streams[r], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreate(&m->done[r]) != hipSuccess || hipEventCreate(&m->copied[r]) != hipSuccess ||
             hipMalloc(&m->counters[r], 3 * sizeof(unsigned long long)) != hipSuccess)
             return fail(RT_ERR_HIP);

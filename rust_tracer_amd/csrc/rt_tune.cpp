@@ -134,7 +134,6 @@ bool apply_one(Tune& t, const std::string& k, const std::string& v, bool build) 
         return set_named(v, n, x, 1, 0, 2, t.seam_adapt);
     }
     if (k == "seam_grid_pct") return set_int(v, 1, 100, t.seam_grid_pct);
-    if (k == "share_queues") return set_int(v, 0, 2, t.share_queues);
     if (k == "frame_fork") {
         static const char* const n[] = {"fork", "caller"};
         static const int x[] = {0, 1};

@@ -61,8 +61,6 @@ struct Tune {
     int seam_adapt = 1;       // meeting row: 1 copy-aware, 2 device finish times, 0 even split
     int seam_grid_pct = 80;   // the shares' grids' share of the chip
     int frame_fork = 0;       // rt_render_frame_async: 1 = share 0 on the caller's stream
-    int share_queues = 0;     // band shares' streams: 0 plain, 1 high priority, 2 full CU mask
-                              // (the last two get a hardware queue of their own)
 };
 
 // Applies "key=value" pairs (separated by ',' or whitespace) to t.  build_keys: whether
