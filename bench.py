@@ -68,10 +68,15 @@ def parse():
     p.add_argument("--seed", type=int, default=None, help="jitter seed (default: 3 for config 5)")
     p.add_argument("--band-rows", type=int, default=8)
     p.add_argument("--batch", type=int, default=None,
-                   help="frames per pipeline pass (rt_render_bands_batch_async, <= 16; default: the timed "
+                   help="frames per pipeline pass (rt_render_bands_batch_async, <= 32; default: the timed "
                         "frames spread evenly over the slots, q = ceil(steps / inflight) per slot in equal "
-                        "passes of up to 16 frames (a divisor of q where one is close) within 16 x 1080p of pixels "
+                        "passes of up to 32 frames (rt_max_frames()) (a divisor of q where one is close) within 16 x 1080p of pixels "
                         "per pass and rank; 1 for spp > 1, whose samples are batched inside each pass)")
+    p.add_argument("--sub-bands", type=int, default=None,
+                   help="N = 1: slots as groups of S band shares of one device, each rendering its rows of "
+                        "every frame of its group's passes in place (rt_render_bands_direct_async): S times "
+                        "the frames per pass at the same rays in flight.  Default: 2 when the timed frames give "
+                        "each slot fewer than 8 (K = 20: 2 groups x 10 frames, each pass half the rows), else 1")
     p.add_argument("--inflight", type=int, default=None,
                    help="frames in flight (F scene handles / HIP streams; default 4 = the box's hardware "
                         "queues per process, 3 from 4 ranks up); 1 = one at a time")
@@ -302,9 +307,9 @@ def seam_stats(args, scene, pipe, tiler, dev):
             if not args.animate:
                 c.origin[0] = 0.01 * (i % 64)
             return c
-        pipe.run(pipe.inflight * pipe.batch, cameras=cam)
+        pipe.run(pipe.round_frames, cameras=cam)
         torch.cuda.synchronize()
-        k = pipe.inflight * pipe.batch  # whole passes on every slot, as the headline's K frames
+        k = pipe.round_frames  # whole passes on every slot, as the headline's K frames
         e0.record(main)
         pipe.run(k, cameras=cam)
         e1.record(main)
@@ -316,9 +321,9 @@ def seam_stats(args, scene, pipe, tiler, dev):
     if args.spp == 1 and args.depth == 8:
         for t in pipe.tilers:
             t.depth = 9
-        pipe.run(pipe.inflight * pipe.batch)
+        pipe.run(pipe.round_frames)
         torch.cuda.synchronize()
-        k = pipe.inflight * pipe.batch
+        k = pipe.round_frames
         e0.record(main)
         pipe.run(k)
         e1.record(main)
@@ -385,24 +390,43 @@ def main():
     # 0.554).  With 16 frames per slot 4 x 16 wins at every N (K = 64, tools/r3_share5.sh:
     # N = 8: 0.251 vs 0.270 for 3 x 11, N = 4: 0.487 vs 0.508)
     inflight = max(1, args.inflight or (3 if world >= 4 and -(-args.steps // 4) < 8 else 4))
+    if args.sub_bands is None:
+        # Round 4 (config 3, K = 20, tools/subband_time.py, profiles/r4m/subband.txt): 4 slots x
+        # 5 whole frames 1.985 ms per frame, 2 groups x 2 shares x 10 frames 1.940, 1 group x 4
+        # shares 1.995; at K = 64 (16 frames per slot) 1.862 / 1.866 / 1.913 -- mixing more
+        # frames per pass pays only while passes are small
+        sub = 1
+        if world == 1 and args.spp == 1 and not args.force_gather and -(-args.steps // inflight) < 8:
+            # the most shares whose group still takes its frames in one pass per slot
+            from rust_tracer_amd import abi as _abi0
+            mf = int(_abi0.lib().rt_max_frames())
+            for cand in (4, 2):
+                if inflight % cand == 0 and -(-args.steps // (inflight // cand)) <= mf:
+                    sub = cand
+                    break
+    else:
+        sub = max(1, args.sub_bands)
+    groups = max(1, inflight // sub)
     if args.batch is None:
         # The timed K frames are spread evenly over the F slots: q = ceil(K / F) frames per
         # slot, in r = ceil(q / cap) passes of B frames -- a divisor of q when one is near
-        # ceil(q / r), so that every slot runs the same passes.  Up to 16 frames per pass
-        # (bounded workspace: <= 16 x 1080p of pixels per pass and rank, ~1.1 KB per pixel).
+        # ceil(q / r), so that every slot runs the same passes.  Up to rt_max_frames() (32)
+        # frames per pass within 16 x 1080p of pixels per pass and rank (bounded workspace,
+        # ~1.1 KB per pixel).
         # Round 2, ms per share-frame on one MI355X at K = 20 (tools/share_burst.py): N = 1:
         # B = 2 / 4 / 5 / 8: 2.46 / 2.51 / 2.31 / 2.36; N = 8: 0.533 / 0.464 / 0.389 / 0.381
         # (DESIGN.md "Frame batches")
-        share = band_rows_per_rank(args.height, args.band_rows, world) * args.width
+        share = band_rows_per_rank(args.height, args.band_rows, world) * args.width // sub
         if args.spp > 1:
             cap = 1
-        else:  # up to 16 frames (RT_MAX_FRAMES), within 16 x 1080p of pixels per pass and rank
+        else:  # up to 32 frames (RT_MAX_FRAMES), within 16 x 1080p of pixels per pass and rank
             # (~37 GB of workspace per slot, ~150 GB for 4 slots of the 288 GB): at K = 64, 4 x 16
             # 1118 - 1126 vs 4 x 8 1077 - 1084 Mpixels/s (tools/r3_steps2.sh).  Passes in flight
             # come first: at K = 20 bigger passes lost (4 x 5: 1027 / 1033, 3 x 7: 1018 / 1017,
             # 2 x 10: 750, 1 x 16: 796)
-            cap = max(1, min(16, (16 * 1920 * 1088) // share))
-        q = -(-args.steps // inflight)
+            from rust_tracer_amd import abi as _abi1
+            cap = max(1, min(int(_abi1.lib().rt_max_frames()), (16 * 1920 * 1088) // share))
+        q = -(-args.steps // groups)
         r = -(-q // cap)
         b = -(-q // r)
         for d in range(b, 0, -1):
@@ -414,7 +438,7 @@ def main():
         args.batch = max(1, b)
     pipe = FramePipeline(scene, desc, args.width, args.height, args.depth, args.band_rows, rank, world, dev,
                          spp=args.spp, seed=args.seed, inflight=inflight, batch=args.batch,
-                         rgb8=args.output == "rgb8", force_gather=bool(args.force_gather))
+                         rgb8=args.output == "rgb8", force_gather=bool(args.force_gather), sub_bands=sub)
     batch = pipe.batch
     tilers = pipe.tilers
     tiler = tilers[0]
@@ -439,7 +463,7 @@ def main():
 
     # slot set-up (untimed, like the scene upload): each slot's workspace is sized by its
     # first full pass
-    run_frames(inflight * batch)
+    run_frames(pipe.round_frames)
     run_frames(args.warmup)
     torch.cuda.synchronize()
     barrier()
@@ -449,12 +473,17 @@ def main():
     # pass), per frame; frames are deterministic, so the timed passes run these tests, uncounted
     ops = None
     if args.count_frame:
-        scene.set_scan_counting(True)
-        scene.scan_ops(reset=True)
-        tiler.render_local(batch, [anim_cam(i) for i in range(batch)] if args.animate else None)
+        counted = [t.scene for t in pipe.group_tilers(0)]  # one pass of group 0 (all its shares)
+        for sc in counted:
+            sc.set_scan_counting(True)
+            sc.scan_ops(reset=True)
+        pipe.render_pass(0, [anim_cam(i) for i in range(batch)] if args.animate else [_abi.camera(args.width, args.height)] * batch)
         torch.cuda.synchronize()
-        ops = {k: v / batch for k, v in scene.scan_ops().items()}
-        scene.set_scan_counting(False)
+        ops = {}
+        for sc in counted:
+            for k, v in sc.scan_ops().items():
+                ops[k] = ops.get(k, 0.0) + v / batch
+            sc.set_scan_counting(False)
     pipe.zero_counters()
 
     lat = []  # one (start, end) event pair per pass
@@ -490,10 +519,11 @@ def main():
         # copies: tiler.step() below re-renders into slot 0's buffers
         frames = [f.clone() for f in pipe.frames()]
         fcams = pipe.frame_cameras()
-        single = tiler.step()
+        whole = pipe.whole_tiler()
+        single = whole.step()
         if rank == 0:
             frames.append(single)
-            fcams.append(tiler.last_cams[0])
+            fcams.append(whole.last_cams[0])
         torch.cuda.synchronize()
         if rank == 0:
             refs = {}
@@ -515,7 +545,7 @@ def main():
             if single_ref is None:  # the oracle row check needs Camera::new's frame
                 single_ref = scene.render(args.width, args.height, args.depth, device=dev.index, spp=args.spp,
                                           seed=args.seed)[0]
-    seam = seam_stats(args, scene, pipe, tiler, dev) if (args.seam_stats and world == 1) else None
+    seam = seam_stats(args, scene, pipe, pipe.whole_tiler(), dev) if (args.seam_stats and world == 1) else None
     for t in tilers:  # every stream-ordered pass of the run, incl. the timed ones, was complete
         t.scene.sync_status()
     if seam is not None:
@@ -543,7 +573,7 @@ def main():
         brute_flops = local_scans * scene.flops_per_scan
         workload = (f"config{args.config}: {scene_label(args.config)}, {args.width}x{args.height}, "
                     f"depth {args.depth}" + (f", {args.spp} spp (jitter seed {args.seed})" if args.spp > 1 else ""))
-        traffic, traffic_note = load_traffic(args.traffic_json, workload, batch)
+        traffic, traffic_note = load_traffic(args.traffic_json, workload, batch if sub == 1 else f"{batch}/{sub}")
         roofline = {
             "bound": "valu",
             "achieved": round(achieved, 3) if ops else None,
@@ -554,7 +584,8 @@ def main():
             "kernel": ("one frame: trace_level_kernel per level + queue sorts + shadow_kernel + "
                        "combine_level_kernel per level"),
             "kernel_ms": round(kernel_ms, 4),
-            "kernel_ms_is": (f"timed-region HIP events / steps ({inflight} passes of {batch} frames in flight)"
+            "kernel_ms_is": (f"timed-region HIP events / steps ({inflight} passes of {batch} frames"
+                             + (f", each 1/{sub} of the rows," if sub > 1 else "") + " in flight)"
                              if inflight * batch > 1 else "timed-region HIP events / steps"),
             "flops_per_launch": per_launch_flops,
             "flops_is": ("the counted tests as executed: reference tests (translate-scale spheres at 33 flops, "
@@ -582,7 +613,7 @@ def main():
                 "source": traffic.get("sq_source"),
             } if traffic and traffic.get("sq_insts_valu_per_frame") else None),
             "profile": ({"path": traffic["profile"], "sources_sha": traffic["sources_sha"],
-                         "commit": traffic["commit"], "frames_per_pass": batch} if traffic else None),
+                         "commit": traffic["commit"], "frames_per_pass": batch, "sub_bands": sub} if traffic else None),
             "traffic_note": traffic_note,
             # exclusive per-kernel times (one frame at a time, nothing overlapping) of the profile
             "exclusive_kernel_ms_per_frame": traffic.get("exclusive_kernel_ms_per_frame") if traffic else None,
@@ -615,10 +646,11 @@ def main():
                 "spp": args.spp, "seed": args.seed, "band_rows": args.band_rows,
                 "frames": ("animation: frame i's camera origin x = 0.01 (i mod 64)" if args.animate
                            else "K renders of Camera::new (the reference's bench -n loop, main.rs:137-140)"),
-                "frames_in_flight": inflight * batch, "passes_in_flight": inflight,
-                "frames_per_pass": batch, "pass_latency_ms": round(latency_ms, 4), "output": args.output,
+                "frames_in_flight": groups * batch, "passes_in_flight": inflight,
+                "frames_per_pass": batch, "sub_bands": sub, "pass_latency_ms": round(latency_ms, 4),
+                "output": args.output,
                 "msamples_per_s": round(args.width * args.height * args.spp * steps / elapsed / 1e6, 3),
-                "parallelism": f"row-bands x{world}" + ((" + RCCL gather" if args.backend == "nccl"
+                "parallelism": f"row-bands x{world}" + (f" (x{sub} band shares per device)" if sub > 1 else "") + ((" + RCCL gather" if args.backend == "nccl"
                                                           else f" + {args.backend} gather (rehearsal)")
                                                          if world > 1 else ""),
                 "workspace_bytes_per_slot": max(t.scene.workspace_bytes for t in tilers),

@@ -138,9 +138,8 @@ typedef struct rt_counters {
                                (Scene::intersect from trace_ray, render.rs:47) */
     uint64_t shadow_rays;   /* scene scans for point-light shadow rays (mod.rs:193) */
     uint64_t pixels;        /* pixels rendered by this call */
-    uint64_t wave_iterations; /* megakernel loop iterations summed over waves (each is one
-                                 scan per active lane): lane utilisation =
-                                 (node_rays + shadow_rays) / (64 * wave_iterations) */
+    uint64_t wave_iterations; /* reserved, 0 (the per-pixel megakernel of round 1 counted its
+                                 loop iterations here; the level pipeline does not) */
 } rt_counters;
 
 typedef struct rt_render_opts {
@@ -246,7 +245,7 @@ rt_status rt_render_bands_async(const rt_scene* scene, const rt_camera* camera,
 rt_status rt_render_frame_async(const rt_scene* scene, const rt_camera* camera, uint32_t depth,
                                 float* d_rgb, uint8_t* d_rgb8, uint64_t* d_counters, void* stream);
 
-/* Frame batch: n_frames (1..16) frames of one resolution, each with its own camera, in one
+/* Frame batch: n_frames (1..rt_max_frames() = 32) frames of one resolution, each with its own camera, in one
  * pipeline pass (the per-level launch and latency floor is paid once per batch).  The ray
  * queues of a batch are ordered by ray alone -- rays of different frames that start in the
  * same place and head the same way share waves (an ordering property only: each task
@@ -260,7 +259,7 @@ rt_status rt_render_bands_batch_async(const rt_scene* scene, const rt_camera* ca
                                       float* d_rgb, uint64_t* d_counters, void* stream);
 
 /* The general stream-ordered render (every *_async render above is a special case of it):
- * n_frames (1..16) frames of one resolution, each with its own camera, spp jittered samples
+ * n_frames (1..rt_max_frames() = 32) frames of one resolution, each with its own camera, spp jittered samples
  * per pixel (spp > 1 needs n_frames == 1), this rank's row bands (as rt_render_bands_async).
  *  - d_rgb:  n_frames band buffers of f32 RGB (may be NULL when spp == 1 and d_rgb8 is set:
  *            then only the bytes are written);
@@ -272,6 +271,18 @@ rt_status rt_render_bands_batch_async(const rt_scene* scene, const rt_camera* ca
 rt_status rt_render_bands_ex_async(const rt_scene* scene, const rt_camera* cams, uint32_t n_frames, uint32_t depth,
                                    uint32_t spp, uint32_t seed, uint32_t band_rows, uint32_t rank, uint32_t world,
                                    float* d_rgb, uint8_t* d_rgb8, uint64_t* d_counters, void* stream);
+
+/* A frame batch (as rt_render_bands_batch_async) whose pixels land in place: d_frames holds
+ * n_frames WHOLE row-major frames (y_res x x_res x 3 floats each; d_frames8 optional, the
+ * Color::as_u8 bytes, same layout), and this call writes only this rank's rows of them --
+ * no band buffer, no padding rows, no un-permute.  `world` band shares of one device (each
+ * its own scene handle and stream) fill the same frames side by side; a pass then mixes
+ * twice (world 2) the frames of a whole-frame pass of the same size.  spp == 1 only.
+ * Every pixel equals rt_render's bit for bit.  No reference counterpart: the throughput
+ * form of render() (src/render.rs:31) over frames. */
+rt_status rt_render_bands_direct_async(const rt_scene* scene, const rt_camera* cams, uint32_t n_frames,
+                                       uint32_t depth, uint32_t band_rows, uint32_t rank, uint32_t world,
+                                       float* d_frames, uint8_t* d_frames8, uint64_t* d_counters, void* stream);
 
 /* Waits for every stream-ordered render enqueued on `scene` so far, on every stream one ran
  * on (the scene records an event per such stream after each render), and reports whether

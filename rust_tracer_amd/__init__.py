@@ -401,8 +401,18 @@ class DeviceScene:
                                                C.c_void_p(d_counters_ptr or None), C.c_void_p(stream_ptr)),
               "rt_render_bands_ex_async")
 
+    def render_bands_direct_async(self, cams, depth, band_rows, rank, world, d_frames_ptr, d_frames8_ptr,
+                                  d_counters_ptr, stream_ptr):
+        """rt_render_bands_direct_async: this rank's rows of len(cams) whole row-major frames,
+        written in place (f32 at d_frames_ptr and / or RGB8 at d_frames8_ptr)."""
+        arr = (abi.rt_camera * len(cams))(*cams)
+        check(self._L.rt_render_bands_direct_async(self.h, arr, len(cams), depth, band_rows, rank, world,
+                                                   C.c_void_p(d_frames_ptr or None), C.c_void_p(d_frames8_ptr or None),
+                                                   C.c_void_p(d_counters_ptr or None), C.c_void_p(stream_ptr)),
+              "rt_render_bands_direct_async")
+
     def render_bands_batch_async(self, cams, depth, band_rows, rank, world, d_rgb_ptr, d_counters_ptr, stream_ptr):
-        """rt_render_bands_batch_async: len(cams) frames (<= 16, one resolution) in one pipeline
+        """rt_render_bands_batch_async: len(cams) frames (<= rt_max_frames() = 32, one resolution) in one pipeline
         pass into len(cams) consecutive band buffers."""
         arr = (abi.rt_camera * len(cams))(*cams)
         check(self._L.rt_render_bands_batch_async(self.h, arr, len(cams), depth, band_rows, rank, world,

@@ -133,6 +133,8 @@ def lib():
                                               C.c_uint32, vp, vp, vp]
     L.rt_render_bands_ex_async.argtypes = [vp, P(rt_camera), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                            C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp]
+    L.rt_render_bands_direct_async.argtypes = [vp, P(rt_camera), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                               C.c_uint32, vp, vp, vp, vp]
     L.rt_render_frame_async.argtypes = [vp, P(rt_camera), C.c_uint32, vp, vp, vp, vp]
     L.rt_scene_sync_status.argtypes = [vp]
     L.rt_scene_clone.argtypes = [vp, C.c_int32, P(vp)]

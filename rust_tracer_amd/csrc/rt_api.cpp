@@ -1628,6 +1628,7 @@ struct PassOut {
     unsigned long long* counters;
     bool latch;
     bool may_sync;  // the caller waits anyway (rt_render, forests): deep passes stop at the first empty level
+    bool direct = false;  // rgb / rgb8 are whole frames: this rank's rows land in place (row-major)
 };
 
 static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t depth, uint32_t spp, uint32_t seed,
@@ -1753,6 +1754,11 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     p.frames = frames;
     p.frame_items = (uint32_t)total;
     p.frame_floats = (size_t)p.rows_local * p.width * 3u;
+    if (o.direct) {
+        if (spp_batch || forest_params) return RT_ERR_INVALID_ARG;
+        p.direct = 1u;
+        p.frame_floats = (size_t)p.height * p.width * 3u;
+    }
     if (frames > 1 && (uint64_t)cam->x_res * cam->y_res >= (1ull << RT_FRAME_SHIFT)) return RT_ERR_UNSUPPORTED;
     {
         // level 0 reads every frame's camera from cams[] (frames == 1: cams[0] = cam)
@@ -2061,9 +2067,9 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     return RT_OK;
 }
 
-rt_status rt_render_bands_ex_async(const rt_scene* scene, const rt_camera* cams, uint32_t n_frames, uint32_t depth,
+static rt_status render_bands_impl(const rt_scene* scene, const rt_camera* cams, uint32_t n_frames, uint32_t depth,
                                    uint32_t spp, uint32_t seed, uint32_t band_rows, uint32_t rank, uint32_t world,
-                                   float* d_rgb, uint8_t* d_rgb8, uint64_t* d_counters, void* stream) {
+                                   float* d_rgb, uint8_t* d_rgb8, uint64_t* d_counters, void* stream, bool direct) {
     rt_scene* s = const_cast<rt_scene*>(scene);
     if (!s || !cams || n_frames == 0 || n_frames > RT_MAX_FRAMES || spp == 0) return RT_ERR_INVALID_ARG;
     if (!d_rgb && (!d_rgb8 || spp > 1)) return RT_ERR_INVALID_ARG;  // spp > 1 accumulates in d_rgb
@@ -2077,7 +2083,7 @@ rt_status rt_render_bands_ex_async(const rt_scene* scene, const rt_camera* cams,
     rt_status st = ensure_ws(s, 0, 0);
     if (st != RT_OK) return st;
     hipStream_t hs = (hipStream_t)stream;
-    const PassOut o{d_rgb, d_rgb8, reinterpret_cast<unsigned long long*>(d_counters), true, false};
+    const PassOut o{d_rgb, d_rgb8, reinterpret_cast<unsigned long long*>(d_counters), true, false, direct};
     // A pass larger (level-0 items) or deeper than any this handle has completed is checked
     // before the call returns: the pool is sized from node_factor, which suits config-3-like
     // trees, and a mirror- or glass-heavy scene needs more.  The call waits for that pass, and
@@ -2147,6 +2153,22 @@ rt_status rt_render_bands_ex_async(const rt_scene* scene, const rt_camera* cams,
     }
     HIP_TRY(hipEventRecord(ev, hs));
     return RT_OK;
+}
+
+rt_status rt_render_bands_ex_async(const rt_scene* scene, const rt_camera* cams, uint32_t n_frames, uint32_t depth,
+                                   uint32_t spp, uint32_t seed, uint32_t band_rows, uint32_t rank, uint32_t world,
+                                   float* d_rgb, uint8_t* d_rgb8, uint64_t* d_counters, void* stream) {
+    return render_bands_impl(scene, cams, n_frames, depth, spp, seed, band_rows, rank, world, d_rgb, d_rgb8, d_counters,
+                             stream, false);
+}
+
+// This rank's rows of n_frames whole frames, written in place (include/rt_api.h): several
+// band shares of one device fill the same frames side by side with no assembly step
+rt_status rt_render_bands_direct_async(const rt_scene* scene, const rt_camera* cams, uint32_t n_frames,
+                                       uint32_t depth, uint32_t band_rows, uint32_t rank, uint32_t world,
+                                       float* d_frames, uint8_t* d_frames8, uint64_t* d_counters, void* stream) {
+    return render_bands_impl(scene, cams, n_frames, depth, 1, 0, band_rows, rank, world, d_frames, d_frames8,
+                             d_counters, stream, true);
 }
 
 rt_status rt_render_bands_spp_async(const rt_scene* scene, const rt_camera* cam, uint32_t depth, uint32_t spp,

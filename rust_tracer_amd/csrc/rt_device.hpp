@@ -172,12 +172,14 @@ enum : uint32_t {
 // frame batches (rt_render_bands_batch_async): up to RT_MAX_FRAMES frames of one
 // resolution in one pipeline pass; a task carries its frame in Task.pixel's top bits
 #ifndef RT_MAX_FRAMES
-#define RT_MAX_FRAMES 16  // 4 frame bits: Task.pixel bits 28-31
+#define RT_MAX_FRAMES 32  // 5 frame bits: Task.pixel bits 27-31 (frames of < 2^27 pixels)
 #endif
-#if RT_MAX_FRAMES > 16
-#define RT_FRAME_SHIFT 27  // 32 frames: bits 27-31 (frames of < 2^27 pixels)
+#if RT_MAX_FRAMES > 32
+#error "RT_MAX_FRAMES: at most 32 (5 frame bits in Task.pixel)"
+#elif RT_MAX_FRAMES > 16
+#define RT_FRAME_SHIFT 27
 #else
-#define RT_FRAME_SHIFT 28
+#define RT_FRAME_SHIFT 28  // -DRT_MAX_FRAMES=16: 4 frame bits, bits 28-31
 #endif
 struct FrameCam {
     float ox, oy, oz, x_min, y_max, x_delta, y_delta, pad;
@@ -189,7 +191,8 @@ struct WaveParams {
     uint32_t task_frame_shift;         // task key |= frame << this (frames > 1)
     uint32_t task_fine;                // key mode 7 with 5 more origin bits (a batch's 3 radix passes have room)
     uint32_t shadow_frame_shift;       // shadow key |= frame << this (frames > 1)
-    size_t frame_floats;               // output floats per frame (rows_local x width x 3)
+    size_t frame_floats;               // output floats per frame (rows_local x width x 3; direct: height x width x 3)
+    uint32_t direct;                   // out / out8 are whole frames: pixel (u, v) at v x width + u, padding never written
     FrameCam cams[RT_MAX_FRAMES];      // frames > 1: each frame's camera (render.rs:155-186)
     uint32_t width, height, depth;
     uint32_t band_rows, rank, world, rows_local;

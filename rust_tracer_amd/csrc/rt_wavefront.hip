@@ -951,8 +951,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_COMBINE_
         const uint32_t fr = level == 0 ? item_frame(P, t, local) : 0u;
         if (flags & NODE_NONE) {  // padding of the band buffer: defined as 0
             PixelRef px = pixel_of(P, local);
-            if (level == 0 && px.u < P.width && px.lr < P.rows_local) {
-                const size_t i = (size_t)px.lr * P.width + px.u;
+            if (level == 0 && px.u < P.width && px.lr < P.rows_local && !(P.direct && px.v >= P.height)) {
+                const size_t i = (size_t)(P.direct ? px.v : px.lr) * P.width + px.u;
                 if (P.out) {
                     float* o = P.out + (size_t)fr * P.frame_floats + i * 3u;
                     o[0] = 0.f;
@@ -1001,7 +1001,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_COMBINE_
         }
         if (level == 0) {
             PixelRef px = pixel_of(P, local);
-            const size_t i = (size_t)px.lr * P.width + px.u;
+            const size_t i = (size_t)(P.direct ? px.v : px.lr) * P.width + px.u;
             bool last = true;
             if (P.out) {  // (null: an RGB8-only pass, spp == 1)
                 float* o = P.out + (size_t)fr * P.frame_floats + i * 3u;

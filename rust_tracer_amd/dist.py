@@ -38,20 +38,27 @@ class FrameTiler:
     """Renders this rank's share of a frame and gathers the frame on rank 0."""
 
     def __init__(self, scene: DeviceScene, width, height, depth, band_rows=8, rank=0, world=1,
-                 device=None, spp=1, seed=0, batch=1, rgb8=False, force_gather=False, split=False):
+                 device=None, spp=1, seed=0, batch=1, rgb8=False, force_gather=False, split=False,
+                 frames_out=None):
         """rgb8: render and gather only Color::as_u8 bytes (3 B per pixel instead of 12; the
         level-0 combine writes them, rt_render_bands_ex_async with no float buffer).
         force_gather: at world 1 too, assemble through the process group's gather and the
         un-permute kernel (a one-rank communicator: runs the RCCL exchange on one GPU).
         split: at world 1, single frames (batch 1, spp 1, f32) go through rt_render_frame_async
         -- rt_render's two band shares side by side, stream-ordered -- instead of one pass
-        (render on a created torch stream, not the null stream: rt_api.h)."""
+        (render on a created torch stream, not the null stream: rt_api.h).
+        frames_out: a [batch, H, W, 3] tensor of whole frames this tiler's rank (a band share of
+        one device, world = the shares) fills in place (rt_render_bands_direct_async); the
+        other shares fill the rest of the same frames, and nothing is gathered."""
         self.scene = scene
         self.rgb8 = bool(rgb8) and spp == 1
         self.spp, self.seed = spp, seed
         self.w, self.h, self.depth = width, height, depth
         self.band_rows, self.rank, self.world = band_rows, rank, world
-        self.gather = world > 1 or bool(force_gather)
+        self.direct = frames_out is not None
+        if self.direct and (spp != 1 or force_gather or split):
+            raise ValueError("frames_out: spp 1, no gather, no split")
+        self.gather = not self.direct and (world > 1 or bool(force_gather))
         self.split = bool(split) and not self.gather and spp == 1 and not self.rgb8 and int(batch) == 1
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.rpr = band_rows_per_rank(height, band_rows, world)
@@ -62,7 +69,12 @@ class FrameTiler:
             self.batch = 1
         self.cam = abi.camera(width, height)
         dt = torch.uint8 if self.rgb8 else torch.float32
-        self.locals = torch.zeros((self.batch, self.rpr, width, 3), dtype=dt, device=self.device)
+        if self.direct:
+            assert tuple(frames_out.shape) == (self.batch, height, width, 3) and frames_out.dtype == dt
+            assert frames_out.is_contiguous() and frames_out.device == self.device
+            self.locals = frames_out
+        else:
+            self.locals = torch.zeros((self.batch, self.rpr, width, 3), dtype=dt, device=self.device)
         self.local = self.locals[0]
         self.counters = torch.zeros(3, dtype=torch.int64, device=self.device)
         self.gathered = None
@@ -85,7 +97,12 @@ class FrameTiler:
         assert n <= self.batch
         cams = list(cams) if cams is not None else [self.cam] * n
         self.last_cams = cams
-        if self.rgb8:
+        if self.direct:
+            ptr = self.locals.data_ptr()
+            self.scene.render_bands_direct_async(cams, self.depth, self.band_rows, self.rank, self.world,
+                                                 0 if self.rgb8 else ptr, ptr if self.rgb8 else 0,
+                                                 self.counters.data_ptr(), stream)
+        elif self.rgb8:
             self.scene.render_bands_ex_async(cams, self.depth, self.band_rows, self.rank, self.world, 0,
                                              self.locals.data_ptr(), self.counters.data_ptr(), stream)
         elif n == 1 and self.split:  # the frame's rows land row-major at the buffer's start
@@ -135,22 +152,42 @@ class FramePipeline:
 
     Slot i = its own scene handle (slot 0 the caller's, the others rt_scene_clone: each its
     own workspace; one handle never runs two renders at once, mirroring the reference's
-    !Sync Scene) + its own HIP stream + its own FrameTiler.  Frame k renders on slot k % inflight.  At world > 1 each frame's
+    !Sync Scene) + its own HIP stream + its own FrameTiler.  Pass k renders on slot k % inflight.  At world > 1 each pass's
     gather + un-permute runs on the caller's stream once its slot is done, and the slot's
     next render waits on an event recorded after that gather (the gather reads the slot's
-    band buffer).  Every frame is rendered and gathered in full."""
+    band buffer).  Every frame is rendered and gathered in full.
+
+    sub_bands S > 1 (world 1 only): the slots form inflight / S groups of S band shares; pass
+    k's frames go to group k % groups, whose S slots each render their share of the rows of
+    every frame of the pass straight into the group's frame buffer
+    (rt_render_bands_direct_async, 8-row bands dealt over the S shares).  A pass then mixes S
+    times as many frames as a whole-frame pass with the same rays in flight -- more rays
+    from the same place per wave (DESIGN.md "Frames in flight")."""
 
     def __init__(self, scene: DeviceScene, desc, width, height, depth, band_rows=8, rank=0, world=1,
                  device=None, spp=1, seed=0, inflight=4, batch=1, rgb8=False, grid_share=75,
-                 force_gather=False):
+                 force_gather=False, sub_bands=1):
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.inflight = max(1, int(inflight))
         self.world = world
-        # slot i > 0: a clone of the scene (device copy, own workspace and stream)
-        self.tilers = [FrameTiler(scene if i == 0 else scene.clone(self.device.index), width, height,
-                                  depth, band_rows, rank, world, self.device, spp=spp, seed=seed, batch=batch,
-                                  rgb8=rgb8, force_gather=force_gather)
-                       for i in range(self.inflight)]
+        self.sub_bands = max(1, int(sub_bands))
+        S = self.sub_bands
+        if S > 1 and (world != 1 or spp != 1 or force_gather or self.inflight % S):
+            raise ValueError("sub_bands > 1: world 1, spp 1, no forced gather, inflight a multiple of sub_bands")
+        self.groups = self.inflight // S
+        scenes = [scene if i == 0 else scene.clone(self.device.index) for i in range(self.inflight)]
+        if S == 1:
+            self.tilers = [FrameTiler(scenes[i], width, height, depth, band_rows, rank, world, self.device, spp=spp,
+                                      seed=seed, batch=batch, rgb8=rgb8, force_gather=force_gather)
+                           for i in range(self.inflight)]
+        else:
+            nb = max(1, min(int(batch), int(abi.lib().rt_max_frames())))
+            dt = torch.uint8 if rgb8 else torch.float32
+            self.group_frames = [torch.zeros((nb, height, width, 3), dtype=dt, device=self.device)
+                                 for _ in range(self.groups)]
+            self.tilers = [FrameTiler(scenes[i], width, height, depth, band_rows, i % S, S, self.device, batch=nb,
+                                      rgb8=rgb8, frames_out=self.group_frames[i // S])
+                           for i in range(self.inflight)]
         self.gather = self.tilers[0].gather
         # several passes share the GPU: each pass's persistent grids take 75% of the chip
         # (DESIGN.md "Frames in flight"; one pass at a time keeps the whole chip)
@@ -160,10 +197,16 @@ class FramePipeline:
             for t in self.tilers:
                 t.scene.set_grid_share(self.grid_share)
         self.frame_index = 0        # frames enqueued so far (the `cameras` callback's argument)
-        self.pass_index = 0         # passes enqueued so far: pass k runs on slot k % inflight
+        self.pass_index = 0         # passes enqueued so far: pass k runs on group k % groups
         self.batch = self.tilers[0].batch
         self.streams = [torch.cuda.Stream(device=self.device) for _ in range(self.inflight)]
         self._reuse = [None] * self.inflight
+        self._whole = None
+
+    @property
+    def round_frames(self):
+        """frames of one pass on every slot group (the unit of whole passes)"""
+        return self.groups * self.batch
 
     @property
     def counters(self):
@@ -174,38 +217,57 @@ class FramePipeline:
         for t in self.tilers:
             t.counters.zero_()
 
+    def group_tilers(self, g):
+        return self.tilers[g * self.sub_bands:(g + 1) * self.sub_bands]
+
+    def whole_tiler(self):
+        """A tiler of whole frames (batch 1) on slot 0's scene: tilers[0] itself unless the
+        slots are band shares (then one made on first use)."""
+        if self.sub_bands == 1:
+            return self.tilers[0]
+        if self._whole is None:
+            t0 = self.tilers[0]
+            self._whole = FrameTiler(t0.scene, t0.w, t0.h, t0.depth, 8, 0, 1, self.device, rgb8=t0.rgb8)
+        return self._whole
+
+    def render_pass(self, g, cams):
+        """One pass of group g on the current stream (untimed uses: counting, checks)."""
+        for t in self.group_tilers(g):
+            t.render_local(len(cams), cams)
+
     def run(self, n, latency_events=None, cameras=None):
         """Enqueue n frames (asynchronous) in passes of up to `batch` frames, pass k (counted
-        across calls) on slot k % inflight; the caller's stream waits for all of them.  latency_events: a list
-        that receives one (start, end) event pair per pass.  cameras: a callable giving the
-        rt_camera of frame i (frames numbered across calls; default Camera::new) -- an
-        animation, each frame its own view."""
+        across calls) on slot group k % groups; the caller's stream waits for all of them.
+        latency_events: a list that receives one (start, end) event pair per pass (per slot).
+        cameras: a callable giving the rt_camera of frame i (frames numbered across calls;
+        default Camera::new) -- an animation, each frame its own view."""
         main = torch.cuda.current_stream(self.device)
         for s in self.streams:
             s.wait_stream(main)
         while n > 0:
             b = min(self.batch, n)
             n -= b
-            i = self.pass_index % self.inflight
+            g = self.pass_index % self.groups
             self.pass_index += 1
-            st = self.streams[i]
-            with torch.cuda.stream(st):
-                if self._reuse[i] is not None:
-                    st.wait_event(self._reuse[i])
-                if latency_events is not None:
-                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                    ev[0].record(st)
-                cams = [cameras(self.frame_index + j) for j in range(b)] if cameras is not None else None
-                self.tilers[i].render_local(b, cams)
-                self.frame_index += b
-                if latency_events is not None:
-                    ev[1].record(st)
-                    latency_events.append(ev)
-            if self.gather:
-                main.wait_stream(st)
-                self.tilers[i].assemble()
-                self._reuse[i] = torch.cuda.Event()
-                self._reuse[i].record(main)
+            cams = [cameras(self.frame_index + j) for j in range(b)] if cameras is not None else None
+            self.frame_index += b
+            for i in range(g * self.sub_bands, (g + 1) * self.sub_bands):
+                st = self.streams[i]
+                with torch.cuda.stream(st):
+                    if self._reuse[i] is not None:
+                        st.wait_event(self._reuse[i])
+                    if latency_events is not None:
+                        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                        ev[0].record(st)
+                    self.tilers[i].render_local(b, cams)
+                    if latency_events is not None:
+                        ev[1].record(st)
+                        latency_events.append(ev)
+                if self.gather:
+                    main.wait_stream(st)
+                    self.tilers[i].assemble()
+                    self._reuse[i] = torch.cuda.Event()
+                    self._reuse[i].record(main)
         for s in self.streams:
             main.wait_stream(s)
 
@@ -222,15 +284,19 @@ class FramePipeline:
         if err is not None:
             raise err
 
+    def _leads(self):
+        """one tiler per frame buffer: every slot, or each group's first share"""
+        return self.tilers[::self.sub_bands]
+
     def frames(self):
-        """every frame of each slot's last pass, assembled (rank 0; [] elsewhere).  Checks
-        every slot's overflow status first: an incomplete frame is never returned."""
+        """every frame of each slot's (group's) last pass, assembled (rank 0; [] elsewhere).
+        Checks every slot's overflow status first: an incomplete frame is never returned."""
         self.sync()
-        return [t.frames[b] for t in self.tilers if t.frames is not None for b in range(t.last)]
+        return [t.frames[b] for t in self._leads() if t.frames is not None for b in range(t.last)]
 
     def frame_cameras(self):
         """the rt_camera of every frame frames() returns, in the same order"""
-        return [t.last_cams[b] for t in self.tilers if t.frames is not None for b in range(t.last)]
+        return [t.last_cams[b] for t in self._leads() if t.frames is not None for b in range(t.last)]
 
     def set_material(self, index, material):
         """rt_scene_set_material on every slot's scene (slot clones are independent copies),

@@ -9,12 +9,6 @@ forked from and joined into the caller's stream.
 - a queue overflow in either share is reported by rt_scene_sync_status, never returned as a
   silent RT_OK, and the grown pools then render the full frame;
 - a material edit reaches both shares' scene clones.
-
-The file name sorts it after every other GPU test file on purpose: run before
-test_gpu_fullframe / test_gpu_parity / test_gpu_seam in one process, these tests made
-test_gpu_seam.py::test_pipeline_overflow_is_raised see no overflow (twice, reproducibly),
-while every pairing of two of those files passes and the whole suite passes with this file
-last (profiles/r3y/README.md; the cause is not found yet, DESIGN.md "Next").
 """
 import numpy as np
 import pytest

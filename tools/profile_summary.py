@@ -99,14 +99,21 @@ def main():
         print(f"warning: the tree's sources ({sources_sha()}) are not the profiled ones ({sha})")
     # PMC passes: (suffix, frames per pass, frames rendered in the run: the slot's set-up pass + steps)
     # (b1: --steps 4 after a 1-frame set-up pass; bN: --steps N after an N-frame set-up pass)
-    sizes = sorted(int(d[len("pmc_fetch_b"):]) for d in os.listdir(src)
-                   if d.startswith("pmc_fetch_b") and d[len("pmc_fetch_b"):].isdigit())
-    runs = [(f"_b{n}", n, 2 * n) for n in sizes]  # the slot's set-up pass + one timed pass
+    # (bNsS: N-frame passes over S band shares of the device, bench.py --sub-bands S: entry "N/S")
+    import re
+    runs = []
+    for d in sorted(os.listdir(src)):
+        m = re.fullmatch(r"pmc_fetch_b(\d+)(?:s(\d+))?", d)
+        if m:
+            n, s = int(m.group(1)), int(m.group(2) or 1)
+            runs.append((d[len("pmc_fetch"):], n if s == 1 else f"{n}/{s}", 2 * n))
+    runs.sort(key=lambda r: (isinstance(r[1], str), r[2]))
     result = {}
     for suf, per_pass, pmc_frames in runs:
         fe, f_fe = pmc_table(os.path.join(src, "pmc_fetch" + suf), "FETCH_SIZE")
         wr, f_wr = pmc_table(os.path.join(src, "pmc_write" + suf), "WRITE_SIZE")
-        label = f"{per_pass} frame{'s' if per_pass > 1 else ''} per pass"
+        label = (f"{per_pass} frame{'s' if per_pass > 1 else ''} per pass" if isinstance(per_pass, int) else
+                 f"{per_pass.split('/')[0]} frames per pass over {per_pass.split('/')[1]} band shares")
         out += ["", f"## HBM bytes per frame, {label} (MB; FETCH_SIZE x 2 + WRITE_SIZE, KB counters)", "",
                 "| kernel | fetch x2 | write | total |", "|---|---|---|---|"]
         tf = tw = 0.0

@@ -41,7 +41,8 @@ def plan(mode):
     out = []
     for g in range(groups):
         fr = list(range(g * q, min(K, (g + 1) * q)))
-        chunks = [fr[k:k + 16] for k in range(0, len(fr), 16)]
+        mf = int(abi.lib().rt_max_frames())
+        chunks = [fr[k:k + mf] for k in range(0, len(fr), mf)]
         for ch in chunks:
             for j in range(S):
                 out.append((g * S + j, j, S, ch))
@@ -54,7 +55,8 @@ tilers = {}
 def tiler(slot, rank, world):
     key = (slot, rank, world)
     if key not in tilers:
-        tilers[key] = FrameTiler(scenes[slot], W, H, DEPTH, 8, rank, world, dev, batch=16)
+        tilers[key] = FrameTiler(scenes[slot], W, H, DEPTH, 8, rank, world, dev,
+                                  batch=int(abi.lib().rt_max_frames()))
     return tilers[key]
 
 
@@ -69,7 +71,7 @@ def run(mode, base):
         main.wait_stream(s)
 
 
-modes = ["frames", "bands2", "bands4"]
+modes = (os.environ.get("MODES") or "frames bands2 bands4").split()
 for m in modes:  # workspaces sized, kernels loaded
     run(m, 0)
     run(m, 0)
