@@ -4,7 +4,7 @@
 #   trace/          rocprofv3 kernel trace of that run (kernels overlap: 4 passes in flight)
 #   trace1/         kernel trace one frame at a time (--inflight 1 --batch 1): exclusive times
 #   pmc_*_bN[sS]/   PMC passes (FETCH_SIZE, WRITE_SIZE, SQ) for passes of N = 1, 5, 16 frames
-#                   on one slot, and 10 frames over S = 2 band shares (PMC collection serialises
+#                   on one slot, and 20 frames over S = 4 band shares (PMC collection serialises
 #                   the dispatches anyway)
 # usage: tools/profile.sh TAG   -> gpurun_out/TAG/   (summary: tools/profile_summary.py TAG)
 set -o pipefail
@@ -23,8 +23,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
     python bench.py --steps 6 --warmup 1 --inflight 1 --batch 1 $B --count-frame 0 > $OUT/trace1.log 2>&1 || exit 4
 echo traces
 # a size N/S: passes of N frames over S band shares of the device (bench.py --sub-bands S; the
-# driver's K = 20 runs 10/2), one group of S slots
-for spec in ${SIZES:-1 5 16 10/2}; do
+# driver's K = 20 runs 20/4), one group of S slots
+for spec in ${SIZES:-1 5 16 20/4}; do
   n=${spec%/*}; s=1; [ "$spec" != "$n" ] && s=${spec#*/}
   args="--steps $n --warmup 0 --inflight $s --sub-bands $s --batch $n $B --count-frame 0"
   [ "$s" = 1 ] && suf=$n || suf=${n}s$s
