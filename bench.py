@@ -360,6 +360,11 @@ def load_traffic(path, workload, frames_per_pass):
 
 def main():
     args = parse()
+    # stdout carries exactly the one JSON line: libraries that print banners to fd 1 (RCCL's
+    # "RCCL version : ..." at communicator creation) write to stderr instead
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -395,8 +400,12 @@ def main():
         # 5 whole frames 1.985 ms per frame, 2 groups x 2 shares x 10 frames 1.940, 1 group x 4
         # shares 1.995; at K = 64 (16 frames per slot) 1.862 / 1.866 / 1.913 -- mixing more
         # frames per pass pays only while passes are small
+        # At N = 2 too (rank 0's share on one MI355X, K = 20, profiles/r4l/subband.txt: 4 x 5
+        # 1.026, 3 x 7 1.019, 2 x 2 x 10 1.008, 1 x 4 x 20 0.997 ms per share-frame); from N = 4
+        # the 3 x 7 whole-share passes stay ahead (N = 4: 0.547 vs 0.556 / 0.567; N = 8: 0.309
+        # vs 0.330 / 0.370) -- a share of a share is too small a pass there
         sub = 1
-        if world == 1 and args.spp == 1 and not args.force_gather and -(-args.steps // inflight) < 8:
+        if world <= 2 and args.spp == 1 and -(-args.steps // inflight) < 8:
             # the most shares whose group still takes its frames in one pass per slot
             from rust_tracer_amd import abi as _abi0
             mf = int(_abi0.lib().rt_max_frames())
@@ -668,7 +677,8 @@ def main():
             out["seam"] = seam
         if world == 1 and args.cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, desc, single_ref)
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if use_pg:
         dist.destroy_process_group()
 

@@ -1598,6 +1598,7 @@ rt_status rt_scene_set_tuning(rt_scene* s, const char* tuning) {
     if (!tune_apply(t, tuning, false)) return RT_ERR_INVALID_ARG;
     auto set = [&](rt_scene* c) {  // clones share the scene-build keys
         c->tune = t;
+        c->occ_trace = 0;  // the kernels' LDS may differ: occupancy measured again
         return RT_OK;
     };
     (void)set(s);

@@ -513,6 +513,8 @@ typedef const uint4 cuint4;
 template <class C>
 __device__ __forceinline__ void bvh_leaf(const DevScene& S, uint32_t li, V3 o, V3 d, float on, float tmax,
                                          float& bt, uint32_t& bk, C& c, lfloat4* ldsph = nullptr) {
+    // (the descriptor from LDS instead -- staged after the sphere pairs, a broadcast read and
+    // 8 readfirstlanes -- measured flat: 1091.7 vs 1093.1 Mpixels/s in 4 pairs, profiles/r4l)
     cuint4* lp = (cuint4*)S.bvh_leaves + 2 * li;
     uint4 a = lp[0], b = lp[1];
     if (ldsph)  // a hierarchy leaf, in a kernel that staged the sphere pairs
@@ -545,6 +547,7 @@ __device__ __forceinline__ bool shadow_decided(V3 o, V3 d, float bt, float l2) {
 __device__ __forceinline__ lfloat4* lds_dsph(const DevScene& S, lfloat4* lnodes) {
     return lnodes + 4 * S.n_bvh_nodes + ((S.graze_lane && S.graze_res) ? 8 * S.n_graze_blk : 0);
 }
+
 // LDS: node records staged in LDS by the kernel (lnodes != null), else read via SMEM
 // novote (shadow): the lane's hierarchy primitives are settled already (light buffer).
 template <bool SHADOW, bool LDS, class C>
@@ -990,7 +993,7 @@ __device__ __forceinline__ void lb_pass(const DevScene& S, uint32_t base, V3 o, 
 //    distance^2 >= |pos - p|^2 (the margin covers the rounding of p + d t and of the
 //    norms) and can neither shadow nor hide a nearer hit: the walk stops at tlim.
 // A wave leaves the scan when every active lane is decided.  Returns `shadowed`.
-template <bool LDS, class C>
+template <bool LDS, class C, bool SPLIT = false>
 __device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lpos, C& c, lfloat4* lnodes,
                                             uint32_t lb_base = 0xFFFFFFFFu) {
     RT_T0(C, t_s);
@@ -998,7 +1001,11 @@ __device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lp
     const float l2 = len2(sub(lpos, o));
     float bt = __builtin_huge_valf();
     uint32_t bk = 0xFFFFFFFFu;
+    // SPLIT (the shadow kernel's counting frames): planes in cyc_load, the light-buffer pass in
+    // cyc_post, the hierarchy walk in cyc_self -- slots the trace kernel uses for other things
+    RT_T0(C, t_pl);
     planes(S, o, d, bt, bk, c);
+    if (SPLIT) RT_T1(C, c, cyc_load, t_pl);
     bool done = shadow_decided(o, d, bt, l2);
     if (__ballot(!done) == 0) goto finish;
     if (S.use_bvh) {
@@ -1009,10 +1016,14 @@ __device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lp
             const float dx = o.x - S.bvh_cx, dy = o.y - S.bvh_cy, dz = o.z - S.bvh_cz;
             const float D = sqrtf(dx * dx + dy * dy + dz * dz) + S.bvh_r;
             lb = lb_base != 0xFFFFFFFFu && D <= S.lb_dmax && l2 <= RT_LB_LMAX * RT_LB_LMAX;
+            RT_T0(C, t_lb);
             if (__ballot(lb)) lb_pass(S, lb_base, o, d, on, tlim, l2, lb, bt, bk, c);
+            if (SPLIT) RT_T1(C, c, cyc_post, t_lb);
         }
+        RT_T0(C, t_w);
         if (__ballot(!lb && !shadow_decided(o, d, bt, l2)))
             bvh_walk<true, LDS>(S, o, d, bt, bk, tlim, l2, c, lnodes, lb);
+        if (SPLIT) RT_T1(C, c, cyc_self, t_w);
         done = shadow_decided(o, d, bt, l2);
         if (__ballot(!done) == 0) goto finish;
         graze_pass<LDS>(S, o, d, bt, bk, c, gp, lnodes, done);

@@ -818,7 +818,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
                 V3 lpos = v3(L.px, L.py, L.pz);
                 V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
                 n_shadow++;
-                lit = !shadow_scan<LDS>(S, ps, ldir, lpos, cnt, lnodes, L.lb_base);
+                lit = !shadow_scan<LDS, decltype(cnt), true>(S, ps, ldir, lpos, cnt, lnodes, L.lb_base);
             }
             q = tn < count ? P.node_ps[en >> P.light_bits] : make_float4(0.f, 0.f, 0.f, 0.f);
             if (lit) atomicOr(&P.node_lit[n], 1u << li);
@@ -843,7 +843,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
                 V3 lpos = v3(L.px, L.py, L.pz);
                 V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
                 n_shadow++;
-                if (!shadow_scan<LDS>(S, ps, ldir, lpos, cnt, lnodes, L.lb_base)) atomicOr(&P.node_lit[n], 1u << li);
+                if (!shadow_scan<LDS, decltype(cnt), true>(S, ps, ldir, lpos, cnt, lnodes, L.lb_base))
+                    atomicOr(&P.node_lit[n], 1u << li);
             }
         }
     }
@@ -1134,12 +1135,14 @@ hipError_t launch_wave_init(uint32_t* levels, uint32_t n_words, uint32_t total_i
 // kernel its six); Tune::lds_nodes=0: never, =trace / =shadow: only that kernel (A/B).  The
 // hierarchy's triangle pairs staged as well (27.9 KB; records from LDS in VGPRs instead of
 // SGPRs, shadow kernel down to five blocks) lost 7.5%: 865 / 867 / 862 vs 936 / 932 / 933.
-static size_t lds_bytes(const WaveParams& p) {
+// kernel_bit 1: the trace kernels, 2: shadow (the same records today)
+static size_t lds_bytes(const WaveParams& p, uint32_t kernel_bit) {
+    (void)kernel_bit;
     return (size_t)p.S.n_bvh_nodes * 64 + ((p.S.graze_lane && p.S.graze_res) ? (size_t)p.S.n_graze_blk * 128 : 0) +
            (size_t)p.S.n_dsph_bvh * 64;
 }
 static bool lds_nodes_for(const WaveParams& p, uint32_t kernel_bit) {
-    size_t lds = lds_bytes(p);
+    size_t lds = lds_bytes(p, kernel_bit);
     if (!(p.lds_mask & kernel_bit)) return false;
     return p.S.use_bvh && lds > 0 && lds <= 32 * 1024;
 }
@@ -1148,7 +1151,7 @@ static bool lds_nodes_for(const WaveParams& p, uint32_t kernel_bit) {
 // bytes (the persistent grids are sized from these, so that every block is resident)
 hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_blocks, int* combine_blocks,
                           int* trace_each) {
-    const size_t lds = lds_bytes(p);
+    const size_t lds = lds_bytes(p, 1u), lds_sh = lds_bytes(p, 2u);
     const bool aware = true;  // (grids sized as if no LDS were used: blocks waited for a slot)
     // every trace instantiation launch_wave_trace may pick (generic, level 0, deep levels):
     // the grid is sized by the least occupancy among them, so every block is resident
@@ -1168,7 +1171,7 @@ hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_bl
     if (trace_each)
         for (int i = 0; i < 3; i++) trace_each[i] = tv[i];
     e = aware && lds_nodes_for(p, 2u)
-            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<true, false>, 256, lds)
+            ? hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<true, false>, 256, lds_sh)
             : hipOccupancyMaxActiveBlocksPerMultiprocessor(shadow_blocks, shadow_kernel<false, false>, 256, 0);
     if (e != hipSuccess) return e;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(combine_blocks, combine_level_kernel, 256, 0);
@@ -1185,7 +1188,7 @@ hipError_t wave_occupancy(const WaveParams& p, int* trace_blocks, int* shadow_bl
 // with more resident blocks per CU gets its grid scaled up to match
 hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hipStream_t stream,
                              const int* occ_each, int occ_min) {
-    const size_t lds = lds_bytes(p);
+    const size_t lds = lds_bytes(p, 1u);
     const bool use = lds_nodes_for(p, 1u);
     // the deep instantiation past level 0 and the inline shadow levels (deep_kernel=0: never, A/B)
     const bool deep_ok = p.deep_kernel != 0;
@@ -1221,7 +1224,7 @@ hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hi
 }
 
 hipError_t launch_wave_shadow(const WaveParams& p, int blocks, hipStream_t stream) {
-    const size_t lds = lds_bytes(p);
+    const size_t lds = lds_bytes(p, 2u);
     const bool use = lds_nodes_for(p, 2u);
     const bool count = (p.count_mask & 2u) != 0;
     if (use && count)

@@ -39,7 +39,7 @@ class FrameTiler:
 
     def __init__(self, scene: DeviceScene, width, height, depth, band_rows=8, rank=0, world=1,
                  device=None, spp=1, seed=0, batch=1, rgb8=False, force_gather=False, split=False,
-                 frames_out=None):
+                 frames_out=None, band_out=None):
         """rgb8: render and gather only Color::as_u8 bytes (3 B per pixel instead of 12; the
         level-0 combine writes them, rt_render_bands_ex_async with no float buffer).
         force_gather: at world 1 too, assemble through the process group's gather and the
@@ -49,7 +49,10 @@ class FrameTiler:
         (render on a created torch stream, not the null stream: rt_api.h).
         frames_out: a [batch, H, W, 3] tensor of whole frames this tiler's rank (a band share of
         one device, world = the shares) fills in place (rt_render_bands_direct_async); the
-        other shares fill the rest of the same frames, and nothing is gathered."""
+        other shares fill the rest of the same frames, and nothing is gathered.
+        band_out: a [batch, rows_per_rank, W, 3] tensor (a slice of a caller's buffer) that
+        receives this rank's band buffers; the caller assembles them (FramePipeline's gathered
+        band-share groups), this tiler never gathers."""
         self.scene = scene
         self.rgb8 = bool(rgb8) and spp == 1
         self.spp, self.seed = spp, seed
@@ -58,7 +61,8 @@ class FrameTiler:
         self.direct = frames_out is not None
         if self.direct and (spp != 1 or force_gather or split):
             raise ValueError("frames_out: spp 1, no gather, no split")
-        self.gather = not self.direct and (world > 1 or bool(force_gather))
+        self.external = band_out is not None
+        self.gather = not self.direct and not self.external and (world > 1 or bool(force_gather))
         self.split = bool(split) and not self.gather and spp == 1 and not self.rgb8 and int(batch) == 1
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.rpr = band_rows_per_rank(height, band_rows, world)
@@ -73,6 +77,10 @@ class FrameTiler:
             assert tuple(frames_out.shape) == (self.batch, height, width, 3) and frames_out.dtype == dt
             assert frames_out.is_contiguous() and frames_out.device == self.device
             self.locals = frames_out
+        elif self.external:
+            assert tuple(band_out.shape) == (self.batch, self.rpr, width, 3) and band_out.dtype == dt
+            assert band_out.is_contiguous() and band_out.device == self.device
+            self.locals = band_out
         else:
             self.locals = torch.zeros((self.batch, self.rpr, width, 3), dtype=dt, device=self.device)
         self.local = self.locals[0]
@@ -83,7 +91,7 @@ class FrameTiler:
             # one gather per pass: every rank's `batch` band buffers, rank-major
             self.gathered = torch.zeros((world, self.batch, self.rpr, width, 3), dtype=dt, device=self.device)
             self.frames = torch.zeros((self.batch, height, width, 3), dtype=dt, device=self.device)
-        elif not self.gather:
+        elif not self.gather and not self.external:
             self.frames = self.locals[:, :height]
         self.frame = self.frames[0] if self.frames is not None else None
         self.last = 1               # frames in the last pass
@@ -157,12 +165,16 @@ class FramePipeline:
     next render waits on an event recorded after that gather (the gather reads the slot's
     band buffer).  Every frame is rendered and gathered in full.
 
-    sub_bands S > 1 (world 1 only): the slots form inflight / S groups of S band shares; pass
-    k's frames go to group k % groups, whose S slots each render their share of the rows of
-    every frame of the pass straight into the group's frame buffer
-    (rt_render_bands_direct_async, 8-row bands dealt over the S shares).  A pass then mixes S
-    times as many frames as a whole-frame pass with the same rays in flight -- more rays
-    from the same place per wave (DESIGN.md "Frames in flight")."""
+    sub_bands S > 1: the slots form inflight / S groups of S band shares; pass k's frames go to
+    group k % groups, whose S slots each render their share of the rows of every frame of the
+    pass.  A pass then mixes S times as many frames as a whole-frame pass with the same rays
+    in flight -- more rays from the same place per wave (DESIGN.md "Band-share slot groups").
+    At world 1 the shares write straight into the group's frames
+    (rt_render_bands_direct_async, 8-row bands dealt over the S shares).  At world > 1 rank r's
+    share j is band rank r*S + j of a world of W*S: its band buffer is slice j of the group's
+    [S, B, rows, W, 3] buffer, which is the rank's contribution to ONE gather per group pass
+    (rank-major, so the gathered buffer is virtual-rank-major) and rank 0 un-permutes it with
+    W*S ranks."""
 
     def __init__(self, scene: DeviceScene, desc, width, height, depth, band_rows=8, rank=0, world=1,
                  device=None, spp=1, seed=0, inflight=4, batch=1, rgb8=False, grid_share=75,
@@ -172,15 +184,19 @@ class FramePipeline:
         self.world = world
         self.sub_bands = max(1, int(sub_bands))
         S = self.sub_bands
-        if S > 1 and (world != 1 or spp != 1 or force_gather or self.inflight % S):
-            raise ValueError("sub_bands > 1: world 1, spp 1, no forced gather, inflight a multiple of sub_bands")
+        if S > 1 and (spp != 1 or self.inflight % S):
+            raise ValueError("sub_bands > 1: spp 1, inflight a multiple of sub_bands")
         self.groups = self.inflight // S
+        self.rank = rank
+        self.band_rows = band_rows
+        self.w, self.h = width, height
+        self.group_gather = S > 1 and (world > 1 or bool(force_gather))
         scenes = [scene if i == 0 else scene.clone(self.device.index) for i in range(self.inflight)]
         if S == 1:
             self.tilers = [FrameTiler(scenes[i], width, height, depth, band_rows, rank, world, self.device, spp=spp,
                                       seed=seed, batch=batch, rgb8=rgb8, force_gather=force_gather)
                            for i in range(self.inflight)]
-        else:
+        elif not self.group_gather:
             nb = max(1, min(int(batch), int(abi.lib().rt_max_frames())))
             dt = torch.uint8 if rgb8 else torch.float32
             self.group_frames = [torch.zeros((nb, height, width, 3), dtype=dt, device=self.device)
@@ -188,6 +204,26 @@ class FramePipeline:
             self.tilers = [FrameTiler(scenes[i], width, height, depth, band_rows, i % S, S, self.device, batch=nb,
                                       rgb8=rgb8, frames_out=self.group_frames[i // S])
                            for i in range(self.inflight)]
+        else:
+            nb = max(1, min(int(batch), int(abi.lib().rt_max_frames())))
+            dt = torch.uint8 if rgb8 else torch.float32
+            self.vworld = world * S
+            rpr = band_rows_per_rank(height, band_rows, self.vworld)
+            self.group_local = [torch.zeros((S, nb, rpr, width, 3), dtype=dt, device=self.device)
+                                for _ in range(self.groups)]
+            self.tilers = [FrameTiler(scenes[i], width, height, depth, band_rows, rank * S + i % S, self.vworld,
+                                      self.device, batch=nb, rgb8=rgb8, band_out=self.group_local[i // S][i % S])
+                           for i in range(self.inflight)]
+            self.group_gathered = self.group_frames = None
+            if rank == 0:
+                self.group_gathered = [torch.zeros((world, S, nb, rpr, width, 3), dtype=dt, device=self.device)
+                                       for _ in range(self.groups)]
+                self.group_frames = [torch.zeros((nb, height, width, 3), dtype=dt, device=self.device)
+                                     for _ in range(self.groups)]
+            for i, t in enumerate(self.tilers):
+                t.frames = self.group_frames[i // S] if rank == 0 else None
+                t.frame = t.frames[0] if t.frames is not None else None
+        self.rgb8 = bool(rgb8)
         self.gather = self.tilers[0].gather
         # several passes share the GPU: each pass's persistent grids take 75% of the chip
         # (DESIGN.md "Frames in flight"; one pass at a time keeps the whole chip)
@@ -268,8 +304,38 @@ class FramePipeline:
                     self.tilers[i].assemble()
                     self._reuse[i] = torch.cuda.Event()
                     self._reuse[i].record(main)
+            if self.group_gather:
+                self._assemble_group(g, b, main)
         for s in self.streams:
             main.wait_stream(s)
+
+    def _assemble_group(self, g, n, main):
+        """One gather of group g's [S, B, rows, W, 3] buffer to rank 0 (on the caller's
+        stream, after every share of the pass), then one un-permute of its n frames over the
+        W*S virtual ranks; the group's slots wait for it before their next render."""
+        S = self.sub_bands
+        for i in range(g * S, (g + 1) * S):
+            main.wait_stream(self.streams[i])
+        local = self.group_local[g]
+        world = self.world
+        if dist.get_backend() == "gloo":
+            host = local.cpu()
+            glist = [torch.empty_like(host) for _ in range(world)] if self.rank == 0 else None
+            dist.gather(host, gather_list=glist, dst=0)
+            if self.rank == 0:
+                for r in range(world):
+                    self.group_gathered[g][r].copy_(glist[r])
+        else:
+            glist = [self.group_gathered[g][r] for r in range(world)] if self.rank == 0 else None
+            dist.gather(local, gather_list=glist, dst=0)
+        if self.rank == 0:
+            unpermute_bands_batch_async(self.group_gathered[g].data_ptr(), self.w, self.h, self.band_rows, self.vworld,
+                                        n, local.shape[1], self.group_frames[g].data_ptr(),
+                                        main.cuda_stream, rgb8=self.rgb8)
+        ev = torch.cuda.Event()
+        ev.record(main)
+        for i in range(g * S, (g + 1) * S):
+            self._reuse[i] = ev
 
     def sync(self):
         """Wait for every slot's enqueued passes; raises RtError(RT_ERR_CAPACITY) if one of

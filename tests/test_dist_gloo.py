@@ -65,3 +65,49 @@ def test_gather_reassembles_frame(world, h):
         p.join(120)
         assert p.exitcode == 0
     assert q.get() is True
+
+
+def _worker_sub(rank, world, sub, port, h, w, band, q):
+    """FramePipeline's gathered band-share groups (rust_tracer_amd/dist.py): rank r's share j
+    is band rank r*S + j of a world of W*S; the rank's [S, rows, W] buffer is its one gather
+    contribution, and rank 0 un-permutes the gathered buffer over W*S ranks."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rust_tracer_amd.dist import band_rows_per_rank_py, local_rows
+        vworld = world * sub
+        rpr = band_rows_per_rank_py(h, band, vworld)
+        local = torch.full((sub, rpr, w), -1.0)
+        for j in range(sub):
+            for lr, v in enumerate(local_rows(h, band, rank * sub + j, vworld)):
+                if v >= 0:
+                    local[j, lr] = float(v)
+        glist = [torch.empty_like(local) for _ in range(world)] if rank == 0 else None
+        dist.gather(local, gather_list=glist, dst=0)
+        if rank == 0:
+            gathered = torch.stack(glist).reshape(vworld, rpr, w)  # virtual-rank-major
+            frame = torch.full((h, w), -2.0)
+            for v in range(h):
+                b = v // band
+                r = b % vworld
+                lr = (b // vworld) * band + (v - b * band)
+                frame[v] = gathered[r, lr]
+            q.put(bool(torch.equal(frame[:, 0], torch.arange(h, dtype=torch.float32))))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,sub,h", [(2, 2, 1080), (2, 4, 117), (3, 2, 90)])
+def test_gather_band_share_groups(world, sub, h):
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_sub, args=(r, world, sub, port, h, 5, 8, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert q.get() is True

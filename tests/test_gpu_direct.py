@@ -7,7 +7,9 @@ whole frames in place) and of FramePipeline's sub-band slot groups (bench.py at 
   padding rows are never written: a guard frame after the batch keeps its sentinel);
 - spp != 1 has no direct form; invalid ranks are rejected before any work;
 - FramePipeline(sub_bands=2): every group's frames equal single renders (animation cameras),
-  counters too; sub_bands needs world 1 and a slot count it divides.
+  counters too; sub_bands needs a slot count it divides;
+- the gathered form of the groups (world > 1: one gather per group pass, un-permuted over
+  W*S virtual ranks), run on one rank through a forced gather.
 """
 import numpy as np
 import pytest
@@ -111,3 +113,42 @@ def test_pipeline_sub_bands_equals_single_renders():
     with pytest.raises(ValueError):
         FramePipeline(s, desc, w, h, depth, inflight=3, batch=2, sub_bands=2)
     s.close()
+
+
+def test_pipeline_sub_bands_gathered_groups():
+    """World > 1's form of the groups, on one rank: force_gather routes every group pass through
+    one process-group gather (gloo, one rank) and the un-permute over W*S virtual ranks."""
+    import os
+    import socket
+
+    import torch.distributed as dist
+    from rust_tracer_amd.dist import FramePipeline
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        desc = SceneDesc.synth_config(3)
+        w, h, depth = 160, 90, 8
+        s = DeviceScene(desc)
+        pipe = FramePipeline(s, desc, w, h, depth, inflight=4, batch=3, sub_bands=4, force_gather=True)
+        assert pipe.group_gather and pipe.groups == 1
+
+        def cam(i):
+            c = abi.camera(w, h)
+            c.origin[0] = 0.01 * (i % 64)
+            return c
+        pipe.run(6, cameras=cam)  # two passes of 3 frames on the one group
+        torch.cuda.synchronize()
+        frames, fc = pipe.frames(), pipe.frame_cameras()
+        assert len(frames) == 3
+        for f, c in zip(frames, fc):
+            ref, _, _, _ = s.render(w, h, depth, cam=c)
+            assert np.array_equal(f.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+        pipe.close()
+        s.close()
+    finally:
+        dist.destroy_process_group()

@@ -2,6 +2,9 @@
   frames: slot i renders frames [i*K/4, (i+1)*K/4) whole (bench.py today);
   bands S: slot i renders sub-band i % S (rank i % S of a world of S) of frame group i // S,
            i.e. each pass mixes S times as many frames, each a 1/S share.
+WORLD=W (default 1): rank 0's share of a W-rank run instead (slots render rank 0 of W, or
+virtual rank j of W*S -- the rank's S sub-shares); F=slots (default 4).  Times are per
+frame of the share.
 usage: python tools/subband_time.py [K] [reps]"""
 import os
 import sys
@@ -15,7 +18,9 @@ from rust_tracer_amd.dist import FrameTiler  # noqa: E402
 
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 REPS = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-W, H, DEPTH, F = 1920, 1080, 8, 4
+W, H, DEPTH = 1920, 1080, 8
+F = int(os.environ.get("F", "4"))
+WORLD = int(os.environ.get("WORLD", "1"))
 dev = torch.device("cuda", 0)
 scene = DeviceScene(SceneDesc.synth_config(3))
 scenes = [scene] + [scene.clone(0) for _ in range(F - 1)]
@@ -34,7 +39,7 @@ def plan(mode):
     """[(slot, rank, world, [frame indices])] passes in enqueue order"""
     if mode == "frames":
         q = -(-K // F)
-        return [(i, 0, 1, list(range(i * q, min(K, (i + 1) * q)))) for i in range(F)]
+        return [(i, 0, WORLD, list(range(i * q, min(K, (i + 1) * q)))) for i in range(F)]
     S = int(mode[5:])
     groups = F // S
     q = -(-K // groups)
@@ -45,7 +50,7 @@ def plan(mode):
         chunks = [fr[k:k + mf] for k in range(0, len(fr), mf)]
         for ch in chunks:
             for j in range(S):
-                out.append((g * S + j, j, S, ch))
+                out.append((g * S + j, j, WORLD * S, ch))
     return out
 
 
@@ -88,7 +93,7 @@ for r in range(REPS):
         base += K
 for m in modes:
     v = sorted(res[m])
-    print(f"K={K} {m:7s} ms/frame median {v[len(v) // 2]:.4f} min {v[0]:.4f} "
+    print(f"K={K} WORLD={WORLD} F={F} {m:7s} ms/frame median {v[len(v) // 2]:.4f} min {v[0]:.4f} "
           f"-> {W * H / (v[len(v) // 2] / 1e3) / 1e6:.1f} Mpixels/s  all {[round(x, 3) for x in res[m]]}")
 for s in scenes:
     s.sync_status()
