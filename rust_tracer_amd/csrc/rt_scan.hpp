@@ -1021,6 +1021,13 @@ __device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lp
             if (SPLIT) RT_T1(C, c, cyc_post, t_lb);
         }
         RT_T0(C, t_w);
+#if RT_STATS
+        {  // slot 15: lanes a hierarchy walk serves (no light buffer, undecided)
+            const uint64_t wl = __ballot(!lb && !shadow_decided(o, d, bt, l2));
+            if (wl && __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == (uint32_t)__builtin_ctzll(__ballot(1)))
+                atomicAdd(&rt_scan_stats[15], (unsigned long long)__builtin_popcountll(wl));
+        }
+#endif
         if (__ballot(!lb && !shadow_decided(o, d, bt, l2)))
             bvh_walk<true, LDS>(S, o, d, bt, bk, tlim, l2, c, lnodes, lb);
         if (SPLIT) RT_T1(C, c, cyc_self, t_w);

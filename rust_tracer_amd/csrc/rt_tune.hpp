@@ -26,7 +26,7 @@ struct Tune {
     int bvh_tris = 1;         // loose triangles in the hierarchy (0: linear)
     int dark_skip = 1;        // shadowed lights skipped in the combine where exact
     double bvh_cnode = 400.0; // SAH node cost
-    int bvh_maxleaf = 32;     // primitives per leaf at most
+    int bvh_maxleaf = 16;     // primitives per leaf at most (32 until round 4: K = 20 +0.9%, K = 64 flat)
     int force_rccl = 0;       // rt_scene_create_multi with one device: a one-rank communicator
     // ---- per pass
     int sort_tasks = 1;       // order the trace queues spatially

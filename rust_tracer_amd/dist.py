@@ -177,7 +177,7 @@ class FramePipeline:
     W*S ranks."""
 
     def __init__(self, scene: DeviceScene, desc, width, height, depth, band_rows=8, rank=0, world=1,
-                 device=None, spp=1, seed=0, inflight=4, batch=1, rgb8=False, grid_share=75,
+                 device=None, spp=1, seed=0, inflight=4, batch=1, rgb8=False, grid_share=None,
                  force_gather=False, sub_bands=1):
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.inflight = max(1, int(inflight))
@@ -225,9 +225,12 @@ class FramePipeline:
                 t.frame = t.frames[0] if t.frames is not None else None
         self.rgb8 = bool(rgb8)
         self.gather = self.tilers[0].gather
-        # several passes share the GPU: each pass's persistent grids take 75% of the chip
-        # (DESIGN.md "Frames in flight"; one pass at a time keeps the whole chip)
-        self.grid_share = int(grid_share)
+        # several passes share the GPU: each pass's persistent trace grids take 75% of the chip
+        # (DESIGN.md "Frames in flight"; one pass at a time keeps the whole chip), 50% as band
+        # shares -- their passes always run side by side (K = 20, 4 shares, 4 runs each: 35 /
+        # 45 / 50 / 55 / 65 / 75%: 1100 / 1121 / 1119 / 1116 / 1108 / 1100 Mpixels/s,
+        # profiles/r4ab/)
+        self.grid_share = int(grid_share if grid_share is not None else (50 if self.sub_bands > 1 else 75))
         self._caller_share = scene.grid_share   # slot 0 is the caller's scene: restored by close()
         if self.inflight > 1:
             for t in self.tilers:

@@ -26,5 +26,7 @@ for depth in (1, 2, 8):
               f"occupancy {v[b + 1] / max(1, v[b]):.3f}; per ray needed {v[b + 1] / max(1, n):.2f}, "
               f"executed {v[b] / max(1, n):.2f}")
     print(f"  hit points: inside the Morton cube {v[11]}, outside {v[12]} (level 0: {v[13]} / {v[14]})")
+    print(f"  shadow rays a hierarchy walk serves (no light buffer, undecided after the planes): {v[15]} "
+          f"of {cnt['shadow_rays']} ({v[15] / max(1, cnt['shadow_rays']):.3f})")
     print(f"  hit paths per wave scan: dsph {v[1] / max(1, v[0]):.2f} gsph {v[2] / max(1, v[0]):.2f} "
           f"tri {v[3] / max(1, v[0]):.2f} cube-tri {v[4] / max(1, v[0]):.2f}")
