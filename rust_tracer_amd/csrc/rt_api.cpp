@@ -222,6 +222,8 @@ struct LbPrim {
     uint32_t shape;  // insertion index of the primitive's shape (a pair record: this member's)
     double h3;       // this primitive's own bound h_P(D) at D = 3 R (+ the slab terms): how far
                      // from it a hit it reports can lie, for any origin within 3 R of the centre
+    double p2, p1, p0;  // ... as the polynomial h_P(D) = ((p2 D + p1) D + p0) (1 + 1e-6)
+    double h_at(double D) const { return ((p2 * D + p1) * D + p0) * (1 + 1e-6); }
 };
 
 struct RunLayout {
@@ -537,6 +539,7 @@ constexpr double LB_MU = 2e-3, LB_RHO = 0.05;  // LB_LMAX: RT_LB_LMAX (rt_device
 // tested exactly like a leaf (prefetching run loops).
 struct LightBuffers {
     uint32_t res = 0;
+    uint32_t tiers = 0;             // tier t: origins with D <= dmax 2^t (cells at base + t 6 res^2)
     std::vector<uint32_t> base;     // per light: leaf index of its first cell, or ~0 (no buffer)
     float dmax = 0.f;
 };
@@ -562,7 +565,6 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
     // origins farther than D_max from the scene ball's centre (+ R) use the hierarchy walk
     const double dmax = 3.0 * (double)L.r;
     B.dmax = down_f(dmax);
-    const double hmax = ((double)L.g2 * dmax + (double)L.g1) * dmax + (double)L.g0;
     // cell centres and angular radii (max angle to a corner, +1%)
     const int nc = 6 * R * R;
     std::vector<double> cdir(3 * (size_t)nc), ccos(nc), csin(nc), crad(nc);
@@ -588,33 +590,72 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
             }
     const double PI = 3.14159265358979323846;
     const double FACE_HALF = 0.9556;  // a face's directions lie within 54.75 deg of its axis
+    // Tier t serves origins with D <= dmax 2^t and a light within LB_LMAX 2^t (the device
+    // compares with down_f(dmax) 2^t and RT_LB_LMAX^2 4^t): every primitive's ball grown by
+    // its own bound at that reach (at most the hierarchy's), its cone by LB_MU 2^t (the
+    // direction error |delta d| (1 + Lambda / rho) doubles with Lambda's limit).  Tiers beyond
+    // the first catch the walk's costliest rays -- far origins, whose bound grows as D^2
+    // (DESIGN.md "Where the shadow scan's cycles go").
+    auto hmax_at = [&](double dm) { return ((double)L.g2 * dm + (double)L.g1) * dm + (double)L.g0; };
+    auto grown = [&](const LbPrim& p, double dm) { return (p.r + std::min(p.h_at(dm), hmax_at(dm))) * (1 + 1e-6); };
+    auto light_ok = [&](const double lp[3], double dm) {  // no grown ball comes within LB_RHO of the light
+        for (const LbPrim& p : L.lb_prims) {
+            const double w[3] = {p.c[0] - lp[0], p.c[1] - lp[1], p.c[2] - lp[2]};
+            if (!(std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]) - grown(p, dm) >= LB_RHO)) return false;
+        }
+        return true;
+    };
+    // per light: the most tiers (<= Tune::lb_tiers) whose grown balls all keep LB_RHO from it
+    const int max_tiers = std::max(1, std::min(7, T.lb_tiers));
+    auto tiers_of = [&](const double lp[3]) {
+        int n = 0;
+        while (n < max_tiers && light_ok(lp, dmax * (double)(1 << n))) n++;
+        return n;
+    };
+    B.tiers = 0;
+#if RT_DIAG
+    if (std::getenv("RT_LB_DEBUG"))
+        for (const LightRec& lr : lights) {
+            const double lp[3] = {lr.px, lr.py, lr.pz};
+            int ok_t = 0;
+            while (ok_t < 7 && light_ok(lp, dmax * (double)(1 << ok_t))) ok_t++;
+            double near = 1e30;
+            for (const LbPrim& p : L.lb_prims) {
+                const double w[3] = {p.c[0] - lp[0], p.c[1] - lp[1], p.c[2] - lp[2]};
+                near = std::min(near, std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]) - p.r);
+            }
+            std::fprintf(stderr, "light (%g %g %g): tiers it supports %d (nearest ball surface %g); R %g\n",
+                         lp[0], lp[1], lp[2], ok_t, near, (double)L.r);
+        }
+#endif
     for (size_t li = 0; li < lights.size(); li++) {
         if (lights[li].kind != RT_LIGHT_POINT) continue;
         const double lp[3] = {lights[li].px, lights[li].py, lights[li].pz};
+        const int tiers = tiers_of(lp);
+        if (tiers == 0) continue;  // a primitive (nearly) at the light: no buffer
+        const uint32_t base = (uint32_t)(L.leaves.size() / 8);
+        if (base >= (1u << 28)) continue;  // (the tier count sits in LightRec::lb_base's top bits)
+        B.tiers = std::max(B.tiers, (uint32_t)tiers);
+        for (int t = 0; t < tiers; t++) {
+        const double dm = dmax * (double)(1 << t);
         struct Cone {
             double u[3], alpha, ca, sa, near;
             uint32_t code;
         };
         std::vector<Cone> cones;
-        bool ok = true;
         for (const LbPrim& p : L.lb_prims) {
             double w[3] = {p.c[0] - lp[0], p.c[1] - lp[1], p.c[2] - lp[2]};
             const double dist = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-            const double rr = (p.r + std::min(p.h3, hmax)) * (1 + 1e-6);
-            if (!(dist - rr >= LB_RHO)) {  // a primitive (nearly) at the light: no buffer
-                ok = false;
-                break;
-            }
+            const double rr = grown(p, dm);
             Cone c;
             for (int k = 0; k < 3; k++) c.u[k] = w[k] / dist;
-            c.alpha = std::asin(rr / dist) + LB_MU;
+            c.alpha = std::asin(std::min(1.0, rr / dist)) + LB_MU * (double)(1 << t);
             c.ca = std::cos(c.alpha);
             c.sa = std::sin(c.alpha);
             c.near = dist - rr;
             c.code = p.code;
             cones.push_back(c);
         }
-        if (!ok) continue;
         // nearest first: every cell's list comes out sorted by distance from the light
         std::stable_sort(cones.begin(), cones.end(), [](const Cone& a, const Cone& b) { return a.near < b.near; });
         std::vector<std::vector<std::pair<uint32_t, double>>> lists(nc);  // (code, nearest distance)
@@ -641,7 +682,6 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
                 }
             }
         }
-        const uint32_t base = (uint32_t)(L.leaves.size() / 8);
         for (int cc = 0; cc < nc; cc++) {
             // per type, nearest first; each copy carries its nearest distance to the light
             // (down-rounded) in the record's spare slot: the device stops a run at the first
@@ -687,7 +727,8 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
             rec[7] = (uint32_t)(L.cube.size() / 16);
             L.leaves.insert(L.leaves.end(), rec, rec + 8);
         }
-        B.base[li] = base;
+        }  // tiers
+        B.base[li] = base | ((uint32_t)tiers << 28);
     }
 }
 
@@ -940,9 +981,10 @@ void build_runs(const std::vector<SphIn>& sph, const std::vector<TriIn>& tris, c
             // every primitive, which the smallest sphere sets), at D = 3 R, plus the slab terms
             const Coef& q = coef[pi];
             const double d3 = 3.0 * (double)L.r;  // the buffers' D_max
-            const double h3 = ((q.a2 * d3 + q.a1 + SAFETY_SLAB * 16.0 * FEPS) * d3 + q.a0 + q.cC * Cn +
-                               SAFETY_SLAB * 8.0 * FEPS * (3.0 * Cn + R)) * (1 + 1e-6);
-            L.lb_prims.push_back(LbPrim{{g.c[0], g.c[1], g.c[2]}, g.r, (type << 30) | (uint32_t)rec, kb >> 4, h3});
+            const double p2 = q.a2, p1 = q.a1 + SAFETY_SLAB * 16.0 * FEPS,
+                         p0 = q.a0 + q.cC * Cn + SAFETY_SLAB * 8.0 * FEPS * (3.0 * Cn + R);
+            const double h3 = ((p2 * d3 + p1) * d3 + p0) * (1 + 1e-6);
+            L.lb_prims.push_back(LbPrim{{g.c[0], g.c[1], g.c[2]}, g.r, (type << 30) | (uint32_t)rec, kb >> 4, h3, p2, p1, p0});
         };
         for (const auto& leaf : T.leaves) {
             std::vector<const SphIn*> ds, gs;
@@ -1475,6 +1517,7 @@ rt_status rt_scene_create_tuned(const rt_scene_desc* d, int32_t device, const ch
     S.graze_lane = tn.graze_lane ? 1u : 0u;  // 0: the wave-union grazing path (A/B)
     S.lb_res = lbuf.res;
     S.lb_dmax = lbuf.dmax;
+    S.lb_tiers = lbuf.tiers;
     S.n_graze_blk = (int32_t)(lay.graze_blk.size() / 32);
 #if RT_DIAG
     if (std::getenv("RT_DEBUG_NO_GRAZE")) S.n_graze_blk = 0;  // measurement only: NOT exact (the grazing pass's cost)

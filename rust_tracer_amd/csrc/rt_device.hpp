@@ -55,7 +55,7 @@ struct LightRec {
     int32_t kind;
     float px, py, pz;
     float r, g, b;
-    uint32_t lb_base;  // first cell of the light's light buffer (DevScene::lb_cells), ~0: none
+    uint32_t lb_base;  // light buffer: first cell (a bvh_leaves index) in bits 0-27, tier count in bits 28-30; ~0: none
 };
 
 // Kernel-argument view of an uploaded scene (pointers into the one allocation).
@@ -96,7 +96,8 @@ struct DevScene {
     // light buffers (shadow rays; rt_api.cpp build_light_buffers): per point light
     // 6 x lb_res x lb_res cells, each a leaf of bvh_leaves (LightRec::lb_base + cell)
     uint32_t lb_res;           // 0: no light buffers
-    float lb_dmax;             // origins with D above it walk the hierarchy
+    float lb_dmax;             // tier t of a light's buffer holds origins with D <= lb_dmax 2^t
+    uint32_t lb_tiers;         // the most tiers of any light (each light's own count: LightRec::lb_base bits 28-30)
     int32_t dark_skip;         // 1: every hit normal is finite with |n| <= 1e3 (shadowed-light skip, light_sum)
 };
 #define RT_LB_LMAX 45.f        // ... and so do origins farther than this from the light

@@ -25,7 +25,7 @@
 #define RT_STATS 0
 #endif
 #if RT_STATS
-__device__ unsigned long long rt_scan_stats[16];
+__device__ unsigned long long rt_scan_stats[32];
 #define RT_STAT(i) do { if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == \
     (uint32_t)__builtin_ctzll(__ballot(1))) atomicAdd(&rt_scan_stats[i], 1ull); } while (0)
 #else
@@ -666,6 +666,22 @@ __device__ __forceinline__ uint32_t lb_cell(uint32_t res, V3 v) {
     return (f * res + (uint32_t)j) * res + (uint32_t)i;
 }
 
+// The light-buffer tier a shadow ray's origin falls in -- the first tier t with D <=
+// lb_dmax 2^t and a light within RT_LB_LMAX 2^t (the buffers built for that reach and that
+// direction error, rt_api.cpp build_light_buffers) -- or -1: no buffer (the light has none,
+// or the origin lies beyond its tiers) -- walk.  LightRec::lb_base: the light's first cell in
+// bits 0-27, its tier count in bits 28-30 (~0: no buffer).
+__device__ __forceinline__ int lb_tier(const DevScene& S, uint32_t lb_base, V3 o, float l2) {
+    if (!S.lb_res || lb_base == 0xFFFFFFFFu) return -1;
+    const int tiers = (int)((lb_base >> 28) & 7u);
+    const float dx = o.x - S.bvh_cx, dy = o.y - S.bvh_cy, dz = o.z - S.bvh_cz;
+    const float D = sqrtf(dx * dx + dy * dy + dz * dz) + S.bvh_r;
+    float thr = S.lb_dmax, lm2 = RT_LB_LMAX * RT_LB_LMAX;
+    for (int t = 0; t < tiers; t++, thr *= 2.f, lm2 *= 4.f)
+        if (D <= thr && l2 <= lm2) return t;
+    return -1;
+}
+
 // Grazing pass: every hierarchy triangle whose plane some lane's ray meets at
 // sin(phi) < 1.01 sin(phi_min) is tested exactly for the wave (the hierarchy's bounds
 // do not cover it).  Triangles come in blocks of 8 with similar normals; a block whose
@@ -1013,19 +1029,35 @@ __device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lp
         float tlim = (sqrtf(l2) * (1.f + 0.0009765625f) + 1e-5f * (on + 1.f)) / sqrtf(len2(d));
         bool lb = false;
         if (S.lb_res) {
-            const float dx = o.x - S.bvh_cx, dy = o.y - S.bvh_cy, dz = o.z - S.bvh_cz;
-            const float D = sqrtf(dx * dx + dy * dy + dz * dz) + S.bvh_r;
-            lb = lb_base != 0xFFFFFFFFu && D <= S.lb_dmax && l2 <= RT_LB_LMAX * RT_LB_LMAX;
+            const int tier = lb_tier(S, lb_base, o, l2);
+            lb = tier >= 0;
             RT_T0(C, t_lb);
-            if (__ballot(lb)) lb_pass(S, lb_base, o, d, on, tlim, l2, lb, bt, bk, c);
+            if (__ballot(lb))
+                lb_pass(S, (lb_base & 0x0FFFFFFFu) + (tier > 0 ? (uint32_t)tier * 6u * S.lb_res * S.lb_res : 0u), o, d,
+                        on, tlim, l2, lb, bt, bk, c);
             if (SPLIT) RT_T1(C, c, cyc_post, t_lb);
         }
         RT_T0(C, t_w);
 #if RT_STATS
-        {  // slot 15: lanes a hierarchy walk serves (no light buffer, undecided)
-            const uint64_t wl = __ballot(!lb && !shadow_decided(o, d, bt, l2));
-            if (wl && __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == (uint32_t)__builtin_ctzll(__ballot(1)))
-                atomicAdd(&rt_scan_stats[15], (unsigned long long)__builtin_popcountll(wl));
+        {  // slot 15: lanes a hierarchy walk serves (no light buffer, undecided); slots 16-21:
+           // those lanes by D / R in (0,3] (3,6] (6,12] (12,25] (25,50] (50,inf); 22: light
+           // farther than RT_LB_LMAX
+            const bool w = !lb && !shadow_decided(o, d, bt, l2);
+            const uint64_t wl = __ballot(w);
+            const bool first = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) ==
+                               (uint32_t)__builtin_ctzll(__ballot(1));
+            if (wl && first) atomicAdd(&rt_scan_stats[15], (unsigned long long)__builtin_popcountll(wl));
+            if (wl) {
+                const float dx = o.x - S.bvh_cx, dy = o.y - S.bvh_cy, dz = o.z - S.bvh_cz;  // (stats)
+                const float q = (sqrtf(dx * dx + dy * dy + dz * dz) + S.bvh_r) / S.bvh_r;
+                const int b = q <= 3.f ? 0 : q <= 6.f ? 1 : q <= 12.f ? 2 : q <= 25.f ? 3 : q <= 50.f ? 4 : 5;
+                for (int k = 0; k < 6; k++) {
+                    const uint64_t m = __ballot(w && b == k);
+                    if (m && first) atomicAdd(&rt_scan_stats[16 + k], (unsigned long long)__builtin_popcountll(m));
+                }
+                const uint64_t far_l = __ballot(w && l2 > RT_LB_LMAX * RT_LB_LMAX);
+                if (far_l && first) atomicAdd(&rt_scan_stats[22], (unsigned long long)__builtin_popcountll(far_l));
+            }
         }
 #endif
         if (__ballot(!lb && !shadow_decided(o, d, bt, l2)))

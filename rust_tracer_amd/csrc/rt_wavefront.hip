@@ -718,10 +718,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                                 // seen from the light), or flag | Morton for rays that walk
                                 const LightRec& L = S.lights[li];
                                 const V3 raw = sub(v3(L.px, L.py, L.pz), sh_ps);
-                                const float dx = sh_ps.x - S.bvh_cx, dy = sh_ps.y - S.bvh_cy, dz = sh_ps.z - S.bvh_cz;
-                                const float D = sqrtf(dx * dx + dy * dy + dz * dz) + S.bvh_r;
-                                const bool lb = L.lb_base != 0xFFFFFFFFu && D <= S.lb_dmax &&
-                                                len2(raw) <= RT_LB_LMAX * RT_LB_LMAX;
+                                const bool lb = lb_tier(S, L.lb_base, sh_ps, len2(raw)) >= 0;
                                 if (!lb) {
                                     low = (1u << (P.shadow_fine - 1u)) |
                                           (P.shadow_fine >= 19u ? mort << (P.shadow_fine - 19u) : mort >> (19u - P.shadow_fine));
@@ -1262,11 +1259,11 @@ hipError_t launch_wave_combine(const WaveParams& p, uint32_t level, int blocks, 
 
 #if RT_STATS
 // tools/scan_stats.py: read (and optionally reset) the wavefront pipeline's scan counters
-extern "C" int rt_debug_scan_stats(unsigned long long* out16, int reset) {
-    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(rtdev::rt_scan_stats), 16 * sizeof(unsigned long long)) != hipSuccess)
+extern "C" int rt_debug_scan_stats(unsigned long long* out32, int reset) {
+    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(rtdev::rt_scan_stats), 32 * sizeof(unsigned long long)) != hipSuccess)
         return 1;
     if (reset) {
-        unsigned long long z[16] = {};
+        unsigned long long z[32] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(rtdev::rt_scan_stats), z, sizeof(z)) != hipSuccess) return 1;
     }
     return 0;

@@ -159,6 +159,27 @@ def test_shape_buffers_change_nothing(case, monkeypatch):
         assert same_bits(img, out[0][0]) and cnt == out[0][1]
 
 
+@pytest.mark.parametrize("case", [None] + CASES)
+def test_light_buffer_tiers_change_nothing(case):
+    """Light-buffer tiers (rt_api.cpp build_light_buffers: tier t serves shadow-ray origins
+    with D <= 3 R 2^t and a light within 45 * 2^t, its records' balls grown by their bound at
+    that reach): frames and counters identical with one tier, the default, seven, and no
+    light buffers at all (every shadow ray walks the hierarchy)."""
+    if case is None:
+        desc, w, h, depth, cam = SceneDesc.synth_config(3), 480, 270, 8, None
+    else:
+        seed, scale, cam_mode, near, slivers = case
+        desc, w, h, depth = stress_scene(seed, scale, near, slivers), 160, 120, 8
+        cam = stress_camera(w, h, scale, cam_mode)
+    out = []
+    for tune in (None, "lb_tiers=1", "lb_tiers=7", "lb_res=0"):
+        s = DeviceScene(desc, device=0, tuning=tune)
+        out.append(s.render(w, h, depth, cam=cam)[:2])
+        s.close()
+    for img, cnt in out[1:]:
+        assert same_bits(img, out[0][0]) and cnt == out[0][1]
+
+
 @pytest.mark.parametrize("key", ["18", "cell", "16"])
 def test_shadow_queue_order_changes_nothing(key, monkeypatch):
     """The shadow queue's sort key (default: light | light-buffer cell | distance) only

@@ -12,7 +12,7 @@ cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 L = abi.lib()
 L.rt_debug_scan_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 s = DeviceScene(SceneDesc.synth_config(cfg))
-st = (C.c_ulonglong * 16)()
+st = (C.c_ulonglong * 32)()
 for depth in (1, 2, 8):
     L.rt_debug_scan_stats(st, 1)
     _, cnt, ms, _ = s.render(1920, 1080, depth)
@@ -27,6 +27,7 @@ for depth in (1, 2, 8):
               f"executed {v[b] / max(1, n):.2f}")
     print(f"  hit points: inside the Morton cube {v[11]}, outside {v[12]} (level 0: {v[13]} / {v[14]})")
     print(f"  shadow rays a hierarchy walk serves (no light buffer, undecided after the planes): {v[15]} "
-          f"of {cnt['shadow_rays']} ({v[15] / max(1, cnt['shadow_rays']):.3f})")
+          f"of {cnt['shadow_rays']} ({v[15] / max(1, cnt['shadow_rays']):.3f}); by D / R in (0,3] (3,6] (6,12] "
+          f"(12,25] (25,50] (50,inf): {v[16:22]}; light farther than 45: {v[22]}")
     print(f"  hit paths per wave scan: dsph {v[1] / max(1, v[0]):.2f} gsph {v[2] / max(1, v[0]):.2f} "
           f"tri {v[3] / max(1, v[0]):.2f} cube-tri {v[4] / max(1, v[0]):.2f}")
