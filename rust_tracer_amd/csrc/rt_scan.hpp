@@ -554,6 +554,26 @@ template <bool SHADOW, bool LDS, class C>
 __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, float tlim,
                                          float l2, C& c, lfloat4* lnodes, bool novote = false) {
     const BvhRay R = bvh_ray(S, o, d);
+#if RT_STATS
+    if (!SHADOW) {  // slots 23-28: trace walks' lanes by D / R in (0,3] (3,6] (6,12] (12,25] (25,50] (50,inf);
+                    // 29-31: leaf visits of waves whose farthest lane is within 3 R / 12 R / beyond
+        const float dx = o.x - S.bvh_cx, dy = o.y - S.bvh_cy, dz = o.z - S.bvh_cz;
+        const float q = (sqrtf(dx * dx + dy * dy + dz * dz) + S.bvh_r) / S.bvh_r;
+        const int b = q <= 3.f ? 0 : q <= 6.f ? 1 : q <= 12.f ? 2 : q <= 25.f ? 3 : q <= 50.f ? 4 : 5;
+        const bool first = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) ==
+                           (uint32_t)__builtin_ctzll(__ballot(1));
+        for (int k = 0; k < 6; k++) {
+            const uint64_t m = __ballot(b == k);
+            if (m && first) atomicAdd(&rt_scan_stats[23 + k], (unsigned long long)__builtin_popcountll(m));
+        }
+    }
+    uint32_t rt_far_class = 0;
+    if (!SHADOW) {
+        const float dx = o.x - S.bvh_cx, dy = o.y - S.bvh_cy, dz = o.z - S.bvh_cz;
+        const float q = (sqrtf(dx * dx + dy * dy + dz * dz) + S.bvh_r) / S.bvh_r;
+        rt_far_class = __ballot(q > 12.f) ? 2u : (__ballot(q > 3.f) ? 1u : 0u);
+    }
+#endif
     uint32_t* stk = rt_bvh_stack + ((threadIdx.x >> 6) << 5);
     uint32_t sp = 0;
     uint32_t cur = S.bvh_root;
@@ -582,6 +602,7 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
                     atomicAdd(&rt_scan_stats[sb], (unsigned long long)__builtin_popcountll(act));
                     atomicAdd(&rt_scan_stats[sb + 1], (unsigned long long)__builtin_popcountll(act & need));
                     atomicAdd(&rt_scan_stats[sb + 2], 1ull);
+                    if (!SHADOW) atomicAdd(&rt_scan_stats[29 + rt_far_class], 1ull);
                 }
             }
 #endif
@@ -723,8 +744,14 @@ __device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float&
         cfloat4* tp = cptr(S.graze_tri);
         if (S.graze_lane) {
             lfloat4* lpn = lnodes + 4 * S.n_bvh_nodes;
+            // the first two words requested together (one memory round trip where a scene has
+            // at most 64 grazing pairs, config 3: 50)
+            const uint32_t w0 = (RT_GRAZE_PRE || novote) ? 0u : mp[0];
+            const uint32_t w1 = (RT_GRAZE_PRE || novote || S.graze_words < 2) ? 0u : mp[1];
             for (uint32_t w = 0; w < S.graze_words; ++w) {
-                uint32_t own = novote ? 0u : ((RT_GRAZE_PRE && w == 0) ? pre.m0 : ((RT_GRAZE_PRE && w == 1) ? pre.m1 : mp[w]));
+                uint32_t own = novote ? 0u
+                                      : (w == 0 ? (RT_GRAZE_PRE ? pre.m0 : w0)
+                                                : (w == 1 ? (RT_GRAZE_PRE ? pre.m1 : w1) : mp[w]));
                 RT_OPS(c, graze);
                 uint32_t real = 0u;  // the pairs of word w this lane grazes
                 while (own) {        // divergent: as many rounds as the longest list

@@ -29,5 +29,7 @@ for depth in (1, 2, 8):
     print(f"  shadow rays a hierarchy walk serves (no light buffer, undecided after the planes): {v[15]} "
           f"of {cnt['shadow_rays']} ({v[15] / max(1, cnt['shadow_rays']):.3f}); by D / R in (0,3] (3,6] (6,12] "
           f"(12,25] (25,50] (50,inf): {v[16:22]}; light farther than 45: {v[22]}")
+    print(f"  trace walks' lanes by D / R (same buckets): {v[23:29]}; leaf visits of trace waves whose farthest "
+          f"lane is within 3 R / 12 R / beyond: {v[29:32]}")
     print(f"  hit paths per wave scan: dsph {v[1] / max(1, v[0]):.2f} gsph {v[2] / max(1, v[0]):.2f} "
           f"tri {v[3] / max(1, v[0]):.2f} cube-tri {v[4] / max(1, v[0]):.2f}")
