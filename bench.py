@@ -396,17 +396,17 @@ def main():
     # N = 8: 0.251 vs 0.270 for 3 x 11, N = 4: 0.487 vs 0.508)
     inflight = max(1, args.inflight or (3 if world >= 4 and -(-args.steps // 4) < 8 else 4))
     if args.sub_bands is None:
-        # Round 4 (config 3, K = 20, tools/subband_time.py, profiles/r4m/subband.txt): 4 slots x
-        # 5 whole frames 1.985 ms per frame, 2 groups x 2 shares x 10 frames 1.940, 1 group x 4
-        # shares 1.995; at K = 64 (16 frames per slot) 1.862 / 1.866 / 1.913 -- mixing more
-        # frames per pass pays only while passes are small
-        # At N = 2 too (rank 0's share on one MI355X, K = 20, profiles/r4l/subband.txt: 4 x 5
-        # 1.026, 3 x 7 1.019, 2 x 2 x 10 1.008, 1 x 4 x 20 0.997 ms per share-frame); from N = 4
-        # the 3 x 7 whole-share passes stay ahead (N = 4: 0.547 vs 0.556 / 0.567; N = 8: 0.309
-        # vs 0.330 / 0.370) -- a share of a share is too small a pass there
+        # Round 4 (config 3, tools/subband_time.py, profiles/r4m/subband.txt): at K = 20, 4 x 5
+        # whole frames 1.977 ms per frame, 2 groups x 2 shares x 10 frames 1.929, 1 group x 4
+        # shares x 20 frames 1.886.  With the light-buffer tiers and 50% trace grids
+        # (profiles/r4k64/): K = 64: 1 / 2 / 4 shares 1237 - 1253 / 1264 - 1269 / 1259 - 1263
+        # Mpixels/s; K = 40: 1220 - 1225 / 1245 / 1233 - 1236 -- the most shares whose group
+        # still takes its frames in one pass per slot.  At N = 2 too (rank 0's share on one
+        # MI355X, K = 20, profiles/r4l/subband.txt: 4 x 5 1.026, 3 x 7 1.019, 2 x 2 x 10 1.008,
+        # 1 x 4 x 20 0.997 ms per share-frame); from N = 4 the 3 x 7 whole-share passes stay
+        # ahead (N = 4: 0.547 vs 0.556 / 0.567; N = 8: 0.309 vs 0.330 / 0.370)
         sub = 1
-        if world <= 2 and args.spp == 1 and -(-args.steps // inflight) < 8:
-            # the most shares whose group still takes its frames in one pass per slot
+        if world <= 2 and args.spp == 1:
             from rust_tracer_amd import abi as _abi0
             mf = int(_abi0.lib().rt_max_frames())
             for cand in (4, 2):
