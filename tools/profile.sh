@@ -24,7 +24,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
 echo traces
 # a size N/S: passes of N frames over S band shares of the device (bench.py --sub-bands S; the
 # driver's K = 20 runs 20/4), one group of S slots
-for spec in ${SIZES:-1 5 16 20/4}; do
+for spec in ${SIZES:-1 5 16 20/4 32/2}; do
   n=${spec%/*}; s=1; [ "$spec" != "$n" ] && s=${spec#*/}
   args="--steps $n --warmup 0 --inflight $s --sub-bands $s --batch $n $B --count-frame 0"
   [ "$s" = 1 ] && suf=$n || suf=${n}s$s
