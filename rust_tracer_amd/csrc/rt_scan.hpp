@@ -1015,8 +1015,10 @@ __device__ __forceinline__ void lb_pass(const DevScene& S, uint32_t base, V3 o, 
         want = want && leaf != cur;
         RT_T0(C, t_l);
         const bool dec = shadow_decided(o, d, bt, l2);
-        // the farthest undecided origin from the light (+ rounding margin)
-        const float reach = wave_max(dec ? 0.f : sqrtf(l2) * 1.001f + 1e-4f);
+        // the farthest undecided origin from the light (+ rounding margin) among the lanes
+        // whose cell this is (the others test these records too, which changes nothing for
+        // them: their own cell's complete list is their pass)
+        const float reach = wave_max((dec || leaf != cur) ? 0.f : sqrtf(l2) * 1.001f + 1e-4f);
         lb_leaf(S, cur, o, d, on, dec ? -1.f : fminf(bt, tlim), reach, bt, bk, c);  // decided lanes do not vote
         RT_T1(C, c, cyc_leaf, t_l);
         want = want && !shadow_decided(o, d, bt, l2);

@@ -768,7 +768,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
 // a bit in the node record.
 
 #ifndef RT_SHADOW_WAVES
-#define RT_SHADOW_WAVES 6  // 80 VGPRs, 48 B scratch: +0.5 - 1% over 5 (96 VGPRs) at 20 frames in flight; 7 / 8: -2% / -4.5%
+#define RT_SHADOW_WAVES 5  // 96 VGPRs (round 4, light-buffer tiers: 5 / 6 / 8 waves 1236 / 1229 / 1196 Mpixels/s at K = 20, 3 runs each; round 3: 6 was +0.5 - 1% over 5)
 #endif
 template <bool LDS, bool COUNT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_WAVES, 8))) void shadow_kernel(WaveParams P) {
