@@ -563,7 +563,7 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
     if (!L.use || R <= 0 || R > 1024 || L.lb_prims.empty()) return;
     B.res = (uint32_t)R;
     // origins farther than D_max from the scene ball's centre (+ R) use the hierarchy walk
-    const double dmax = 3.0 * (double)L.r;
+    const double dmax = T.lb_dmax_k * (double)L.r;  // tier 0 (Tune::lb_dmax_k, default 3)
     B.dmax = down_f(dmax);
     // cell centres and angular radii (max angle to a corner, +1%)
     const int nc = 6 * R * R;
@@ -637,97 +637,97 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
         if (base >= (1u << 28)) continue;  // (the tier count sits in LightRec::lb_base's top bits)
         B.tiers = std::max(B.tiers, (uint32_t)tiers);
         for (int t = 0; t < tiers; t++) {
-        const double dm = dmax * (double)(1 << t);
-        struct Cone {
-            double u[3], alpha, ca, sa, near;
-            uint32_t code;
-        };
-        std::vector<Cone> cones;
-        for (const LbPrim& p : L.lb_prims) {
-            double w[3] = {p.c[0] - lp[0], p.c[1] - lp[1], p.c[2] - lp[2]};
-            const double dist = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-            const double rr = grown(p, dm);
-            Cone c;
-            for (int k = 0; k < 3; k++) c.u[k] = w[k] / dist;
-            c.alpha = std::asin(std::min(1.0, rr / dist)) + LB_MU * (double)(1 << t);
-            c.ca = std::cos(c.alpha);
-            c.sa = std::sin(c.alpha);
-            c.near = dist - rr;
-            c.code = p.code;
-            cones.push_back(c);
-        }
-        // nearest first: every cell's list comes out sorted by distance from the light
-        std::stable_sort(cones.begin(), cones.end(), [](const Cone& a, const Cone& b) { return a.near < b.near; });
-        std::vector<std::vector<std::pair<uint32_t, double>>> lists(nc);  // (code, nearest distance)
-        for (const Cone& c : cones) {
-            for (int f = 0; f < 6; f++) {
-                const int k = f >> 1;
-                const double s = (f & 1) ? -1.0 : 1.0;
-                const double ax_ang = std::acos(std::max(-1.0, std::min(1.0, s * c.u[k])));
-                if (ax_ang > c.alpha + FACE_HALF + 1e-3) continue;
-                for (int cc = f * R * R; cc < (f + 1) * R * R; cc++) {
-                    bool in = c.alpha + crad[cc] >= PI;
-                    if (!in) {
-                        // angle(u, cell centre) <= alpha + cell radius  <=>  dot >= cos(alpha + rad)
-                        const double dt =
-                            c.u[0] * cdir[3 * cc] + c.u[1] * cdir[3 * cc + 1] + c.u[2] * cdir[3 * cc + 2];
-                        in = dt >= c.ca * ccos[cc] - c.sa * csin[cc] - 1e-12;
-                    }
-                    if (in) {
-                        auto& l = lists[cc];
-                        bool dup = false;  // a sphere / triangle pair's partner: keep the first entry
-                        for (const auto& q : l) dup = dup || q.first == c.code;
-                        if (!dup) l.push_back(std::make_pair(c.code, c.near));
+            const double dm = dmax * (double)(1 << t);
+            struct Cone {
+                double u[3], alpha, ca, sa, near;
+                uint32_t code;
+            };
+            std::vector<Cone> cones;
+            for (const LbPrim& p : L.lb_prims) {
+                double w[3] = {p.c[0] - lp[0], p.c[1] - lp[1], p.c[2] - lp[2]};
+                const double dist = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+                const double rr = grown(p, dm);
+                Cone c;
+                for (int k = 0; k < 3; k++) c.u[k] = w[k] / dist;
+                c.alpha = std::asin(std::min(1.0, rr / dist)) + LB_MU * (double)(1 << t);
+                c.ca = std::cos(c.alpha);
+                c.sa = std::sin(c.alpha);
+                c.near = dist - rr;
+                c.code = p.code;
+                cones.push_back(c);
+            }
+            // nearest first: every cell's list comes out sorted by distance from the light
+            std::stable_sort(cones.begin(), cones.end(), [](const Cone& a, const Cone& b) { return a.near < b.near; });
+            std::vector<std::vector<std::pair<uint32_t, double>>> lists(nc);  // (code, nearest distance)
+            for (const Cone& c : cones) {
+                for (int f = 0; f < 6; f++) {
+                    const int k = f >> 1;
+                    const double s = (f & 1) ? -1.0 : 1.0;
+                    const double ax_ang = std::acos(std::max(-1.0, std::min(1.0, s * c.u[k])));
+                    if (ax_ang > c.alpha + FACE_HALF + 1e-3) continue;
+                    for (int cc = f * R * R; cc < (f + 1) * R * R; cc++) {
+                        bool in = c.alpha + crad[cc] >= PI;
+                        if (!in) {
+                            // angle(u, cell centre) <= alpha + cell radius  <=>  dot >= cos(alpha + rad)
+                            const double dt =
+                                c.u[0] * cdir[3 * cc] + c.u[1] * cdir[3 * cc + 1] + c.u[2] * cdir[3 * cc + 2];
+                            in = dt >= c.ca * ccos[cc] - c.sa * csin[cc] - 1e-12;
+                        }
+                        if (in) {
+                            auto& l = lists[cc];
+                            bool dup = false;  // a sphere / triangle pair's partner: keep the first entry
+                            for (const auto& q : l) dup = dup || q.first == c.code;
+                            if (!dup) l.push_back(std::make_pair(c.code, c.near));
+                        }
                     }
                 }
             }
+            for (int cc = 0; cc < nc; cc++) {
+                // per type, nearest first; each copy carries its nearest distance to the light
+                // (down-rounded) in the record's spare slot: the device stops a run at the first
+                // record no undecided lane can reach
+                std::vector<uint32_t> by[4];
+                std::vector<float> nr[4];
+                for (const auto& q : lists[cc]) {
+                    by[q.first >> 30].push_back(q.first & 0x3FFFFFFFu);
+                    nr[q.first >> 30].push_back(reach_cut ? down_f(q.second) : 0.f);
+                }
+                uint32_t rec[8];
+                rec[0] = (uint32_t)(L.dsph.size() / 16);
+                for (size_t q = 0; q < by[LB_DSPH].size(); q++) {
+                    const uint32_t r = by[LB_DSPH][q];
+                    std::vector<float> t(L.dsph.begin() + 16 * (size_t)r, L.dsph.begin() + 16 * (size_t)r + 16);
+                    t[15] = nr[LB_DSPH][q];
+                    L.dsph.insert(L.dsph.end(), t.begin(), t.end());
+                }
+                rec[1] = (uint32_t)(L.dsph.size() / 16);
+                rec[2] = (uint32_t)(L.gsph.size() / 16);
+                for (size_t q = 0; q < by[LB_GSPH].size(); q++) {
+                    const uint32_t r = by[LB_GSPH][q];
+                    std::vector<float> t(L.gsph.begin() + 16 * (size_t)r, L.gsph.begin() + 16 * (size_t)r + 16);
+                    t[15] = nr[LB_GSPH][q];
+                    L.gsph.insert(L.gsph.end(), t.begin(), t.end());
+                }
+                rec[3] = (uint32_t)(L.gsph.size() / 16);
+                rec[4] = (uint32_t)(L.tri.size() / 24);
+                for (size_t q = 0; q < by[LB_TRI].size(); q++) {
+                    const uint32_t r = by[LB_TRI][q];
+                    std::vector<float> t(L.tri.begin() + 24 * (size_t)r, L.tri.begin() + 24 * (size_t)r + 24);
+                    t[20] = nr[LB_TRI][q];
+                    L.tri.insert(L.tri.end(), t.begin(), t.end());
+                }
+                rec[5] = (uint32_t)(L.tri.size() / 24);
+                rec[6] = (uint32_t)(L.cube.size() / 16);
+                for (size_t q = 0; q < by[LB_CUBE].size(); q++) {
+                    const uint32_t r = by[LB_CUBE][q];
+                    std::vector<float> t(L.cube.begin() + 16 * (size_t)r, L.cube.begin() + 16 * (size_t)r + 16);
+                    t[15] = nr[LB_CUBE][q];
+                    L.cube.insert(L.cube.end(), t.begin(), t.end());
+                }
+                rec[7] = (uint32_t)(L.cube.size() / 16);
+                L.leaves.insert(L.leaves.end(), rec, rec + 8);
+            }
         }
-        for (int cc = 0; cc < nc; cc++) {
-            // per type, nearest first; each copy carries its nearest distance to the light
-            // (down-rounded) in the record's spare slot: the device stops a run at the first
-            // record no undecided lane can reach
-            std::vector<uint32_t> by[4];
-            std::vector<float> nr[4];
-            for (const auto& q : lists[cc]) {
-                by[q.first >> 30].push_back(q.first & 0x3FFFFFFFu);
-                nr[q.first >> 30].push_back(reach_cut ? down_f(q.second) : 0.f);
-            }
-            uint32_t rec[8];
-            rec[0] = (uint32_t)(L.dsph.size() / 16);
-            for (size_t q = 0; q < by[LB_DSPH].size(); q++) {
-                const uint32_t r = by[LB_DSPH][q];
-                std::vector<float> t(L.dsph.begin() + 16 * (size_t)r, L.dsph.begin() + 16 * (size_t)r + 16);
-                t[15] = nr[LB_DSPH][q];
-                L.dsph.insert(L.dsph.end(), t.begin(), t.end());
-            }
-            rec[1] = (uint32_t)(L.dsph.size() / 16);
-            rec[2] = (uint32_t)(L.gsph.size() / 16);
-            for (size_t q = 0; q < by[LB_GSPH].size(); q++) {
-                const uint32_t r = by[LB_GSPH][q];
-                std::vector<float> t(L.gsph.begin() + 16 * (size_t)r, L.gsph.begin() + 16 * (size_t)r + 16);
-                t[15] = nr[LB_GSPH][q];
-                L.gsph.insert(L.gsph.end(), t.begin(), t.end());
-            }
-            rec[3] = (uint32_t)(L.gsph.size() / 16);
-            rec[4] = (uint32_t)(L.tri.size() / 24);
-            for (size_t q = 0; q < by[LB_TRI].size(); q++) {
-                const uint32_t r = by[LB_TRI][q];
-                std::vector<float> t(L.tri.begin() + 24 * (size_t)r, L.tri.begin() + 24 * (size_t)r + 24);
-                t[20] = nr[LB_TRI][q];
-                L.tri.insert(L.tri.end(), t.begin(), t.end());
-            }
-            rec[5] = (uint32_t)(L.tri.size() / 24);
-            rec[6] = (uint32_t)(L.cube.size() / 16);
-            for (size_t q = 0; q < by[LB_CUBE].size(); q++) {
-                const uint32_t r = by[LB_CUBE][q];
-                std::vector<float> t(L.cube.begin() + 16 * (size_t)r, L.cube.begin() + 16 * (size_t)r + 16);
-                t[15] = nr[LB_CUBE][q];
-                L.cube.insert(L.cube.end(), t.begin(), t.end());
-            }
-            rec[7] = (uint32_t)(L.cube.size() / 16);
-            L.leaves.insert(L.leaves.end(), rec, rec + 8);
-        }
-        }  // tiers
         B.base[li] = base | ((uint32_t)tiers << 28);
     }
 }

@@ -22,6 +22,7 @@ struct Tune {
     int graze_lane = 1;       // per-lane grazing sets (0: the wave-union path)
     int lb_res = 48;          // light-buffer cells per face side (0: no light buffers)
     int lb_reach = 1;         // light-buffer runs cut at the undecided lanes' reach
+    double lb_dmax_k = 3.0;   // light-buffer tier 0 serves origins with D <= lb_dmax_k R
     int lb_tiers = 4;         // light-buffer tiers (at most, per light): tier t serves origins with D <= 3 R 2^t
                               // (1 until round 4; K = 20: 1 / 3 / 4 / 5 tiers 1097 / 1200 / 1212 / 1212)
     int shape_buf = 1;        // shape buffers for rays inside spheres

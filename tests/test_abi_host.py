@@ -167,10 +167,10 @@ def test_tuning_strings_are_validated_on_the_host():
         L.rt_scene_destroy(h)
         pytest.skip("a HIP device is present: the valid strings would create scenes")
     for bad in (b"bogus=1", b"lb_res", b"lb_res=x", b"task_w=48", b"sort=maybe", b"seam_split=0",
-                b"shadow_key=17", b"=3", b"lb_tiers=0", b"lb_tiers=8"):
+                b"shadow_key=17", b"=3", b"lb_tiers=0", b"lb_tiers=8", b"lb_dmax_k=0.5"):
         assert L.rt_scene_create_tuned(desc.ptr(), 0, bad, C.byref(h)) == abi.RT_ERR_INVALID_ARG, bad
     for good in (b"", b"lb_res=0,bvh=0", b"task_w=32 task_fill=2.5", b"sort=shadow,dup=shc",
                  b"shadow_key=cell,frame_keys=frame,spp_keys=mix", b"lds_nodes=trace,seam_adapt=device",
                  b"force_rccl=1,node_cap=4096", b"graze_k=3e-3,bvh_cnode=200,bvh_maxleaf=16",
-                 b"lb_tiers=1", b"lb_tiers=7,lb_res=32"):
+                 b"lb_tiers=1", b"lb_tiers=7,lb_res=32", b"lb_dmax_k=2.01"):
         assert L.rt_scene_create_tuned(desc.ptr(), 0, good, C.byref(h)) == abi.RT_ERR_NO_DEVICE, good
