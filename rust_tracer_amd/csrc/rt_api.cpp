@@ -607,7 +607,11 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
     };
     // per light: the most tiers (<= Tune::lb_tiers) whose grown balls all keep LB_RHO from it
     const int max_tiers = std::max(1, std::min(7, T.lb_tiers));
+    // Tune::lb_near_all: tier 0 as before, and every further tier: a record whose grown ball
+    // comes within LB_RHO of the light goes into every cell of that tier (a hit on it may lie
+    // in any direction from the light); the others keep the direction bound with rho = LB_RHO
     auto tiers_of = [&](const double lp[3]) {
+        if (T.lb_near_all) return light_ok(lp, dmax) ? max_tiers : 0;
         int n = 0;
         while (n < max_tiers && light_ok(lp, dmax * (double)(1 << n))) n++;
         return n;
@@ -648,11 +652,15 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
                 const double dist = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
                 const double rr = grown(p, dm);
                 Cone c;
-                for (int k = 0; k < 3; k++) c.u[k] = w[k] / dist;
-                c.alpha = std::asin(std::min(1.0, rr / dist)) + LB_MU * (double)(1 << t);
+                for (int k = 0; k < 3; k++) c.u[k] = dist > 0 ? w[k] / dist : (k == 0 ? 1.0 : 0.0);
+                if (dist - rr >= LB_RHO) {
+                    c.alpha = std::asin(std::min(1.0, rr / dist)) + LB_MU * (double)(1 << t);
+                } else {  // (lb_near_all tiers only) within LB_RHO of the light: every cell
+                    c.alpha = PI;
+                }
                 c.ca = std::cos(c.alpha);
                 c.sa = std::sin(c.alpha);
-                c.near = dist - rr;
+                c.near = std::max(0.0, dist - rr);
                 c.code = p.code;
                 cones.push_back(c);
             }

@@ -23,8 +23,10 @@ struct Tune {
     int lb_res = 48;          // light-buffer cells per face side (0: no light buffers)
     int lb_reach = 1;         // light-buffer runs cut at the undecided lanes' reach
     double lb_dmax_k = 3.0;   // light-buffer tier 0 serves origins with D <= lb_dmax_k R
-    int lb_tiers = 4;         // light-buffer tiers (at most, per light): tier t serves origins with D <= 3 R 2^t
-                              // (1 until round 4; K = 20: 1 / 3 / 4 / 5 tiers 1097 / 1200 / 1212 / 1212)
+    int lb_near_all = 1;      // light-buffer tiers past the first: records near the light in every cell (no tier limit)
+    int lb_tiers = 5;         // light-buffer tiers (at most, per light): tier t serves origins with D <= 3 R 2^t
+                              // (1 until round 4; K = 20: 1 / 3 / 4 / 5 tiers 1097 / 1200 / 1212 / 1212 without
+                              // lb_near_all; with it 4 / 5 / 6 tiers 1245 / 1258 / 1250 vs 1240)
     int shape_buf = 1;        // shape buffers for rays inside spheres
     int bvh_tris = 1;         // loose triangles in the hierarchy (0: linear)
     int dark_skip = 1;        // shadowed lights skipped in the combine where exact

@@ -163,8 +163,9 @@ def test_shape_buffers_change_nothing(case, monkeypatch):
 def test_light_buffer_tiers_change_nothing(case):
     """Light-buffer tiers (rt_api.cpp build_light_buffers: tier t serves shadow-ray origins
     with D <= 3 R 2^t and a light within 45 * 2^t, its records' balls grown by their bound at
-    that reach): frames and counters identical with one tier, the default, seven, and no
-    light buffers at all (every shadow ray walks the hierarchy)."""
+    that reach): frames and counters identical with one tier, the default, seven, no light
+    buffers at all (every shadow ray walks the hierarchy), and six tiers for every light with
+    the records near the light in every cell of a tier (lb_near_all)."""
     if case is None:
         desc, w, h, depth, cam = SceneDesc.synth_config(3), 480, 270, 8, None
     else:
@@ -172,7 +173,7 @@ def test_light_buffer_tiers_change_nothing(case):
         desc, w, h, depth = stress_scene(seed, scale, near, slivers), 160, 120, 8
         cam = stress_camera(w, h, scale, cam_mode)
     out = []
-    for tune in (None, "lb_tiers=1", "lb_tiers=7", "lb_res=0"):
+    for tune in (None, "lb_tiers=1", "lb_tiers=7", "lb_res=0", "lb_near_all=1,lb_tiers=6"):
         s = DeviceScene(desc, device=0, tuning=tune)
         out.append(s.render(w, h, depth, cam=cam)[:2])
         s.close()
