@@ -75,8 +75,10 @@ def parse():
     p.add_argument("--sub-bands", type=int, default=None,
                    help="N = 1: slots as groups of S band shares of one device, each rendering its rows of "
                         "every frame of its group's passes in place (rt_render_bands_direct_async): S times "
-                        "the frames per pass at the same rays in flight.  Default: 2 when the timed frames give "
-                        "each slot fewer than 8 (K = 20: 2 groups x 10 frames, each pass half the rows), else 1")
+                        "the frames per pass at the same rays in flight.  Default (N <= 2, spp 1): the largest S "
+                        "of 4, 2 that divides the slots and whose groups still take the timed frames in one pass "
+                        "each (ceil(K / (F / S)) <= rt_max_frames()): K = 20 gives 1 group x 4 shares x 20 "
+                        "frames, K = 64 2 groups x 2 shares x 32 frames; otherwise 1")
     p.add_argument("--inflight", type=int, default=None,
                    help="frames in flight (F scene handles / HIP streams; default 4 = the box's hardware "
                         "queues per process, 3 from 4 ranks up); 1 = one at a time")
@@ -223,6 +225,8 @@ def seam_stats(args, scene, pipe, tiler, dev):
     - one frame at a time: the pipeline with nothing overlapping it (HIP events);
     - rt_render: the reference's render() seam (src/render.rs:31) with its device-to-host
       copy of the float frame, wall clock per call (main.rs:250-253 times render only);
+    - the drop-in render() (the C++ mirror of render.rs:31) called repeatedly on one Scene:
+      the first call builds the device scene, later ones reuse it (render_call_ms);
     - the scene build: rt_scene_create (host hierarchy, light buffers, grazing masks, upload)
       and rt_scene_clone (a second handle, device-to-device);
     - 'primary+8 bounces' read literally: depth 9 (reference depth 8 = primary + 7 levels,
@@ -289,6 +293,23 @@ def seam_stats(args, scene, pipe, tiler, dev):
             walls.append((time.perf_counter() - t0) * 1e3)
         hf.close()
         out["rt_render_pinned_host_copy_ms"] = round(min(walls), 3)
+        # the drop-in render() itself (render.rs:31-38): the C++ host mirror's
+        # render(camera, scene, buffer, depth) called again and again on ONE Scene -- the
+        # reference's bench loop (main.rs:137-140, render_scene_basic :244-261).  The first call
+        # builds the device scene; later calls find it unchanged (rt_scene_update) and cost a
+        # frame: flatten + compare, rt_render, the frame into the RenderBuffer (pageable)
+        if args.config in (2, 3, 4):
+            try:  # an untimed extra
+                from rust_tracer_amd import mirror_render_calls
+                ms, up, _, _ = mirror_render_calls(args.config, args.width, args.height, args.depth, 7,
+                                                   device=dev.index)
+                later = sorted(ms[1:])
+                out["render_call_first_ms"] = round(ms[0], 3)
+                out["render_call_ms"] = round(later[len(later) // 2], 3)  # median of calls 2..7
+                out["render_call_min_ms"] = round(later[0], 3)
+                out["render_call_updates"] = up
+            except Exception as e:  # noqa: BLE001
+                out["render_call_error"] = repr(e)[:200]
     t0 = time.perf_counter()
     c = scene.clone(dev.index)
     out["scene_clone_ms"] = round((time.perf_counter() - t0) * 1e3, 2)

@@ -166,6 +166,12 @@ rt_status rt_scene_create_tuned(const rt_scene_desc* desc, int32_t device, const
  * scene-build keys are RT_ERR_INVALID_ARG here.  Not while a render of the handle runs. */
 rt_status rt_scene_set_tuning(rt_scene* scene, const char* tuning);
 rt_status rt_scene_destroy(rt_scene* scene);
+/* The host half of rt_scene_create alone (no HIP call, no device needed): builds the image
+ * the scene's device allocation would hold for `desc` under `tuning` and returns its FNV-1a
+ * digest and size in bytes.  A check that the scene build is deterministic (e.g. the same
+ * image for any build_threads), and a way to time the build on a machine without a GPU. */
+rt_status rt_scene_layout_digest(const rt_scene_desc* desc, const char* tuning, uint64_t* digest,
+                                 uint64_t* bytes);
 
 /* Page-locked host memory for a caller's frame buffer (the RenderBuffer a render() caller
  * owns, render.rs:5-19): rt_render's device-to-host copy of the frame then runs at the
@@ -267,7 +273,16 @@ rt_status rt_render_bands_batch_async(const rt_scene* scene, const rt_camera* ca
  *            pixel, written by the render's last pass (no separate quantise launch) -- 3 B per
  *            pixel for the multi-GPU gather instead of 12.
  * A queue overflow cannot be returned by a stream-ordered call: it is latched in the scene
- * and reported by rt_scene_sync_status. */
+ * and reported by rt_scene_sync_status.
+ * HOST WAIT (every *_async render, rt_render_frame_async and the multi-device shares): a pass
+ * with more level-0 items (pixels x frames x samples of this rank) or a greater depth than any
+ * pass this handle has completed is checked before the call returns -- the call waits for
+ * `stream` and the handle's other streams, and if a ray queue overflowed it grows the node
+ * pool and renders the pass again (up to 8 times).  Passes no larger than a checked one are
+ * enqueued without any host wait.  So the first pass of a new size blocks; render one such
+ * pass before capturing a stream into a graph: while `stream` is being captured, a pass that
+ * would need the check returns RT_ERR_UNSUPPORTED and enqueues nothing.  Tuning key
+ * node_cap pins the pool and skips the check (an overflow is then only latched). */
 rt_status rt_render_bands_ex_async(const rt_scene* scene, const rt_camera* cams, uint32_t n_frames, uint32_t depth,
                                    uint32_t spp, uint32_t seed, uint32_t band_rows, uint32_t rank, uint32_t world,
                                    float* d_rgb, uint8_t* d_rgb8, uint64_t* d_counters, void* stream);
@@ -410,6 +425,22 @@ rt_status rt_forest_counters(const rt_forest* forest, rt_counters* out);
 /* Replace material `index`'s parameters (same kind) -- the GUI's material edits
  * (gui.rs:221-236).  Affects later renders and forest shades. */
 rt_status rt_scene_set_material(rt_scene* scene, uint32_t index, const rt_material* material);
+
+/* Brings a handle up to date with `desc` -- the caller's Scene as it is now -- so that a
+ * render() binding can keep ONE handle across calls (render.rs:31 takes the same &Scene every
+ * frame: main.rs:137-140, 244-261) instead of rebuilding the device scene per call:
+ *  - `desc` equal to the description the handle renders (byte for byte): nothing; *what = 0;
+ *  - only materials differ, each keeping its kind: rt_scene_set_material per edited index
+ *    (no rebuild); *what = 1;
+ *  - anything else (a shape added or transformed, a light, the ambient, a material's kind or
+ *    count): the scene is rebuilt with the handle's device and tuning and adopted in place --
+ *    the handle, its stream, workspace, band shares and devices stay valid; *what = 2.
+ * Renders on the handle must not run concurrently with it; it waits for the handle's streams.
+ * A stream-ordered render's unreported status (rt_scene_sync_status) is returned first and
+ * the update is then not made.  Forests created before a rebuild describe the old scene.
+ * `what` may be NULL.  Errors of the rebuild (e.g. RT_ERR_SINGULAR_MATRIX) leave the handle
+ * rendering its previous scene. */
+rt_status rt_scene_update(rt_scene* scene, const rt_scene_desc* desc, int32_t* what);
 
 const char* rt_status_str(rt_status status);
 int32_t rt_api_version(void);

@@ -40,6 +40,21 @@ rt_status rt_synth_config(int32_t config, rt_synth_params* out);
 
 void rt_desc_free(rt_scene_desc* desc);
 
+/* The C++ host mirror's render() (csrc/host/scene.hpp; render.rs:31-38) called n_calls times
+ * on ONE Scene into one RenderBuffer -- the reference's bench loop (main.rs:137-140,
+ * render_scene_basic main.rs:244-261) through the drop-in seam, whose Scene keeps its device
+ * scene across calls.  scene: 0 = my_scene.rs, 2 .. 5 = rt_synth_config(scene).  edit,
+ * applied before the last call (n_calls >= 2): 0 none; 1 set_transform of the first sphere
+ * (find_shape_mut, translated 0.1 in x); 2 the first shape's material's reflectivity + 0.05
+ * (an Rc<RefCell<Material>> edit); 3 a point light added.  Out: ms[i] = wall time of call i
+ * (the frame's device-to-host copy included), updates[i] = what render() did to the device
+ * scene (-1 created, 0 reused, 1 materials edited in place, 2 rebuilt); rgb (optional,
+ * x_res * y_res * 3 floats) = the last call's frame; rgb_fresh (optional) = the same edited
+ * Scene rendered by a newly created handle, for comparison.  Test and bench harness. */
+rt_status rt_mirror_render_calls(int32_t scene, uint32_t x_res, uint32_t y_res, uint32_t depth, uint32_t n_calls,
+                                 int32_t edit, int32_t device, float* ms, int32_t* updates, float* rgb,
+                                 float* rgb_fresh);
+
 #ifdef __cplusplus
 }
 #endif

@@ -374,6 +374,17 @@ class DeviceScene:
         """rt_scene_set_material: replace material `index` (same kind), e.g. the GUI's edits."""
         check(self._L.rt_scene_set_material(self.h, index, C.byref(material)), "rt_scene_set_material")
 
+    UPDATE_KINDS = {0: "unchanged", 1: "materials", 2: "rebuilt"}
+
+    def update(self, desc):
+        """rt_scene_update: bring this handle up to date with `desc` (the caller's scene after
+        edits) -- nothing when unchanged, material edits in place, else a rebuild adopted by
+        this handle.  Returns "unchanged" / "materials" / "rebuilt"."""
+        what = C.c_int32(0)
+        check(self._L.rt_scene_update(self.h, desc.ptr(), C.byref(what)), "rt_scene_update")
+        self.desc = desc
+        return self.UPDATE_KINDS[what.value]
+
     def forest(self, x_res, y_res, depth):
         """generate_ray_forest (render_tree.rs:147-164) on the device."""
         return DeviceForest(self, x_res, y_res, depth)
@@ -563,3 +574,21 @@ def render(x_res, y_res, desc, depth, device=-1, want_u8=False):
         return s.render(x_res, y_res, depth, want_u8=want_u8, device=device)
     finally:
         s.close()
+
+
+def mirror_render_calls(scene, x_res, y_res, depth, n_calls, edit=0, device=-1, fresh=False):
+    """rt_mirror_render_calls (include/rt_scenes.h): the C++ mirror's render() called n_calls
+    times on one Scene (the reference's bench loop through the drop-in seam).  scene: 0 =
+    my_scene, 2..5 = BASELINE configs; edit before the last call: 0 none, 1 set_transform,
+    2 material, 3 light.  Returns (ms per call, update kinds per call, last frame, the frame of a
+    fresh handle of the edited scene or None)."""
+    L = lib()
+    ms = (C.c_float * n_calls)()
+    up = (C.c_int32 * n_calls)()
+    rgb = np.zeros((y_res, x_res, 3), np.float32)
+    ref = np.zeros((y_res, x_res, 3), np.float32) if fresh else None
+    fp = C.POINTER(C.c_float)
+    check(L.rt_mirror_render_calls(scene, x_res, y_res, depth, n_calls, edit, device, ms, up,
+                                   rgb.ctypes.data_as(fp), ref.ctypes.data_as(fp) if fresh else None),
+          "rt_mirror_render_calls")
+    return list(ms), list(up), rgb, ref

@@ -120,6 +120,7 @@ def lib():
     L.rt_scene_create.argtypes = [P(rt_scene_desc), C.c_int32, P(vp)]
     L.rt_scene_create_tuned.argtypes = [P(rt_scene_desc), C.c_int32, C.c_char_p, P(vp)]
     L.rt_scene_set_tuning.argtypes = [vp, C.c_char_p]
+    L.rt_scene_layout_digest.argtypes = [P(rt_scene_desc), C.c_char_p, P(C.c_uint64), P(C.c_uint64)]
     L.rt_scene_destroy.argtypes = [vp]
     L.rt_render.argtypes = [vp, P(rt_camera), C.c_uint32, P(rt_render_opts),
                             P(C.c_float), P(C.c_uint8)]
@@ -170,6 +171,7 @@ def lib():
     L.rt_forest_trees_with.argtypes = [vp, C.c_int32, P(C.c_uint64)]
     L.rt_forest_counters.argtypes = [vp, P(rt_counters)]
     L.rt_scene_set_material.argtypes = [vp, C.c_uint32, P(rt_material)]
+    L.rt_scene_update.argtypes = [vp, P(rt_scene_desc), P(C.c_int32)]
     L.rt_write_image.argtypes = [C.c_char_p, P(C.c_uint8), C.c_uint32, C.c_uint32]
     L.rt_scene_uses_bvh.argtypes = [vp]
     L.rt_scene_uses_bvh.restype = C.c_int32
@@ -183,6 +185,8 @@ def lib():
     L.rt_desc_synth.argtypes = [P(rt_synth_params), P(P(rt_scene_desc))]
     L.rt_desc_free.argtypes = [P(rt_scene_desc)]
     L.rt_synth_config.argtypes = [C.c_int32, P(rt_synth_params)]
+    L.rt_mirror_render_calls.argtypes = [C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int32,
+                                         C.c_int32, P(C.c_float), P(C.c_int32), P(C.c_float), P(C.c_float)]
     _lib = L
     return L
 

@@ -128,10 +128,15 @@ int main(int argc, char** argv) {
     }
     std::printf("Done Creating Scene\n");
 
-    auto flat = scene.flatten();
+    // a handle of its own for the forest and supersampling paths; the basic path renders
+    // through render(), whose Scene keeps its device scene
     rt_scene* s = nullptr;
-    rt_status st = rt_scene_create(&flat->desc, device, &s);
-    if (st != RT_OK) return fail("rt_scene_create", st);
+    rt_status st = RT_OK;
+    if (forest_method || spp != 1) {
+        auto flat = scene.flatten();
+        st = rt_scene_create(&flat->desc, device, &s);
+        if (st != RT_OK) return fail("rt_scene_create", st);
+    }
     Camera cam(w, h);
     rt_camera c = cam.to_c();
     std::vector<float> rgb((size_t)w * h * 3);
@@ -147,12 +152,24 @@ int main(int argc, char** argv) {
         float kms = 0.f;
         rt_render_opts opts{device, &cnt, &kms};
         int n = bench ? runs : 1;
+        RenderBuffer buffer(w, h);
         auto t0 = Clock::now();
         for (int k = 0; k < n; k++) {
             auto r0 = Clock::now();
-            st = rt_render_spp(s, &c, depth, spp, seed, &opts, rgb.data(), rgb8.data());
-            if (st != RT_OK) return fail("rt_render_spp", st);
+            if (spp == 1) {
+                // render_scene_basic (main.rs:244-261): render() on the same Scene every call;
+                // the Scene keeps its device scene (the first call builds it)
+                st = render(cam, scene, buffer, depth, device, &cnt, &kms);
+                if (st != RT_OK) return fail("render", st);
+            } else {
+                st = rt_render_spp(s, &c, depth, spp, seed, &opts, rgb.data(), rgb8.data());
+                if (st != RT_OK) return fail("rt_render_spp", st);
+            }
             std::printf("render_scene: %lldms\n", ms_since(r0));  // main.rs:250-253
+        }
+        if (spp == 1) {
+            std::memcpy(rgb.data(), buffer.buf.data(), rgb.size() * sizeof(float));
+            as_u8(rgb, rgb8);  // bmp.rs:8-19
         }
         long long ns = (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
         if (bench) {
@@ -250,6 +267,6 @@ int main(int argc, char** argv) {
         }
         if (!out.empty()) std::printf("wrote %s\n", out.c_str());
     }
-    rt_scene_destroy(s);
+    if (s) rt_scene_destroy(s);
     return 0;
 }

@@ -2,6 +2,7 @@
 // builders exported through include/rt_scenes.h.
 #include "scene.hpp"
 
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -152,6 +153,36 @@ Light AmbientLight(const Color& color) {
     return l;
 }
 
+struct Scene::DeviceCache {
+    std::mutex m;
+    rt_scene* handle = nullptr;
+    int32_t device = -1;
+    ~DeviceCache() {
+        if (handle) rt_scene_destroy(handle);
+    }
+};
+
+Scene::Scene() : cache_(new DeviceCache()) {}
+Scene::~Scene() = default;
+Scene::Scene(const Scene& o)
+    : ambient_(o.ambient_), shapes_(o.shapes_), lights_(o.lights_), cache_(new DeviceCache()) {}
+Scene& Scene::operator=(const Scene& o) {
+    if (this != &o) {
+        ambient_ = o.ambient_;
+        shapes_ = o.shapes_;
+        lights_ = o.lights_;  // the device handle stays; the next render() updates it
+    }
+    return *this;
+}
+Scene::Scene(Scene&&) noexcept = default;
+Scene& Scene::operator=(Scene&&) noexcept = default;
+
+Shape* Scene::find_shape_mut(const std::string& name) {
+    for (auto& s : shapes_)
+        if (s.name == name) return &s;
+    return nullptr;
+}
+
 void Scene::add_shape(Shape s) {
     s.id = (int32_t)shapes_.size();
     shapes_.push_back(std::move(s));
@@ -227,21 +258,37 @@ rt_camera Camera::to_c() const {
 }
 
 rt_status render(const Camera& camera, const Scene& scene, RenderBuffer& buffer, uint32_t depth,
-                 int32_t device, rt_counters* counters, float* kernel_ms) {
+                 int32_t device, rt_counters* counters, float* kernel_ms, int32_t* update) {
     if (buffer.w != camera.x_res || buffer.h != camera.y_res) return RT_ERR_INVALID_ARG;
     auto flat = scene.flatten();
-    rt_scene* s = nullptr;
-    rt_status st = rt_scene_create(&flat->desc, device, &s);
-    if (st != RT_OK) return st;
+    Scene::DeviceCache& c = scene.device_cache();
+    std::lock_guard<std::mutex> lock(c.m);  // one render of a Scene at a time (the handle is !Sync)
+    if (c.handle && c.device != device) {
+        rt_scene_destroy(c.handle);
+        c.handle = nullptr;
+    }
+    rt_status st = RT_OK;
+    if (!c.handle) {
+        st = rt_scene_create(&flat->desc, device, &c.handle);
+        if (st != RT_OK) {
+            c.handle = nullptr;
+            return st;
+        }
+        c.device = device;
+        if (update) *update = -1;
+    } else {
+        int32_t what = 0;
+        st = rt_scene_update(c.handle, &flat->desc, &what);
+        if (st != RT_OK) return st;
+        if (update) *update = what;
+    }
     rt_camera cam = camera.to_c();
     rt_render_opts opts;
     opts.device = device;
     opts.counters = counters;
     opts.kernel_ms = kernel_ms;
     static_assert(sizeof(Color) == 3 * sizeof(float), "Color must be 3 packed floats");
-    st = rt_render(s, &cam, depth, &opts, reinterpret_cast<float*>(buffer.buf.data()), nullptr);
-    rt_scene_destroy(s);
-    return st;
+    return rt_render(c.handle, &cam, depth, &opts, reinterpret_cast<float*>(buffer.buf.data()), nullptr);
 }
 
 // ---------------------------------------------------------------- scenes
@@ -434,6 +481,54 @@ rt_status rt_synth_config(int32_t config, rt_synth_params* out) {
         return RT_OK;
     }
     return RT_ERR_INVALID_ARG;
+}
+
+rt_status rt_mirror_render_calls(int32_t scene_id, uint32_t x_res, uint32_t y_res, uint32_t depth, uint32_t n_calls,
+                                 int32_t edit, int32_t device, float* ms, int32_t* updates, float* rgb,
+                                 float* rgb_fresh) {
+    if (n_calls == 0 || x_res == 0 || y_res == 0 || edit < 0 || edit > 3 || (edit && n_calls < 2))
+        return RT_ERR_INVALID_ARG;
+    Scene scene;
+    if (scene_id == 0) {
+        create_scene(scene);
+    } else {
+        rt_synth_params p;
+        if (rt_synth_config(scene_id, &p) != RT_OK) return RT_ERR_INVALID_ARG;
+        create_synth_scene(scene, p);
+    }
+    Camera camera(x_res, y_res);
+    RenderBuffer buffer(x_res, y_res);
+    for (uint32_t k = 0; k < n_calls; k++) {
+        if (edit && k + 1 == n_calls) {
+            if (edit == 1) {
+                Shape* s = scene.find_shape_mut("Sphere");
+                if (!s) return RT_ERR_INVALID_ARG;
+                s->set_transform(Matrix::translate(0.1f, 0.f, 0.f) * s->transform);
+            } else if (edit == 2) {
+                scene.shapes().front().material->reflectivity += 0.05f;
+            } else {
+                scene.add_light(PointLight(Point3(-3.f, 5.f, -6.f), Color(0.3f, 0.3f, 0.3f)));
+            }
+        }
+        auto t0 = std::chrono::steady_clock::now();
+        int32_t what = 0;
+        rt_status st = render(camera, scene, buffer, depth, device, nullptr, nullptr, &what);
+        if (st != RT_OK) return st;
+        if (ms) ms[k] = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (updates) updates[k] = what;
+    }
+    const size_t n = (size_t)x_res * y_res * 3;
+    if (rgb) std::memcpy(rgb, buffer.buf.data(), n * sizeof(float));
+    if (rgb_fresh) {
+        Scene copy(scene);  // a Scene of its own: a newly created device handle
+        RenderBuffer fresh(x_res, y_res);
+        int32_t what = 0;
+        rt_status st = render(camera, copy, fresh, depth, device, nullptr, nullptr, &what);
+        if (st != RT_OK) return st;
+        if (what != -1) return RT_ERR_INVALID_ARG;
+        std::memcpy(rgb_fresh, fresh.buf.data(), n * sizeof(float));
+    }
+    return RT_OK;
 }
 
 void rt_desc_free(rt_scene_desc* desc) {

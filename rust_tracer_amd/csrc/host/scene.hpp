@@ -16,6 +16,7 @@
 
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -112,6 +113,13 @@ Light AmbientLight(const Color& color);                   // mod.rs:228-233
 
 class Scene {  // mod.rs:22-85
 public:
+    Scene();
+    ~Scene();
+    Scene(const Scene& o);             // the copy renders through a device scene of its own
+    Scene& operator=(const Scene& o);
+    Scene(Scene&&) noexcept;
+    Scene& operator=(Scene&&) noexcept;
+
     void add_shape(Shape s);
     void add_light(const Light& l) { lights_.push_back(l); }
     void set_ambient(const Color& c) { ambient_ = c; }
@@ -119,6 +127,7 @@ public:
     const std::vector<Shape>& shapes() const { return shapes_; }
     const std::vector<Light>& lights() const { return lights_; }
     const Shape* find_shape(const std::string& name) const;
+    Shape* find_shape_mut(const std::string& name);  // mod.rs:66-74 (e.g. set_transform after add)
     // Renderable::size (mod.rs:124-126): a cube counts its 12 triangles (cube.rs:113-115)
     size_t size() const;
 
@@ -132,10 +141,19 @@ public:
     };
     std::unique_ptr<Flat> flatten() const;
 
+    // The device scene render() keeps across calls (the reference's render() takes the same
+    // &Scene every frame, main.rs:137-140): created by the first render(), brought up to date
+    // by rt_scene_update on later ones -- nothing to do when the scene is unchanged, material
+    // edits in place (Rc<RefCell<Material>> edits through a MaterialRef land here too), a
+    // rebuild after any other edit.  Freed with the Scene.
+    struct DeviceCache;
+    DeviceCache& device_cache() const { return *cache_; }
+
 private:
     Color ambient_ = colors::BLACK;
     std::vector<Shape> shapes_;
     std::vector<Light> lights_;
+    std::unique_ptr<DeviceCache> cache_;
 };
 
 struct Camera {  // render.rs:155-176
@@ -154,9 +172,12 @@ struct RenderBuffer {  // render.rs:5-19; stored row-major [v][u] (the reference
     const Color& at(uint32_t u, uint32_t v) const { return buf[(size_t)v * w + u]; }
 };
 
-// render.rs:31-38 through the C ABI.  `device` = -1 uses the current HIP device.
+// render.rs:31-38 through the C ABI.  `device` = -1 uses the current HIP device.  The scene's
+// device handle is kept across calls (Scene::DeviceCache); `update` (optional) reports what
+// this call did to it: -1 created, 0 reused as is, 1 materials edited in place, 2 rebuilt.
 rt_status render(const Camera& camera, const Scene& scene, RenderBuffer& buffer, uint32_t depth,
-                 int32_t device = -1, rt_counters* counters = nullptr, float* kernel_ms = nullptr);
+                 int32_t device = -1, rt_counters* counters = nullptr, float* kernel_ms = nullptr,
+                 int32_t* update = nullptr);
 
 // my_scene.rs:45-120
 void create_scene(Scene& scene);

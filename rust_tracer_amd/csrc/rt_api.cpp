@@ -16,9 +16,13 @@
 #include <cstring>
 #include <limits>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
+
+#include <sched.h>
 
 #include "../../include/rt_api.h"
 #include "rt_bvh.hpp"
@@ -216,6 +220,7 @@ struct CubeIn {
 // A hierarchy primitive as the light buffers see it: bounding ball and the run record
 // that tests it (LB_* type << 30 | record index).
 enum : uint32_t { LB_DSPH = 0, LB_GSPH = 1, LB_TRI = 2, LB_CUBE = 3 };
+constexpr size_t RUN_WIDTH[4] = {16, 16, 24, 16};  // floats per record of each run array
 struct LbPrim {
     double c[3], r;
     uint32_t code;
@@ -236,6 +241,15 @@ struct RunLayout {
     uint32_t graze_res = 0, graze_words = 0;
     std::vector<uint32_t> leaves;
     std::vector<LbPrim> lb_prims;  // every hierarchy primitive (light buffers)
+    // Record copies that follow a run array's own records in the device image: the light
+    // buffers' cells, then the shape buffers.  Kept apart (never concatenated on the host:
+    // the upload places each piece); lb is filled in parallel, uninitialised until then.
+    struct Ext {
+        std::unique_ptr<float[]> lb;
+        size_t lb_floats = 0;
+        std::vector<float> sb;
+    };
+    Ext ext[4];  // LB_DSPH, LB_GSPH, LB_TRI, LB_CUBE
     uint32_t root = BVH_LEAF;
     bool use = false;
     int n_dsph_bvh = 0, n_gsph_bvh = 0, n_tri_bvh = 0, n_cube_bvh = 0;
@@ -556,6 +570,65 @@ static void lb_face_dir(int f, double a, double b, double out[3]) {
     for (int i = 0; i < 3; i++) out[i] /= l;
 }
 
+// Host threads the scene build may use: Tune::build_threads, or the CPUs of the process's
+// affinity mask capped by its cgroup CPU quota (a container may see 256 CPUs and be granted
+// 16), at most 32.
+int build_thread_count(const Tune& T) {
+    if (T.build_threads > 0) return T.build_threads;
+    int n = 1;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) n = std::max(1, CPU_COUNT(&set));
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {  // cgroup v2: "quota period" or "max period"
+        char q[32] = {0};
+        long long period = 0;
+        if (std::fscanf(f, "%31s %lld", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0) {
+            const long long quota = std::atoll(q);
+            if (quota > 0) n = std::min<long long>(n, std::max(1LL, (quota + period - 1) / period));
+        }
+        std::fclose(f);
+    }
+    return std::min(n, 32);
+}
+
+// Runs f(0 .. n_jobs - 1) over up to `threads` host threads (the calling thread included).
+template <class F>
+void parallel_jobs(int n_jobs, int threads, F&& f) {
+    threads = std::max(1, std::min(threads, n_jobs));
+    std::atomic<int> next{0};
+    auto worker = [&]() {
+        for (int j; (j = next.fetch_add(1)) < n_jobs;) f(j);
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; t++) pool.emplace_back(worker);
+    worker();
+    for (auto& th : pool) th.join();
+}
+
+// One (light, tier) job of build_light_buffers: the cone of every hierarchy primitive's grown
+// ball seen from the light (nearest first), then per cell the records whose cone meets the
+// cell (a pair record listed once) and, per cell and record type, the place of their copies.
+struct LbJob {
+    uint32_t li = 0;
+    int tier = 0;
+    struct Cone {
+        double u[3], alpha, ca, sa, near;
+        uint32_t code;
+        int prev_same;  // the previous cone (nearest-first order) of the same record, or -1
+        uint8_t faces;  // the cube-map faces the cone may meet
+    };
+    std::vector<Cone> cones;
+    struct Ent {
+        uint32_t code;
+        float near;  // down-rounded nearest distance to the light (0 without the reach cut)
+    };
+    std::vector<std::vector<std::pair<uint32_t, Ent>>> chunk_hits;  // (cell, entry) per cone chunk
+    std::vector<uint32_t> cell_start;  // [nc + 1] into `ent` (entries grouped by cell)
+    std::vector<Ent> ent;
+    std::vector<uint32_t> cell_first;  // [4 nc]: per cell and type its first copy (job-relative)
+    size_t count[4] = {0, 0, 0, 0};  // copies per record type
+    size_t first[4] = {0, 0, 0, 0};  // the job's first copy in each run array
+};
+
 void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, LightBuffers& B, const Tune& T) {
     const int R = T.lb_res;  // cells per face side; 0: no light buffers (A/B)
     const bool reach_cut = T.lb_reach != 0;  // 0: runs are never cut at the reach (A/B)
@@ -590,6 +663,29 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
             }
     const double PI = 3.14159265358979323846;
     const double FACE_HALF = 0.9556;  // a face's directions lie within 54.75 deg of its axis
+    // blocks of up to 8 x 8 cells: a direction and an angle brad that exceeds the angle to
+    // every cell centre of the block plus that cell's radius.  A cone whose axis lies more
+    // than alpha + brad + 1e-4 rad from the block's direction meets none of its cells (the
+    // cell test below fails for each by far more than its 1e-12 slack), so the block is skipped
+    const int BS = 8, NB = (R + BS - 1) / BS;
+    std::vector<double> bdir(3 * (size_t)6 * NB * NB), brad((size_t)6 * NB * NB);
+    for (int f = 0; f < 6; f++)
+        for (int bj = 0; bj < NB; bj++)
+            for (int bi = 0; bi < NB; bi++) {
+                const size_t b = ((size_t)f * NB + bj) * NB + bi;
+                const int i0 = bi * BS, i1 = std::min(R, i0 + BS), j0 = bj * BS, j1 = std::min(R, j0 + BS);
+                double m[3];
+                lb_face_dir(f, -1.0 + (double)(i0 + i1) / R, -1.0 + (double)(j0 + j1) / R, m);
+                double rad = 0;
+                for (int j = j0; j < j1; j++)
+                    for (int i = i0; i < i1; i++) {
+                        const size_t c = ((size_t)f * R + j) * R + i;
+                        const double dt = m[0] * cdir[3 * c] + m[1] * cdir[3 * c + 1] + m[2] * cdir[3 * c + 2];
+                        rad = std::max(rad, std::acos(std::max(-1.0, std::min(1.0, dt))) + crad[c]);
+                    }
+                for (int k = 0; k < 3; k++) bdir[3 * b + k] = m[k];
+                brad[b] = rad;
+            }
     // Tier t serves origins with D <= dmax 2^t and a light within LB_LMAX 2^t (the device
     // compares with down_f(dmax) 2^t and RT_LB_LMAX^2 4^t): every primitive's ball grown by
     // its own bound at that reach (at most the hierarchy's), its cone by LB_MU 2^t (the
@@ -632,112 +728,182 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
                          lp[0], lp[1], lp[2], ok_t, near, (double)L.r);
         }
 #endif
+    // the jobs: every tier of every light that gets a buffer, in light then tier order (the
+    // order their cells take in the leaf table and their copies in the run arrays)
+    std::vector<LbJob> jobs;
+    uint32_t next_leaf = (uint32_t)(L.leaves.size() / 8);
     for (size_t li = 0; li < lights.size(); li++) {
         if (lights[li].kind != RT_LIGHT_POINT) continue;
         const double lp[3] = {lights[li].px, lights[li].py, lights[li].pz};
         const int tiers = tiers_of(lp);
         if (tiers == 0) continue;  // a primitive (nearly) at the light: no buffer
-        const uint32_t base = (uint32_t)(L.leaves.size() / 8);
-        if (base >= (1u << 28)) continue;  // (the tier count sits in LightRec::lb_base's top bits)
+        if (next_leaf >= (1u << 28)) continue;  // (the tier count sits in LightRec::lb_base's top bits)
+        B.base[li] = next_leaf | ((uint32_t)tiers << 28);
         B.tiers = std::max(B.tiers, (uint32_t)tiers);
+        next_leaf += (uint32_t)(tiers * nc);
         for (int t = 0; t < tiers; t++) {
-            const double dm = dmax * (double)(1 << t);
-            struct Cone {
-                double u[3], alpha, ca, sa, near;
-                uint32_t code;
-            };
-            std::vector<Cone> cones;
-            for (const LbPrim& p : L.lb_prims) {
-                double w[3] = {p.c[0] - lp[0], p.c[1] - lp[1], p.c[2] - lp[2]};
-                const double dist = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-                const double rr = grown(p, dm);
-                Cone c;
-                for (int k = 0; k < 3; k++) c.u[k] = dist > 0 ? w[k] / dist : (k == 0 ? 1.0 : 0.0);
-                if (dist - rr >= LB_RHO) {
-                    c.alpha = std::asin(std::min(1.0, rr / dist)) + LB_MU * (double)(1 << t);
-                } else {  // (lb_near_all tiers only) within LB_RHO of the light: every cell
-                    c.alpha = PI;
-                }
-                c.ca = std::cos(c.alpha);
-                c.sa = std::sin(c.alpha);
-                c.near = std::max(0.0, dist - rr);
-                c.code = p.code;
-                cones.push_back(c);
+            LbJob jb;
+            jb.li = (uint32_t)li;
+            jb.tier = t;
+            jobs.push_back(std::move(jb));
+        }
+    }
+    if (jobs.empty()) return;
+    const int threads = build_thread_count(T);
+    // (1) per job: the cones, nearest first, their faces and same-record links
+    parallel_jobs((int)jobs.size(), threads, [&](int ji) {
+        LbJob& jb = jobs[ji];
+        const double lp[3] = {lights[jb.li].px, lights[jb.li].py, lights[jb.li].pz};
+        const int t = jb.tier;
+        const double dm = dmax * (double)(1 << t);
+        std::vector<LbJob::Cone>& cones = jb.cones;
+        cones.reserve(L.lb_prims.size());
+        for (const LbPrim& p : L.lb_prims) {
+            double w[3] = {p.c[0] - lp[0], p.c[1] - lp[1], p.c[2] - lp[2]};
+            const double dist = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+            const double rr = grown(p, dm);
+            LbJob::Cone c;
+            for (int k = 0; k < 3; k++) c.u[k] = dist > 0 ? w[k] / dist : (k == 0 ? 1.0 : 0.0);
+            if (dist - rr >= LB_RHO) {
+                c.alpha = std::asin(std::min(1.0, rr / dist)) + LB_MU * (double)(1 << t);
+            } else {  // (lb_near_all tiers only) within LB_RHO of the light: every cell
+                c.alpha = PI;
             }
-            // nearest first: every cell's list comes out sorted by distance from the light
-            std::stable_sort(cones.begin(), cones.end(), [](const Cone& a, const Cone& b) { return a.near < b.near; });
-            std::vector<std::vector<std::pair<uint32_t, double>>> lists(nc);  // (code, nearest distance)
-            for (const Cone& c : cones) {
-                for (int f = 0; f < 6; f++) {
-                    const int k = f >> 1;
-                    const double s = (f & 1) ? -1.0 : 1.0;
-                    const double ax_ang = std::acos(std::max(-1.0, std::min(1.0, s * c.u[k])));
-                    if (ax_ang > c.alpha + FACE_HALF + 1e-3) continue;
-                    for (int cc = f * R * R; cc < (f + 1) * R * R; cc++) {
-                        bool in = c.alpha + crad[cc] >= PI;
-                        if (!in) {
-                            // angle(u, cell centre) <= alpha + cell radius  <=>  dot >= cos(alpha + rad)
-                            const double dt =
-                                c.u[0] * cdir[3 * cc] + c.u[1] * cdir[3 * cc + 1] + c.u[2] * cdir[3 * cc + 2];
-                            in = dt >= c.ca * ccos[cc] - c.sa * csin[cc] - 1e-12;
-                        }
-                        if (in) {
-                            auto& l = lists[cc];
-                            bool dup = false;  // a sphere / triangle pair's partner: keep the first entry
-                            for (const auto& q : l) dup = dup || q.first == c.code;
-                            if (!dup) l.push_back(std::make_pair(c.code, c.near));
-                        }
+            c.ca = std::cos(c.alpha);
+            c.sa = std::sin(c.alpha);
+            c.near = std::max(0.0, dist - rr);
+            c.code = p.code;
+            c.prev_same = -1;
+            c.faces = 0;
+            for (int f = 0; f < 6; f++) {  // the angle to the face's axis
+                const int k = f >> 1;
+                const double sg = (f & 1) ? -1.0 : 1.0;
+                const double ax_ang = std::acos(std::max(-1.0, std::min(1.0, sg * c.u[k])));
+                if (!(ax_ang > c.alpha + FACE_HALF + 1e-3)) c.faces |= (uint8_t)(1u << f);
+            }
+            cones.push_back(c);
+        }
+        // nearest first: every cell's list comes out sorted by distance from the light
+        std::stable_sort(cones.begin(), cones.end(),
+                         [](const LbJob::Cone& a, const LbJob::Cone& b) { return a.near < b.near; });
+        std::vector<std::pair<uint32_t, int>> byc(cones.size());
+        for (size_t i = 0; i < cones.size(); i++) byc[i] = std::make_pair(cones[i].code, (int)i);
+        std::sort(byc.begin(), byc.end());
+        for (size_t i = 1; i < byc.size(); i++)
+            if (byc[i].first == byc[i - 1].first) cones[byc[i].second].prev_same = byc[i - 1].second;
+    });
+    // (2) per job and chunk of cones: the (cell, entry) pairs in cone order
+    const int CONE_CHUNK = 64;
+    std::vector<std::pair<int, int>> units;
+    for (size_t ji = 0; ji < jobs.size(); ji++) {
+        const int n_chunks = (int)((jobs[ji].cones.size() + CONE_CHUNK - 1) / CONE_CHUNK);
+        jobs[ji].chunk_hits.resize(n_chunks);
+        for (int c = 0; c < n_chunks; c++) units.push_back(std::make_pair((int)ji, c));
+    }
+    parallel_jobs((int)units.size(), threads, [&](int ui) {
+        LbJob& jb = jobs[units[ui].first];
+        const std::vector<LbJob::Cone>& cones = jb.cones;
+        auto cell_in = [&](const LbJob::Cone& c, int cc) {
+            if (c.alpha + crad[cc] >= PI) return true;
+            // angle(u, cell centre) <= alpha + cell radius  <=>  dot >= cos(alpha + rad)
+            const double dt = c.u[0] * cdir[3 * cc] + c.u[1] * cdir[3 * cc + 1] + c.u[2] * cdir[3 * cc + 2];
+            return dt >= c.ca * ccos[cc] - c.sa * csin[cc] - 1e-12;
+        };
+        auto& hits = jb.chunk_hits[units[ui].second];
+        const size_t c0 = (size_t)units[ui].second * CONE_CHUNK, c1 = std::min(cones.size(), c0 + CONE_CHUNK);
+        for (size_t ci = c0; ci < c1; ci++) {
+            const LbJob::Cone& c = cones[ci];
+            const LbJob::Ent en{c.code, reach_cut ? down_f(c.near) : 0.f};
+            for (int f = 0; f < 6; f++) {
+                if (!(c.faces >> f & 1)) continue;
+                for (int b = f * NB * NB; b < (f + 1) * NB * NB; b++) {
+                    if (c.alpha + brad[b] + 1e-4 < PI) {
+                        const double dt = c.u[0] * bdir[3 * b] + c.u[1] * bdir[3 * b + 1] + c.u[2] * bdir[3 * b + 2];
+                        if (std::acos(std::max(-1.0, std::min(1.0, dt))) > c.alpha + brad[b] + 1e-4) continue;
                     }
+                    const int bj = (b - f * NB * NB) / NB, bi = (b - f * NB * NB) % NB;
+                    for (int j = bj * BS; j < std::min(R, bj * BS + BS); j++)
+                        for (int i = bi * BS; i < std::min(R, bi * BS + BS); i++) {
+                            const int cc = (f * R + j) * R + i;
+                            if (!cell_in(c, cc)) continue;
+                            // a pair record's partner listed here already: keep the first entry
+                            bool dup = false;
+                            for (int q = c.prev_same; q >= 0 && !dup; q = cones[q].prev_same)
+                                dup = (cones[q].faces >> f & 1) && cell_in(cones[q], cc);
+                            if (!dup) hits.push_back(std::make_pair((uint32_t)cc, en));
+                        }
                 }
-            }
-            for (int cc = 0; cc < nc; cc++) {
-                // per type, nearest first; each copy carries its nearest distance to the light
-                // (down-rounded) in the record's spare slot: the device stops a run at the first
-                // record no undecided lane can reach
-                std::vector<uint32_t> by[4];
-                std::vector<float> nr[4];
-                for (const auto& q : lists[cc]) {
-                    by[q.first >> 30].push_back(q.first & 0x3FFFFFFFu);
-                    nr[q.first >> 30].push_back(reach_cut ? down_f(q.second) : 0.f);
-                }
-                uint32_t rec[8];
-                rec[0] = (uint32_t)(L.dsph.size() / 16);
-                for (size_t q = 0; q < by[LB_DSPH].size(); q++) {
-                    const uint32_t r = by[LB_DSPH][q];
-                    std::vector<float> t(L.dsph.begin() + 16 * (size_t)r, L.dsph.begin() + 16 * (size_t)r + 16);
-                    t[15] = nr[LB_DSPH][q];
-                    L.dsph.insert(L.dsph.end(), t.begin(), t.end());
-                }
-                rec[1] = (uint32_t)(L.dsph.size() / 16);
-                rec[2] = (uint32_t)(L.gsph.size() / 16);
-                for (size_t q = 0; q < by[LB_GSPH].size(); q++) {
-                    const uint32_t r = by[LB_GSPH][q];
-                    std::vector<float> t(L.gsph.begin() + 16 * (size_t)r, L.gsph.begin() + 16 * (size_t)r + 16);
-                    t[15] = nr[LB_GSPH][q];
-                    L.gsph.insert(L.gsph.end(), t.begin(), t.end());
-                }
-                rec[3] = (uint32_t)(L.gsph.size() / 16);
-                rec[4] = (uint32_t)(L.tri.size() / 24);
-                for (size_t q = 0; q < by[LB_TRI].size(); q++) {
-                    const uint32_t r = by[LB_TRI][q];
-                    std::vector<float> t(L.tri.begin() + 24 * (size_t)r, L.tri.begin() + 24 * (size_t)r + 24);
-                    t[20] = nr[LB_TRI][q];
-                    L.tri.insert(L.tri.end(), t.begin(), t.end());
-                }
-                rec[5] = (uint32_t)(L.tri.size() / 24);
-                rec[6] = (uint32_t)(L.cube.size() / 16);
-                for (size_t q = 0; q < by[LB_CUBE].size(); q++) {
-                    const uint32_t r = by[LB_CUBE][q];
-                    std::vector<float> t(L.cube.begin() + 16 * (size_t)r, L.cube.begin() + 16 * (size_t)r + 16);
-                    t[15] = nr[LB_CUBE][q];
-                    L.cube.insert(L.cube.end(), t.begin(), t.end());
-                }
-                rec[7] = (uint32_t)(L.cube.size() / 16);
-                L.leaves.insert(L.leaves.end(), rec, rec + 8);
             }
         }
-        B.base[li] = base | ((uint32_t)tiers << 28);
+    });
+    // (3) per job: the entries grouped by cell (stable: nearest first), per cell and type the
+    // first copy
+    parallel_jobs((int)jobs.size(), threads, [&](int ji) {
+        LbJob& jb = jobs[ji];
+        jb.cell_start.assign((size_t)nc + 1, 0);
+        size_t n = 0;
+        for (const auto& hits : jb.chunk_hits) {
+            n += hits.size();
+            for (const auto& h : hits) jb.cell_start[h.first + 1]++;
+        }
+        for (int cc = 0; cc < nc; cc++) jb.cell_start[cc + 1] += jb.cell_start[cc];
+        jb.ent.resize(n);
+        std::vector<uint32_t> fill(jb.cell_start.begin(), jb.cell_start.end() - 1);
+        for (auto& hits : jb.chunk_hits) {
+            for (const auto& h : hits) jb.ent[fill[h.first]++] = h.second;
+            std::vector<std::pair<uint32_t, LbJob::Ent>>().swap(hits);
+        }
+        jb.cell_first.resize(4 * (size_t)nc);
+        for (int cc = 0; cc < nc; cc++) {
+            for (int k = 0; k < 4; k++) jb.cell_first[4 * cc + k] = (uint32_t)jb.count[k];
+            for (uint32_t e = jb.cell_start[cc]; e < jb.cell_start[cc + 1]; e++) jb.count[jb.ent[e].code >> 30]++;
+        }
+    });
+    // the copies' places: each job's copies follow the previous job's, per run array, after
+    // the array's own records
+    const size_t spare[4] = {15, 15, 20, 15};  // the record slot that carries the nearest distance
+    const std::vector<float>* run[4] = {&L.dsph, &L.gsph, &L.tri, &L.cube};
+    size_t n_src[4], n_rec[4];
+    for (int k = 0; k < 4; k++) n_src[k] = n_rec[k] = run[k]->size() / RUN_WIDTH[k];
+    for (LbJob& jb : jobs)
+        for (int k = 0; k < 4; k++) {
+            jb.first[k] = n_rec[k];
+            n_rec[k] += jb.count[k];
+        }
+    for (int k = 0; k < 4; k++) {
+        L.ext[k].lb_floats = (n_rec[k] - n_src[k]) * RUN_WIDTH[k];
+        L.ext[k].lb.reset(new float[std::max<size_t>(1, L.ext[k].lb_floats)]);
     }
+    const size_t leaf0 = L.leaves.size();
+    L.leaves.resize(leaf0 + jobs.size() * (size_t)nc * 8);
+    // per cell, per type nearest first; each copy carries its nearest distance to the light
+    // (down-rounded) in the record's spare slot: the device stops a run at the first record
+    // no undecided lane can reach
+    const int CELL_CHUNK = 512;
+    const int n_cell_chunks = (nc + CELL_CHUNK - 1) / CELL_CHUNK;
+    parallel_jobs((int)jobs.size() * n_cell_chunks, threads, [&](int ui) {
+        const int ji = ui / n_cell_chunks, c0 = (ui % n_cell_chunks) * CELL_CHUNK, c1 = std::min(nc, c0 + CELL_CHUNK);
+        const LbJob& jb = jobs[ji];
+        uint32_t* leaf = L.leaves.data() + leaf0 + ((size_t)ji * nc + c0) * 8;
+        for (int cc = c0; cc < c1; cc++, leaf += 8) {
+            for (int k = 0; k < 4; k++) {
+                const size_t w = RUN_WIDTH[k];
+                size_t at = jb.first[k] + jb.cell_first[4 * cc + k];
+                leaf[2 * k] = (uint32_t)at;
+                const float* src = run[k]->data();
+                float* dst = L.ext[k].lb.get() - n_src[k] * w;  // record index -> its place
+                for (uint32_t e = jb.cell_start[cc]; e < jb.cell_start[cc + 1]; e++) {
+                    const LbJob::Ent& en = jb.ent[e];
+                    if ((int)(en.code >> 30) != k) continue;
+                    const size_t r = en.code & 0x3FFFFFFFu;  // a hierarchy record (< n_src)
+                    std::memcpy(dst + w * at, src + w * r, w * sizeof(float));
+                    dst[w * at + spare[k]] = en.near;
+                    at++;
+                }
+                leaf[2 * k + 1] = (uint32_t)at;
+            }
+        }
+    });
 }
 
 // Shape buffers (rt_scan.hpp scan_buffered, key mode 7).  A ray inside a sphere S tests S
@@ -783,18 +949,15 @@ void build_shape_buffers(RunLayout& L, std::vector<ShapeRec>& shapes, const Tune
 #endif
         if (n_rec == 0 || n_rec > 96) continue;
         uint32_t rec[8];
-        auto copy = [&](std::vector<float>& run, size_t width, const std::vector<uint32_t>& recs, uint32_t* range) {
-            range[0] = (uint32_t)(run.size() / width);
-            for (uint32_t r : recs) {
-                std::vector<float> t(run.begin() + width * (size_t)r, run.begin() + width * (size_t)r + width);
-                run.insert(run.end(), t.begin(), t.end());
-            }
-            range[1] = (uint32_t)(run.size() / width);
-        };
-        copy(L.dsph, 16, by[LB_DSPH], rec + 0);
-        copy(L.gsph, 16, by[LB_GSPH], rec + 2);
-        copy(L.tri, 24, by[LB_TRI], rec + 4);
-        copy(L.cube, 16, by[LB_CUBE], rec + 6);
+        // copies of hierarchy records, after the run array's records and light-buffer copies
+        const std::vector<float>* runs[4] = {&L.dsph, &L.gsph, &L.tri, &L.cube};
+        for (int k = 0; k < 4; k++) {
+            const size_t w = RUN_WIDTH[k];
+            std::vector<float>& sb = L.ext[k].sb;
+            rec[2 * k] = (uint32_t)((runs[k]->size() + L.ext[k].lb_floats + sb.size()) / w);
+            for (uint32_t r : by[k]) sb.insert(sb.end(), runs[k]->begin() + w * r, runs[k]->begin() + w * (r + 1));
+            rec[2 * k + 1] = (uint32_t)((runs[k]->size() + L.ext[k].lb_floats + sb.size()) / w);
+        }
         const uint32_t leaf = (uint32_t)(L.leaves.size() / 8);
         L.leaves.insert(L.leaves.end(), rec, rec + 8);
         R.pad1 = (int32_t)(leaf + 1);
@@ -1169,6 +1332,11 @@ struct rt_scene {
     uint64_t checked_items = 0;
     uint32_t checked_depth = 0;
     bool ovf_pending = false;
+    // the description the device scene was built from (rt_scene_update compares against it)
+    std::vector<rt_material> d_mats;
+    std::vector<rt_shape> d_shapes;
+    std::vector<rt_light> d_lights;
+    rt_color d_ambient{0.f, 0.f, 0.f};
 };
 
 rt_multi_state*& rt_scene_multi(rt_scene* s) { return s->multi; }
@@ -1277,58 +1445,49 @@ void free_workspace(Workspace& w) {
     w = Workspace();
 }
 
-}  // namespace
+// The host half of rt_scene_create: every array of the device scene, built from the
+// description without a HIP call (rt_scene_layout_digest runs it alone), and the section
+// table of the one device allocation.
+struct HostScene {
+    static constexpr int N_SECS = 16;
+    struct Sec {  // a section of the device allocation: up to three host pieces, back to back
+        const void* src[3];
+        size_t bytes[3];
+        size_t off;
+        size_t size() const { return bytes[0] + bytes[1] + bytes[2]; }
+    };
+    std::vector<float> dsph, gsph, tri, cube, plane, cubetri;
+    std::vector<ShapeRec> shapes;
+    std::vector<MatRec> mats;
+    std::vector<LightRec> lights;
+    RunLayout lay;
+    LightBuffers lbuf;
+    uint64_t flops = 0;
+    uint32_t n_point = 0;
+    bool normals_ok = true;
+    double nmax = 1.0;
+    int n_dsph_all = 0, n_gsph_all = 0, n_tri_all = 0, n_cube_all = 0;
+    Sec secs[N_SECS];
+    size_t total = 0;
+};
 
-extern "C" {
+rt_status create_handle(const rt_scene_desc* d, int32_t device, const Tune& tn, rt_scene** out);
 
-int32_t rt_api_version(void) { return RT_API_VERSION; }
-uint32_t rt_max_frames(void) { return RT_MAX_FRAMES; }
-
-const char* rt_status_str(rt_status s) {
-    switch (s) {
-        case RT_OK: return "RT_OK";
-        case RT_ERR_INVALID_ARG: return "RT_ERR_INVALID_ARG";
-        case RT_ERR_SINGULAR_MATRIX: return "RT_ERR_SINGULAR_MATRIX";
-        case RT_ERR_UNSUPPORTED: return "RT_ERR_UNSUPPORTED";
-        case RT_ERR_NO_DEVICE: return "RT_ERR_NO_DEVICE";
-        case RT_ERR_HIP: return "RT_ERR_HIP";
-        case RT_ERR_OUT_OF_MEMORY: return "RT_ERR_OUT_OF_MEMORY";
-        case RT_ERR_BAD_MATERIAL: return "RT_ERR_BAD_MATERIAL";
-        case RT_ERR_CAPACITY: return "RT_ERR_CAPACITY";
-        default: return "RT_ERR_UNKNOWN";
-    }
-}
-
-uint32_t rt_band_rows_per_rank(uint32_t y_res, uint32_t band_rows, uint32_t world) {
-    if (band_rows == 0 || world == 0) return 0;
-    uint32_t n_bands = (y_res + band_rows - 1) / band_rows;
-    uint32_t per_rank = (n_bands + world - 1) / world;
-    return per_rank * band_rows;
-}
-
-rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out) {
-    return rt_scene_create_tuned(d, device, nullptr, out);
-}
-
-rt_status rt_scene_create_tuned(const rt_scene_desc* d, int32_t device, const char* tuning, rt_scene** out) {
-    if (!d || !out) return RT_ERR_INVALID_ARG;
-    // the handle's tuning: defaults, the environment's RT_TUNE (A/B harness), then `tuning`
-    Tune tn;
-    if (!tune_apply(tn, std::getenv("RT_TUNE"), true) || !tune_apply(tn, tuning, true)) return RT_ERR_INVALID_ARG;
+rt_status prepare_scene(const rt_scene_desc* d, const Tune& tn, HostScene& H) {
     if ((d->n_materials && !d->materials) || (d->n_shapes && !d->shapes) || (d->n_lights && !d->lights))
         return RT_ERR_INVALID_ARG;
     if (d->n_shapes >= (1u << 27)) return RT_ERR_UNSUPPORTED;
     if (d->n_materials > RT_MAX_MATERIALS) return RT_ERR_UNSUPPORTED;  // node_flags holds the index
 
     // ---- host preprocessing: per-shape records
-    std::vector<float> dsph, gsph, tri, cube, plane, cubetri;
-    std::vector<ShapeRec> shapes(d->n_shapes);
+    std::vector<ShapeRec>& shapes = H.shapes;
+    shapes.resize(d->n_shapes);
     std::vector<SphIn> sph_in;
     std::vector<TriIn> tri_in;
     std::vector<CubeIn> cube_in;
-    uint64_t flops = 0;
-    bool normals_ok = true;  // DevScene::dark_skip: every hit normal finite with |n| <= 1e3
-    double nmax = 1.0;       // largest hit-normal length (unit normals; planes: |transform * n|)
+    uint64_t& flops = H.flops;
+    bool& normals_ok = H.normals_ok;  // DevScene::dark_skip: every hit normal finite with |n| <= 1e3
+    double& nmax = H.nmax;    // largest hit-normal length (unit normals; planes: |transform * n|)
     for (uint32_t i = 0; i < d->n_shapes; i++) {
         const rt_shape& s = d->shapes[i];
         if (s.material < 0 || (uint32_t)s.material >= d->n_materials) return RT_ERR_BAD_MATERIAL;
@@ -1367,9 +1526,9 @@ rt_status rt_scene_create_tuned(const rt_scene_desc* d, int32_t device, const ch
                 nmax = std::max(nmax, std::sqrt((double)tn.x * tn.x + (double)tn.y * tn.y + (double)tn.z * tn.z));
                 const float a[15] = {n.x, n.y, n.z, o.x, o.y, o.z, tn.x, tn.y, tn.z, u.x, u.y, u.z, v.x, v.y, v.z};
                 std::memcpy(R.a, a, sizeof(a));
-                for (int r = 0; r < 3; r++) put4(plane, inv.m[r][0], inv.m[r][1], inv.m[r][2], inv.m[r][3]);
-                put4(plane, n.x, n.y, n.z, key);
-                put4(plane, o.x, o.y, o.z, 0.f);
+                for (int r = 0; r < 3; r++) put4(H.plane, inv.m[r][0], inv.m[r][1], inv.m[r][2], inv.m[r][3]);
+                put4(H.plane, n.x, n.y, n.z, key);
+                put4(H.plane, o.x, o.y, o.z, 0.f);
                 flops += 49;
                 break;
             }
@@ -1403,21 +1562,23 @@ rt_status rt_scene_create_tuned(const rt_scene_desc* d, int32_t device, const ch
         }
     }
     if (d->n_lights > 32) return RT_ERR_UNSUPPORTED;  // shadow results are a 32-bit mask per node
-    uint32_t n_point = 0;
-    std::vector<LightRec> lights(d->n_lights);
+    std::vector<LightRec>& lights = H.lights;
+    lights.resize(d->n_lights);
     for (uint32_t i = 0; i < d->n_lights; i++) {
         const rt_light& l = d->lights[i];
         if (l.kind != RT_LIGHT_POINT && l.kind != RT_LIGHT_AMBIENT) return RT_ERR_INVALID_ARG;
         lights[i] = LightRec{l.kind, l.pos[0], l.pos[1], l.pos[2], l.color.r, l.color.g, l.color.b, 0xFFFFFFFFu};
-        if (l.kind == RT_LIGHT_POINT) n_point++;
+        if (l.kind == RT_LIGHT_POINT) H.n_point++;
     }
     // ---- culling hierarchy and the run layout (leaf order first, then the linear rest)
-    RunLayout lay;
+    RunLayout& lay = H.lay;
     build_runs(sph_in, tri_in, cube_in, tn, lay);
     // light buffers append cell leaves and record copies to the layout (after the linear
     // rest: the scan's run counts below exclude them)
-    const int n_dsph_all = (int)(lay.dsph.size() / 16), n_gsph_all = (int)(lay.gsph.size() / 16);
-    const int n_tri_all = (int)(lay.tri.size() / 24), n_cube_all = (int)(lay.cube.size() / 16);
+    H.n_dsph_all = (int)(lay.dsph.size() / 16);
+    H.n_gsph_all = (int)(lay.gsph.size() / 16);
+    H.n_tri_all = (int)(lay.tri.size() / 24);
+    H.n_cube_all = (int)(lay.cube.size() / 16);
     // the Morton code (morton15, rt_wavefront.hip) of every sphere's and cube's centre -- the
     // forward transform's translation: the task key of rays inside the shape
     if (lay.use) {
@@ -1437,48 +1598,102 @@ rt_status rt_scene_create_tuned(const rt_scene_desc* d, int32_t device, const ch
             shapes[i].center_key = (spread5(x) << 2) | (spread5(y) << 1) | spread5(z);
         }
     }
-    LightBuffers lbuf;
+    LightBuffers& lbuf = H.lbuf;
     build_light_buffers(lay, lights, lbuf, tn);
     for (size_t i = 0; i < lights.size(); i++) lights[i].lb_base = lbuf.base[i];
     build_shape_buffers(lay, shapes, tn);
-    dsph.swap(lay.dsph);
-    gsph.swap(lay.gsph);
-    tri.swap(lay.tri);
-    cube.swap(lay.cube);
-    cube_triangles(cubetri);
-    if (!rt_cube_table_check(cubetri.data())) return RT_ERR_UNSUPPORTED;
-    std::vector<MatRec> mats(d->n_materials);
+    H.dsph.swap(lay.dsph);
+    H.gsph.swap(lay.gsph);
+    H.tri.swap(lay.tri);
+    H.cube.swap(lay.cube);
+    cube_triangles(H.cubetri);
+    if (!rt_cube_table_check(H.cubetri.data())) return RT_ERR_UNSUPPORTED;
+    std::vector<MatRec>& mats = H.mats;
+    mats.resize(d->n_materials);
     for (uint32_t i = 0; i < d->n_materials; i++) {
         rt_status r = mat_rec(d->materials[i], mats[i], nmax);
         if (r != RT_OK) return r;
     }
     // ---- one allocation, 256-B aligned sections
-    struct Sec {
-        const void* src;
-        size_t bytes;
-        size_t off;
-    };
     static const unsigned long long zero_ops[RT_OPS_SLOTS * RT_OPS_STRIDE] = {0};
-    Sec secs[16] = {{dsph.data(), dsph.size() * 4, 0},       {gsph.data(), gsph.size() * 4, 0},
-                    {tri.data(), tri.size() * 4, 0},         {cube.data(), cube.size() * 4, 0},
-                    {plane.data(), plane.size() * 4, 0},     {cubetri.data(), cubetri.size() * 4, 0},
-                    {shapes.data(), shapes.size() * sizeof(ShapeRec), 0},
-                    {mats.data(), mats.size() * sizeof(MatRec), 0},
-                    {lights.data(), lights.size() * sizeof(LightRec), 0},
-                    {lay.nodes.data(), lay.nodes.size() * 4, 0},
-                    {lay.leaves.data(), lay.leaves.size() * 4, 0},
-                    {lay.graze_blk.data(), lay.graze_blk.size() * 4, 0},
-                    {zero_ops, sizeof(zero_ops), 0},
-                    {lay.graze_tri.data(), lay.graze_tri.size() * 4, 0},
-                    {lay.graze_pn.data(), lay.graze_pn.size() * 4, 0},
-                    {lay.graze_mask.data(), lay.graze_mask.size() * 4, 0}};
+    auto one = [](const void* p, size_t n) { return HostScene::Sec{{p, nullptr, nullptr}, {n, 0, 0}, 0}; };
+    // a run array: its records, the light buffers' copies, the shape buffers' copies
+    auto run = [&](const std::vector<float>& v, int k) {
+        const RunLayout::Ext& e = lay.ext[k];
+        return HostScene::Sec{{v.data(), e.lb.get(), e.sb.data()}, {v.size() * 4, e.lb_floats * 4, e.sb.size() * 4}, 0};
+    };
+    const HostScene::Sec secs[HostScene::N_SECS] = {
+        run(H.dsph, LB_DSPH), run(H.gsph, LB_GSPH), run(H.tri, LB_TRI), run(H.cube, LB_CUBE),
+        one(H.plane.data(), H.plane.size() * 4), one(H.cubetri.data(), H.cubetri.size() * 4),
+        one(shapes.data(), shapes.size() * sizeof(ShapeRec)),
+        one(mats.data(), mats.size() * sizeof(MatRec)),
+        one(lights.data(), lights.size() * sizeof(LightRec)),
+        one(lay.nodes.data(), lay.nodes.size() * 4),
+        one(lay.leaves.data(), lay.leaves.size() * 4),
+        one(lay.graze_blk.data(), lay.graze_blk.size() * 4),
+        one(zero_ops, sizeof(zero_ops)),
+        one(lay.graze_tri.data(), lay.graze_tri.size() * 4),
+        one(lay.graze_pn.data(), lay.graze_pn.size() * 4),
+        one(lay.graze_mask.data(), lay.graze_mask.size() * 4)};
     size_t total = 0;
-    for (auto& s : secs) {
-        s.off = total;
-        total += (s.bytes + 96 + 255) & ~(size_t)255;  // + one record group of look-ahead slack
+    for (int k = 0; k < HostScene::N_SECS; k++) {
+        H.secs[k] = secs[k];
+        H.secs[k].off = total;
+        total += (secs[k].size() + 96 + 255) & ~(size_t)255;  // + one record group of look-ahead slack
     }
-    if (total == 0) total = 256;
+    H.total = total == 0 ? 256 : total;
+    return RT_OK;
+}
 
+}  // namespace
+
+extern "C" {
+
+int32_t rt_api_version(void) { return RT_API_VERSION; }
+uint32_t rt_max_frames(void) { return RT_MAX_FRAMES; }
+
+const char* rt_status_str(rt_status s) {
+    switch (s) {
+        case RT_OK: return "RT_OK";
+        case RT_ERR_INVALID_ARG: return "RT_ERR_INVALID_ARG";
+        case RT_ERR_SINGULAR_MATRIX: return "RT_ERR_SINGULAR_MATRIX";
+        case RT_ERR_UNSUPPORTED: return "RT_ERR_UNSUPPORTED";
+        case RT_ERR_NO_DEVICE: return "RT_ERR_NO_DEVICE";
+        case RT_ERR_HIP: return "RT_ERR_HIP";
+        case RT_ERR_OUT_OF_MEMORY: return "RT_ERR_OUT_OF_MEMORY";
+        case RT_ERR_BAD_MATERIAL: return "RT_ERR_BAD_MATERIAL";
+        case RT_ERR_CAPACITY: return "RT_ERR_CAPACITY";
+        default: return "RT_ERR_UNKNOWN";
+    }
+}
+
+uint32_t rt_band_rows_per_rank(uint32_t y_res, uint32_t band_rows, uint32_t world) {
+    if (band_rows == 0 || world == 0) return 0;
+    uint32_t n_bands = (y_res + band_rows - 1) / band_rows;
+    uint32_t per_rank = (n_bands + world - 1) / world;
+    return per_rank * band_rows;
+}
+
+rt_status rt_scene_create(const rt_scene_desc* d, int32_t device, rt_scene** out) {
+    return rt_scene_create_tuned(d, device, nullptr, out);
+}
+
+rt_status rt_scene_create_tuned(const rt_scene_desc* d, int32_t device, const char* tuning, rt_scene** out) {
+    if (!d || !out) return RT_ERR_INVALID_ARG;
+    // the handle's tuning: defaults, the environment's RT_TUNE (A/B harness), then `tuning`
+    Tune tn;
+    if (!tune_apply(tn, std::getenv("RT_TUNE"), true) || !tune_apply(tn, tuning, true)) return RT_ERR_INVALID_ARG;
+    return create_handle(d, device, tn, out);
+}
+
+}  // extern "C"
+
+namespace {
+
+rt_status create_handle(const rt_scene_desc* d, int32_t device, const Tune& tn, rt_scene** out) {
+    HostScene H;
+    rt_status pst = prepare_scene(d, tn, H);
+    if (pst != RT_OK) return pst;
     std::unique_ptr<rt_scene> sc(new (std::nothrow) rt_scene());
     if (!sc) return RT_ERR_OUT_OF_MEMORY;
     rt_status st = select_device(device, &sc->device);
@@ -1486,15 +1701,17 @@ rt_status rt_scene_create_tuned(const rt_scene_desc* d, int32_t device, const ch
     HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreate(&sc->ev0));
     HIP_TRY(hipEventCreate(&sc->ev1));
-    HIP_TRY(hipMalloc(&sc->dmem, total));
-    sc->dbytes = total;
-    std::vector<uint8_t> host(total, 0);
-    for (auto& s : secs)
-        if (s.bytes) std::memcpy(host.data() + s.off, s.src, s.bytes);
-    // on the scene's own stream, waited for (the host buffer is pageable and goes out of scope)
-    HIP_TRY(hipMemcpyAsync(sc->dmem, host.data(), total, hipMemcpyHostToDevice, sc->stream));
+    HIP_TRY(hipMalloc(&sc->dmem, H.total));
+    sc->dbytes = H.total;
+    // on the scene's own stream, waited for (the host arrays are pageable and go out of
+    // scope): the padding zeroed, then each section straight from its array
+    HIP_TRY(hipMemsetAsync(sc->dmem, 0, H.total, sc->stream));
+    for (const auto& s : H.secs)
+        for (size_t p = 0, at = s.off; p < 3; at += s.bytes[p], p++)
+            if (s.bytes[p])
+                HIP_TRY(hipMemcpyAsync((uint8_t*)sc->dmem + at, s.src[p], s.bytes[p], hipMemcpyHostToDevice, sc->stream));
     HIP_TRY(hipStreamSynchronize(sc->stream));
-    auto at = [&](int k) { return (const void*)((const uint8_t*)sc->dmem + secs[k].off); };
+    auto at = [&](int k) { return (const void*)((const uint8_t*)sc->dmem + H.secs[k].off); };
     DevScene& S = sc->S;
     S.dsph = (const float4*)at(0);
     S.gsph = (const float4*)at(1);
@@ -1505,11 +1722,11 @@ rt_status rt_scene_create_tuned(const rt_scene_desc* d, int32_t device, const ch
     S.shapes = (const ShapeRec*)at(6);
     S.mats = (const MatRec*)at(7);
     S.lights = (const LightRec*)at(8);
-    S.n_dsph = n_dsph_all;  // pairs (light-buffer copies follow)
-    S.n_gsph = n_gsph_all;
-    S.n_tri = n_tri_all;    // pairs
-    S.n_cube = n_cube_all;
-    S.n_plane = (int32_t)(plane.size() / 20);
+    S.n_dsph = H.n_dsph_all;  // pairs (light-buffer copies follow)
+    S.n_gsph = H.n_gsph_all;
+    S.n_tri = H.n_tri_all;    // pairs
+    S.n_cube = H.n_cube_all;
+    S.n_plane = (int32_t)(H.plane.size() / 20);
     S.n_shapes = (int32_t)d->n_shapes;
     S.n_lights = (int32_t)d->n_lights;
     S.n_mats = (int32_t)d->n_materials;
@@ -1520,46 +1737,127 @@ rt_status rt_scene_create_tuned(const rt_scene_desc* d, int32_t device, const ch
     S.graze_tri = (const float4*)at(13);
     S.graze_pn = (const float4*)at(14);
     S.graze_mask = (const uint32_t*)at(15);
-    S.graze_res = lay.graze_res;
-    S.graze_words = lay.graze_words;
+    S.graze_res = H.lay.graze_res;
+    S.graze_words = H.lay.graze_words;
     S.graze_lane = tn.graze_lane ? 1u : 0u;  // 0: the wave-union grazing path (A/B)
-    S.lb_res = lbuf.res;
-    S.lb_dmax = lbuf.dmax;
-    S.lb_tiers = lbuf.tiers;
-    S.n_graze_blk = (int32_t)(lay.graze_blk.size() / 32);
+    S.lb_res = H.lbuf.res;
+    S.lb_dmax = H.lbuf.dmax;
+    S.lb_tiers = H.lbuf.tiers;
+    S.n_graze_blk = (int32_t)(H.lay.graze_blk.size() / 32);
 #if RT_DIAG
     if (std::getenv("RT_DEBUG_NO_GRAZE")) S.n_graze_blk = 0;  // measurement only: NOT exact (the grazing pass's cost)
 #endif
-    S.bvh_root = lay.root;
-    S.n_bvh_nodes = (int32_t)(lay.nodes.size() / 16);
-    S.use_bvh = lay.use ? 1 : 0;
-    S.n_dsph_bvh = lay.n_dsph_bvh;
-    S.n_gsph_bvh = lay.n_gsph_bvh;
-    S.n_tri_bvh = lay.n_tri_bvh;
-    S.n_cube_bvh = lay.n_cube_bvh;
-    S.bvh_cx = lay.c[0];
-    S.bvh_cy = lay.c[1];
-    S.bvh_cz = lay.c[2];
-    S.bvh_r = lay.r;
-    S.bvh_g2 = lay.g2;
-    S.bvh_g1 = lay.g1;
-    S.bvh_g0 = lay.g0;
-    S.bvh_m1 = lay.m1;
-    S.bvh_m0 = lay.m0;
+    S.bvh_root = H.lay.root;
+    S.n_bvh_nodes = (int32_t)(H.lay.nodes.size() / 16);
+    S.use_bvh = H.lay.use ? 1 : 0;
+    S.n_dsph_bvh = H.lay.n_dsph_bvh;
+    S.n_gsph_bvh = H.lay.n_gsph_bvh;
+    S.n_tri_bvh = H.lay.n_tri_bvh;
+    S.n_cube_bvh = H.lay.n_cube_bvh;
+    S.bvh_cx = H.lay.c[0];
+    S.bvh_cy = H.lay.c[1];
+    S.bvh_cz = H.lay.c[2];
+    S.bvh_r = H.lay.r;
+    S.bvh_g2 = H.lay.g2;
+    S.bvh_g1 = H.lay.g1;
+    S.bvh_g0 = H.lay.g0;
+    S.bvh_m1 = H.lay.m1;
+    S.bvh_m0 = H.lay.m0;
     S.graze_s2 = 1.0201f;  // normals pre-divided by sin(phi_T): checked at 1.01 sin(phi_T)
 #if RT_DIAG
     if (const char* e = std::getenv("RT_DEBUG_GRAZE_S2")) S.graze_s2 = (float)std::atof(e);  // measurement only: NOT exact
 #endif
-    S.dark_skip = (normals_ok && tn.dark_skip) ? 1 : 0;
+    S.dark_skip = (H.normals_ok && tn.dark_skip) ? 1 : 0;
     S.amb_r = d->ambient.r;
     S.amb_g = d->ambient.g;
     S.amb_b = d->ambient.b;
-    sc->flops_per_scan = flops;
-    sc->n_point_lights = n_point;
-    sc->normal_max = nmax;
+    sc->flops_per_scan = H.flops;
+    sc->n_point_lights = H.n_point;
+    sc->normal_max = H.nmax;
     sc->num_cus = g_num_cus(sc->device);
     sc->tune = tn;
+    sc->d_mats.assign(d->materials, d->materials + d->n_materials);
+    sc->d_shapes.assign(d->shapes, d->shapes + d->n_shapes);
+    sc->d_lights.assign(d->lights, d->lights + d->n_lights);
+    sc->d_ambient = d->ambient;
     *out = sc.release();
+    return RT_OK;
+}
+
+// Replaces the scene data of `dst` (its device allocation and DevScene) by a copy of src's,
+// on dst's device, after dst's renders have finished (the caller synchronised them).
+rt_status adopt_scene_data(rt_scene* dst, const rt_scene* src) {
+    HIP_TRY(hipSetDevice(dst->device));
+    HIP_TRY(hipStreamSynchronize(dst->stream));
+    for (auto& se : dst->ev_streams) HIP_TRY(hipEventSynchronize(se.second));  // renders on other streams
+    void* mem = nullptr;
+    HIP_TRY(hipMalloc(&mem, src->dbytes));
+    rt_status st = RT_OK;
+    if (dst->device == src->device)
+        st = hip_status(hipMemcpyAsync(mem, src->dmem, src->dbytes, hipMemcpyDeviceToDevice, dst->stream));
+    else
+        st = hip_status(hipMemcpyPeerAsync(mem, dst->device, src->dmem, src->device, src->dbytes, dst->stream));
+    if (st == RT_OK) st = hip_status(hipStreamSynchronize(dst->stream));
+    if (st != RT_OK) {
+        (void)hipFree(mem);
+        return st;
+    }
+    if (dst->dmem) (void)hipFree(dst->dmem);
+    dst->dmem = mem;
+    dst->dbytes = src->dbytes;
+    dst->S = src->S;
+    const uint8_t* from = (const uint8_t*)src->dmem;
+    uint8_t* to = (uint8_t*)dst->dmem;
+    auto rebase = [&](auto& ptr) {
+        if (ptr) ptr = reinterpret_cast<std::remove_reference_t<decltype(ptr)>>(to + ((const uint8_t*)ptr - from));
+    };
+    DevScene& S = dst->S;
+    rebase(S.dsph); rebase(S.gsph); rebase(S.tri); rebase(S.cube); rebase(S.plane); rebase(S.cubetri);
+    rebase(S.shapes); rebase(S.mats); rebase(S.lights); rebase(S.bvh_nodes); rebase(S.bvh_leaves);
+    rebase(S.graze_blk); rebase(S.graze_tri); rebase(S.graze_pn); rebase(S.graze_mask); rebase(S.scan_ops);
+    const bool new_lights = dst->n_point_lights != src->n_point_lights;
+    dst->flops_per_scan = src->flops_per_scan;
+    dst->normal_max = src->normal_max;
+    dst->n_point_lights = src->n_point_lights;
+    dst->d_mats = src->d_mats;
+    dst->d_shapes = src->d_shapes;
+    dst->d_lights = src->d_lights;
+    dst->d_ambient = src->d_ambient;
+    // deeper ray trees may need a larger pool than any pass checked so far: check again
+    dst->checked_items = 0;
+    dst->checked_depth = 0;
+    if (new_lights) free_workspace(dst->ws);  // the shadow queue and the node-index limit follow the lights
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+rt_status rt_scene_layout_digest(const rt_scene_desc* d, const char* tuning, uint64_t* digest, uint64_t* bytes) {
+    if (!d || !digest) return RT_ERR_INVALID_ARG;
+    Tune tn;
+    if (!tune_apply(tn, std::getenv("RT_TUNE"), true) || !tune_apply(tn, tuning, true)) return RT_ERR_INVALID_ARG;
+    HostScene H;
+    rt_status st = prepare_scene(d, tn, H);
+    if (st != RT_OK) return st;
+    // FNV-1a over the image the device allocation would hold (padding as zeros)
+    uint64_t h = 0xcbf29ce484222325ull;
+    auto mix = [&](const uint8_t* p, size_t n) {
+        for (size_t i = 0; i < n; i++) h = (h ^ p[i]) * 0x100000001b3ull;
+    };
+    size_t at = 0;
+    const uint8_t z[256] = {0};
+    for (const auto& s : H.secs) {
+        for (; at < s.off; at += std::min<size_t>(256, s.off - at)) mix(z, std::min<size_t>(256, s.off - at));
+        for (int p = 0; p < 3; p++) mix((const uint8_t*)s.src[p], s.bytes[p]);
+        at += s.size();
+    }
+    for (; at < H.total; at += std::min<size_t>(256, H.total - at)) mix(z, std::min<size_t>(256, H.total - at));
+    const uint64_t tail[4] = {H.flops, H.n_point, (uint64_t)H.normals_ok, (uint64_t)H.lbuf.tiers};
+    mix((const uint8_t*)tail, sizeof(tail));
+    *digest = h;
+    if (bytes) *bytes = H.total;
     return RT_OK;
 }
 
@@ -2150,6 +2448,10 @@ static rt_status render_bands_impl(const rt_scene* scene, const rt_camera* cams,
                            std::min<uint32_t>(spp, RT_MAX_FRAMES);
     const bool checked = !s->tune.node_cap && (items > s->checked_items || depth > s->checked_depth);
     if (checked) {
+        // the check waits on the host: never inside a stream capture (rt_api.h "HOST WAIT")
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        HIP_TRY(hipStreamIsCapturing(hs, &cap));
+        if (cap != hipStreamCaptureStatusNone) return RT_ERR_UNSUPPORTED;
         HIP_TRY(hipStreamSynchronize(hs));
         for (auto& se : s->ev_streams) HIP_TRY(hipEventSynchronize(se.second));
         if (s->ws.overflow) {  // an earlier pass's unreported overflow stays reported
@@ -2428,6 +2730,10 @@ rt_status rt_scene_clone(const rt_scene* src, int32_t device, rt_scene** out) {
     sc->num_cus = g_num_cus(sc->device);
     sc->count_ops = src->count_ops;
     sc->tune = src->tune;
+    sc->d_mats = src->d_mats;
+    sc->d_shapes = src->d_shapes;
+    sc->d_lights = src->d_lights;
+    sc->d_ambient = src->d_ambient;
     *out = sc.release();
     return RT_OK;
 }
@@ -2829,6 +3135,58 @@ rt_status rt_scene_set_material(rt_scene* s, uint32_t index, const rt_material* 
         if (e != RT_OK) return e;
     }
     if (s->multi) return rt_multi_each(s->multi, [&](rt_scene* c) { return rt_scene_set_material(c, index, m); });
+    s->d_mats[index] = *m;
+    return RT_OK;
+}
+
+rt_status rt_scene_update(rt_scene* s, const rt_scene_desc* d, int32_t* what) {
+    if (what) *what = 0;
+    if (!s || !d) return RT_ERR_INVALID_ARG;
+    if ((d->n_materials && !d->materials) || (d->n_shapes && !d->shapes) || (d->n_lights && !d->lights))
+        return RT_ERR_INVALID_ARG;
+    auto same = [](const void* a, const void* b, size_t n) { return n == 0 || std::memcmp(a, b, n) == 0; };
+    const bool geometry = d->n_shapes == s->d_shapes.size() && d->n_lights == s->d_lights.size() &&
+                          d->n_materials == s->d_mats.size() &&
+                          same(d->shapes, s->d_shapes.data(), d->n_shapes * sizeof(rt_shape)) &&
+                          same(d->lights, s->d_lights.data(), d->n_lights * sizeof(rt_light)) &&
+                          same(&d->ambient, &s->d_ambient, sizeof(rt_color));
+    if (geometry) {
+        // material edits of the same kind (the GUI's sliders, gui.rs:221-236) in place
+        std::vector<uint32_t> edits;
+        bool kinds = true;
+        for (uint32_t i = 0; i < d->n_materials; i++)
+            if (!same(&d->materials[i], &s->d_mats[i], sizeof(rt_material))) {
+                edits.push_back(i);
+                kinds = kinds && d->materials[i].kind == s->d_mats[i].kind;
+            }
+        if (edits.empty()) return RT_OK;
+        if (kinds) {
+            for (uint32_t i : edits) {
+                rt_status st = rt_scene_set_material(s, i, &d->materials[i]);
+                if (st != RT_OK) return st;
+            }
+            if (what) *what = 1;
+            return RT_OK;
+        }
+    }
+    // anything else: the scene is rebuilt (same device and tuning) and adopted in place, so the
+    // caller's handle, its stream, workspace and band shares stay valid.  A stream-ordered
+    // render's unreported status is returned first (the update is then not made).
+    rt_status st = rt_scene_sync_status(s);
+    if (st != RT_OK) return st;
+    if (s->multi) {
+        st = rt_multi_each(s->multi, [](rt_scene* c) { return rt_scene_sync_status(c); });
+        if (st != RT_OK) return st;
+    }
+    rt_scene* fresh = nullptr;
+    st = create_handle(d, s->device, s->tune, &fresh);
+    if (st != RT_OK) return st;
+    st = adopt_scene_data(s, fresh);
+    if (st == RT_OK && s->split) st = rt_multi_each(s->split, [&](rt_scene* c) { return adopt_scene_data(c, fresh); });
+    if (st == RT_OK && s->multi) st = rt_multi_each(s->multi, [&](rt_scene* c) { return adopt_scene_data(c, fresh); });
+    rt_scene_destroy(fresh);
+    if (st != RT_OK) return st;
+    if (what) *what = 2;
     return RT_OK;
 }
 

@@ -9,7 +9,7 @@
 // algorithms (~1 ulp apart), and the checkerboard texture (my_scene.rs:26-43) truncates
 // u * 20 / v * 10 to an integer, where one ulp can flip a texel.  So the device replays
 // fdlibm's evaluation: the same constants, the same argument reduction, the same operation
-// order.  tests/test_libmf.py checks host and device builds against the host's libm bit for
+// order.  tests/test_libm.py checks host and device builds against the host's libm bit for
 // bit (acosf over every float, atanf over every float, atan2f over every float class).
 //
 // Upstream: fdlibm's float translations by Ian Lance Taylor, Cygnus Support

@@ -47,7 +47,7 @@ bool apply_one(Tune& t, const std::string& k, const std::string& v, bool build) 
     // ---- scene build
     if (k == "bvh" || k == "graze_k" || k == "graze_res" || k == "graze_lane" || k == "lb_res" || k == "lb_reach" ||
         k == "shape_buf" || k == "bvh_tris" || k == "dark_skip" || k == "bvh_cnode" || k == "bvh_maxleaf" ||
-        k == "force_rccl" || k == "lb_tiers" || k == "lb_dmax_k" || k == "lb_near_all") {
+        k == "force_rccl" || k == "lb_tiers" || k == "lb_dmax_k" || k == "lb_near_all" || k == "build_threads") {
         if (!build) return false;
         if (k == "bvh") return set_int(v, 0, 1, t.bvh);
         if (k == "graze_k") return parse_real(v, 1e-6, 1.0, &t.graze_k);
@@ -58,6 +58,7 @@ bool apply_one(Tune& t, const std::string& k, const std::string& v, bool build) 
         if (k == "lb_tiers") return set_int(v, 1, 7, t.lb_tiers);
         if (k == "lb_dmax_k") return parse_real(v, 1.0, 100.0, &t.lb_dmax_k);
         if (k == "lb_near_all") return set_int(v, 0, 1, t.lb_near_all);
+        if (k == "build_threads") return set_int(v, 0, 256, t.build_threads);
         if (k == "shape_buf") return set_int(v, 0, 1, t.shape_buf);
         if (k == "bvh_tris") return set_int(v, 0, 1, t.bvh_tris);
         if (k == "dark_skip") return set_int(v, 0, 1, t.dark_skip);

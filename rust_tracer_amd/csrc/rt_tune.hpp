@@ -33,6 +33,7 @@ struct Tune {
     double bvh_cnode = 400.0; // SAH node cost
     int bvh_maxleaf = 16;     // primitives per leaf at most (32 until round 4: K = 20 +0.9%, K = 64 flat)
     int force_rccl = 0;       // rt_scene_create_multi with one device: a one-rank communicator
+    int build_threads = 0;    // host threads of the scene build (0: the CPUs the process may use, at most 32)
     // ---- per pass
     int sort_tasks = 1;       // order the trace queues spatially
     int sort_shadow = 1;      // order the shadow queue

@@ -174,3 +174,28 @@ def test_tuning_strings_are_validated_on_the_host():
                  b"force_rccl=1,node_cap=4096", b"graze_k=3e-3,bvh_cnode=200,bvh_maxleaf=16",
                  b"lb_tiers=1", b"lb_tiers=7,lb_res=32", b"lb_dmax_k=2.01"):
         assert L.rt_scene_create_tuned(desc.ptr(), 0, good, C.byref(h)) == abi.RT_ERR_NO_DEVICE, good
+
+
+def _layout_digest(desc, tuning):
+    dg, nb = C.c_uint64(), C.c_uint64()
+    st = abi.lib().rt_scene_layout_digest(desc.ptr(), tuning.encode(), C.byref(dg), C.byref(nb))
+    assert st == 0, st
+    return dg.value, nb.value
+
+
+@pytest.mark.parametrize("which", ["my_scene", "config3", "stress"])
+def test_scene_build_is_deterministic_over_host_threads(which):
+    """rt_scene_create's host build (hierarchy, light-buffer tiers built by several host
+    threads, shape buffers) produces the same device image for any thread count
+    (rt_scene_layout_digest: the host half alone, no GPU)."""
+    if which == "my_scene":
+        desc = rt.SceneDesc.my_scene()
+    elif which == "config3":
+        desc = rt.SceneDesc.synth_config(3)
+    else:
+        from tests.test_gpu_cull_stress import stress_scene
+        desc = stress_scene(13, 1000.0, False, True)
+    one = _layout_digest(desc, "build_threads=1")
+    assert one == _layout_digest(desc, "build_threads=5")
+    assert one == _layout_digest(desc, "")
+    assert one[1] > 0

@@ -123,10 +123,12 @@ def test_hierarchy_is_exact_under_stress(seed, scale, cam_mode, near, slivers, m
     assert cnt["node_rays"] > w * h // 4  # the scene is in view
 
 
-@pytest.mark.parametrize("seed,scale,cam_mode,near,slivers", CASES[:4] + CASES[6:7])
+@pytest.mark.parametrize("seed,scale,cam_mode,near,slivers", CASES)
 def test_stress_scenes_match_oracle(seed, scale, cam_mode, near, slivers):
+    """Every stress scene at the hierarchy test's size (160x120, depth 6) against the oracle:
+    the culling hierarchy, light-buffer tiers, shape buffers and grazing pass together."""
     desc = stress_scene(seed, scale, near, slivers)
-    w, h, depth = 48, 36, 6
+    w, h, depth = 160, 120, 6
     cam = stress_camera(w, h, scale, cam_mode)
     s = DeviceScene(desc, device=0)
     img, cnt, _, _ = s.render(w, h, depth, cam=cam)
@@ -134,9 +136,12 @@ def test_stress_scenes_match_oracle(seed, scale, cam_mode, near, slivers):
     ref, rcnt = OracleScene(desc).render(w, h, depth, cam=cam, threads=8)
     assert cnt == rcnt
     diff = np.abs(img.astype(np.float64) - ref.astype(np.float64))
-    diff[np.isnan(img) & np.isnan(ref)] = 0.0
+    both_nan = np.isnan(img) & np.isnan(ref)
+    diff[both_nan] = 0.0
     assert not np.isnan(diff).any()
     assert float(diff.max()) <= 1e-4  # north_star: every RGB channel within 1e-4
+    differ = ~((img.view(np.uint32) == ref.view(np.uint32)) | both_nan)
+    print(f"stress {seed}: max |diff| {float(diff.max()):.3g}, channels differing {int(differ.sum())}")
 
 
 @pytest.mark.parametrize("case", [None] + CASES[:3] + CASES[4:5])

@@ -1,12 +1,14 @@
 """Whole-frame parity at the benchmark configs: the HIP path through the C ABI against the
-CPU oracle on EVERY pixel (configs 2 and 3) or every 4th row (config 4), not a row sample.
+CPU oracle on EVERY pixel (configs 2, 3 and 4), not a row sample.
 
 Reference semantics pinned: render.rs:31-103 (pixel loop, Whitted recursion),
 scene/mod.rs:98-116 (nearest hit in insertion order), scene/mod.rs:189-206 (shadow rays).
 Tolerance (north_star): |gpu - oracle| <= 1e-4 per RGB channel; NaN where and only where the
 oracle has NaN.  For whole frames the ray counters (node rays, shadow rays, pixels) must also
-be equal: equal counters mean the ray trees are identical.  The assertion messages report
-max |diff| and the bit-exact share of channels.
+be equal: equal counters mean the ray trees are identical.  The path delivers more than the
+tolerance: every channel bit-identical to the oracle (NaN where the oracle has NaN), and
+that is asserted -- a regression that moved one channel by one ulp fails.  The messages
+report max |diff| and the number of differing channels.
 
 The oracle runs over the host CPUs this process may use (the GPU box grants 16 CPUs of time:
 ~10 s per 1080p depth-8 frame).
@@ -36,16 +38,18 @@ def host_threads():
 
 
 def report(gpu, ref):
+    """(max |diff|, channels that differ, NaN pattern equal, message).  A channel differs
+    unless its bits are equal or it is NaN in both frames."""
     g, r = gpu.astype(np.float64), ref.astype(np.float64)
     nan_g, nan_r = np.isnan(gpu), np.isnan(ref)
-    same = gpu.view(np.uint32) == ref.view(np.uint32)
+    same = (gpu.view(np.uint32) == ref.view(np.uint32)) | (nan_g & nan_r)
     d = np.abs(g - r)
-    d[same | (nan_g & nan_r)] = 0.0          # equal infinities, NaN in both
+    d[same] = 0.0          # equal infinities, NaN in both
     worst = float(np.nanmax(d)) if d.size else 0.0
-    exact = float(np.mean(same))
-    msg = (f"max |diff| {worst:.3g} (tol {TOL}), bit-exact channels {exact:.6f}, "
-           f"NaN pattern equal {bool(np.array_equal(nan_g, nan_r))}")
-    return worst, exact, bool(np.array_equal(nan_g, nan_r)), msg
+    mismatches = int(np.count_nonzero(~same))
+    msg = (f"max |diff| {worst:.3g} (tol {TOL}), channels differing from the oracle {mismatches} "
+           f"of {same.size}, NaN pattern equal {bool(np.array_equal(nan_g, nan_r))}")
+    return worst, mismatches, bool(np.array_equal(nan_g, nan_r)), msg
 
 
 @pytest.mark.parametrize("config,depth", [(3, 8), (2, 4)])
@@ -57,29 +61,32 @@ def test_benchmark_frame_every_pixel(config, depth):
     img, cnt, _, _ = s.render(1920, 1080, depth)
     s.close()
     ref, rcnt = OracleScene(desc).render(1920, 1080, depth, threads=host_threads())
-    worst, exact, nan_ok, msg = report(img, ref)
+    worst, mismatches, nan_ok, msg = report(img, ref)
     print(f"config {config}: {msg}; counters {cnt}")
     assert nan_ok, msg
     assert worst <= TOL, msg
-    assert exact > 0.99, msg
+    # the path is bit-exact (every channel equal to the oracle's): the 1e-4 tolerance of
+    # north_star is the contract, bit equality is what this build delivers and guards
+    assert mismatches == 0, msg
     assert cnt == rcnt, (cnt, rcnt)
 
 
-def test_config4_every_fourth_row():
-    """Config 4 (3840x2160, depth 8): every 4th row (2.07 M pixels) against the oracle."""
+def test_config4_every_pixel():
+    """Config 4 (3840x2160, depth 8): every pixel (8.3 M) against the oracle, counters equal."""
     desc = SceneDesc.synth_config(4)
     s = DeviceScene(desc, device=0)
     img, cnt, _, _ = s.render(3840, 2160, 8)
     s.close()
     assert cnt["pixels"] == 3840 * 2160
-    rows = np.arange(1, 2160, 4)
-    ref, rcnt = OracleScene(desc).render(3840, 2160, 8, rows=(1, 2160, 4), threads=host_threads())
-    worst, exact, nan_ok, msg = report(img[rows], ref[rows])
-    print(f"config 4 (every 4th row): {msg}")
-    assert rcnt["pixels"] == len(rows) * 3840
+    ref, rcnt = OracleScene(desc).render(3840, 2160, 8, threads=host_threads())
+    worst, mismatches, nan_ok, msg = report(img, ref)
+    print(f"config 4 (every pixel): {msg}; counters {cnt}")
+    assert cnt == rcnt, (cnt, rcnt)
     assert nan_ok, msg
     assert worst <= TOL, msg
-    assert exact > 0.99, msg
+    # the path is bit-exact (every channel equal to the oracle's): the 1e-4 tolerance of
+    # north_star is the contract, bit equality is what this build delivers and guards
+    assert mismatches == 0, msg
 
 
 def test_textured_spheres_every_pixel():
@@ -100,9 +107,11 @@ def test_textured_spheres_every_pixel():
     img, cnt, _, _ = s.render(1920, 1080, 8)
     s.close()
     ref, rcnt = OracleScene(desc).render(1920, 1080, 8, threads=host_threads())
-    worst, exact, nan_ok, msg = report(img, ref)
+    worst, mismatches, nan_ok, msg = report(img, ref)
     print(f"textured config 3 ({len(spheres[::5])} textured spheres): {msg}; counters {cnt}")
     assert nan_ok, msg
     assert worst <= TOL, msg
-    assert exact > 0.99, msg
+    # the path is bit-exact (every channel equal to the oracle's): the 1e-4 tolerance of
+    # north_star is the contract, bit equality is what this build delivers and guards
+    assert mismatches == 0, msg
     assert cnt == rcnt, (cnt, rcnt)
