@@ -57,7 +57,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     # K = 64 timed frames by default: every slot runs a pass of 16 frames (K = 20 is one pass
     # of 5 per slot: 1051 - 1062 Mpixels/s; 2 passes of 8 per slot at K = 64: 1077 - 1095;
-    # tools/r3_steps.sh, tools/r3_steps2.sh)
+    # round-3 A/B run r3_steps, profiles/r3ab/, round-3 A/B run r3_steps2, profiles/r3ab/)
     p.add_argument("--steps", type=int, default=64)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--config", type=int, default=3, help="BASELINE config (2..5 synth scenes)")
@@ -401,10 +401,14 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    from rust_tracer_amd import DeviceScene, SceneDesc, band_rows_per_rank
+    import ctypes as C
+    from rust_tracer_amd import DeviceScene, SceneDesc, abi, band_rows_per_rank
     from rust_tracer_amd.dist import FramePipeline
 
     desc = SceneDesc.synth_config(args.config)
+    _d = desc.ptr().contents
+    scene_soa_bytes = (_d.n_shapes * C.sizeof(abi.rt_shape) + _d.n_materials * C.sizeof(abi.rt_material)
+                       + _d.n_lights * C.sizeof(abi.rt_light))
     torch.cuda.synchronize()
     t_sc = time.perf_counter()
     scene = DeviceScene(desc, device=dev.index)   # host build (hierarchy, light buffers) + upload
@@ -412,8 +416,8 @@ def main():
     # 4 passes in flight.  A short burst at N >= 4 (fewer than 8 frames per slot) takes 3, so
     # that each pass is bigger: a rank's share of a frame is small there and bigger passes
     # amortise each level's fixed latency (one rank's share on one MI355X, K = 20,
-    # tools/r3_share2.sh: N = 8: 3 x 7 0.310 vs 4 x 5 0.326 ms per share-frame, N = 4: 0.543 vs
-    # 0.554).  With 16 frames per slot 4 x 16 wins at every N (K = 64, tools/r3_share5.sh:
+    # round-3 A/B run r3_share2, profiles/r3ab/: N = 8: 3 x 7 0.310 vs 4 x 5 0.326 ms per share-frame, N = 4: 0.543 vs
+    # 0.554).  With 16 frames per slot 4 x 16 wins at every N (K = 64, round-3 A/B run r3_share5, profiles/r3ab/:
     # N = 8: 0.251 vs 0.270 for 3 x 11, N = 4: 0.487 vs 0.508)
     inflight = max(1, args.inflight or (3 if world >= 4 and -(-args.steps // 4) < 8 else 4))
     if args.sub_bands is None:
@@ -451,7 +455,7 @@ def main():
             cap = 1
         else:  # up to 32 frames (RT_MAX_FRAMES), within 16 x 1080p of pixels per pass and rank
             # (~37 GB of workspace per slot, ~150 GB for 4 slots of the 288 GB): at K = 64, 4 x 16
-            # 1118 - 1126 vs 4 x 8 1077 - 1084 Mpixels/s (tools/r3_steps2.sh).  Passes in flight
+            # 1118 - 1126 vs 4 x 8 1077 - 1084 Mpixels/s (round-3 A/B run r3_steps2, profiles/r3ab/).  Passes in flight
             # come first: at K = 20 bigger passes lost (4 x 5: 1027 / 1033, 3 x 7: 1018 / 1017,
             # 2 x 10: 750, 1 x 16: 796)
             from rust_tracer_amd import abi as _abi1
@@ -648,7 +652,13 @@ def main():
             # exclusive per-kernel times (one frame at a time, nothing overlapping) of the profile
             "exclusive_kernel_ms_per_frame": traffic.get("exclusive_kernel_ms_per_frame") if traffic else None,
             "hbm": {
-                "algorithmic_bytes_per_launch": args.spp * (scene.device_bytes + args.width * args.height * 12 / world),
+                # B_alg = S_scene + W H 12 / world per launch (the float frame; S_scene
+                # = the reference scene's own records: shapes, materials, lights as the C ABI
+                # describes them), once per sample; the device scene's acceleration data (hierarchy,
+                # light-buffer and shape-buffer record copies) is the builder's, reported apart
+                "algorithmic_bytes_per_launch": round(args.spp * (scene_soa_bytes + args.width * args.height * 12 / world)),
+                "scene_soa_bytes": scene_soa_bytes,
+                "accel_bytes": scene.device_bytes,
                 "achieved_GBps": round((traffic["bytes_per_launch"] / (kernel_ms / 1e3) / 1e9), 3)
                 if traffic else None,
                 "peak_GBps": PEAK_HBM_GBPS,

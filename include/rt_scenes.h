@@ -45,8 +45,8 @@ void rt_desc_free(rt_scene_desc* desc);
  * render_scene_basic main.rs:244-261) through the drop-in seam, whose Scene keeps its device
  * scene across calls.  scene: 0 = my_scene.rs, 2 .. 5 = rt_synth_config(scene).  edit,
  * applied before the last call (n_calls >= 2): 0 none; 1 set_transform of the first sphere
- * (find_shape_mut, translated 0.1 in x); 2 the first shape's material's reflectivity + 0.05
- * (an Rc<RefCell<Material>> edit); 3 a point light added.  Out: ms[i] = wall time of call i
+ * (find_shape_mut, translated 0.1 in x); 2 the first shape's material's diffuse colour set to
+ * (0.25, 0.5, 0.75) (an Rc<RefCell<Material>> edit); 3 a point light added.  Out: ms[i] = wall time of call i
  * (the frame's device-to-host copy included), updates[i] = what render() did to the device
  * scene (-1 created, 0 reused, 1 materials edited in place, 2 rebuilt); rgb (optional,
  * x_res * y_res * 3 floats) = the last call's frame; rgb_fresh (optional) = the same edited

@@ -505,7 +505,9 @@ rt_status rt_mirror_render_calls(int32_t scene_id, uint32_t x_res, uint32_t y_re
                 if (!s) return RT_ERR_INVALID_ARG;
                 s->set_transform(Matrix::translate(0.1f, 0.f, 0.f) * s->transform);
             } else if (edit == 2) {
-                scene.shapes().front().material->reflectivity += 0.05f;
+                // (reflectivity is only a switch in trace_ray, render.rs:70: the diffuse colour
+                // changes the lights' and refracted terms)
+                scene.shapes().front().material->diffuse = Texture::constant(Color(0.25f, 0.5f, 0.75f));
             } else {
                 scene.add_light(PointLight(Point3(-3.f, 5.f, -6.f), Color(0.3f, 0.3f, 0.3f)));
             }

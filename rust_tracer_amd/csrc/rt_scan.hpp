@@ -25,7 +25,7 @@
 #define RT_STATS 0
 #endif
 #if RT_STATS
-__device__ unsigned long long rt_scan_stats[32];
+__device__ unsigned long long rt_scan_stats[40];
 #define RT_STAT(i) do { if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == \
     (uint32_t)__builtin_ctzll(__ballot(1))) atomicAdd(&rt_scan_stats[i], 1ull); } while (0)
 #else
@@ -574,6 +574,42 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
         rt_far_class = __ballot(q > 12.f) ? 2u : (__ballot(q > 3.f) ? 1u : 0u);
     }
 #endif
+#if RT_STATS
+    // leaf-major planning (DESIGN.md "Leaf-major trace pass"): the leaves a trace ray's own
+    // box tests admit with no nearest-hit bound during the walk (its bound at the start:
+    // infinite, or the enclosing sphere's exit) -- slot 32, rays in slot 33 -- and, after the
+    // walk, with its final nearest hit as the bound -- slot 34
+    auto lane_leaves = [&](float tb) {
+        uint32_t lst[48];
+        int lsp = 0;
+        uint32_t c = S.bvh_root, nl = 0;
+        const float tn = tb < 0.f ? -__builtin_huge_valf() : tb + R.m;
+        for (;;) {
+            if (c & BVH_LEAF) {
+                nl++;
+            } else {
+                cfloat4* q = cptr(S.bvh_nodes) + 4 * c;
+                bool a, b;
+                node_test(q[0], q[1], q[2], R, tn, a, b);
+                const uint32_t ca = __float_as_uint(q[3].x), cb = __float_as_uint(q[3].y);
+                if (a && b && lsp < 48) {
+                    lst[lsp++] = cb;
+                    c = ca;
+                    continue;
+                }
+                if (a) { c = ca; continue; }
+                if (b) { c = cb; continue; }
+            }
+            if (lsp == 0) break;
+            c = lst[--lsp];
+        }
+        return nl;
+    };
+    if (!SHADOW && !novote) {
+        atomicAdd(&rt_scan_stats[32], (unsigned long long)lane_leaves(bt));
+        atomicAdd(&rt_scan_stats[33], 1ull);
+    }
+#endif
     uint32_t* stk = rt_bvh_stack + ((threadIdx.x >> 6) << 5);
     uint32_t sp = 0;
     uint32_t cur = S.bvh_root;
@@ -657,6 +693,9 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
         RT_NEED(need = nstk[sp - 1];)
         cur = rfl(stk[--sp]);
     }
+#if RT_STATS
+    if (!SHADOW && !novote) atomicAdd(&rt_scan_stats[34], (unsigned long long)lane_leaves(bt));
+#endif
 }
 
 // cube-map cell of a direction (face = largest |component|, ties x > y > z); the host

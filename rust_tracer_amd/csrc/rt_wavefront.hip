@@ -1259,11 +1259,11 @@ hipError_t launch_wave_combine(const WaveParams& p, uint32_t level, int blocks, 
 
 #if RT_STATS
 // tools/scan_stats.py: read (and optionally reset) the wavefront pipeline's scan counters
-extern "C" int rt_debug_scan_stats(unsigned long long* out32, int reset) {
-    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(rtdev::rt_scan_stats), 32 * sizeof(unsigned long long)) != hipSuccess)
+extern "C" int rt_debug_scan_stats(unsigned long long* out40, int reset) {
+    if (hipMemcpyFromSymbol(out40, HIP_SYMBOL(rtdev::rt_scan_stats), 40 * sizeof(unsigned long long)) != hipSuccess)
         return 1;
     if (reset) {
-        unsigned long long z[32] = {};
+        unsigned long long z[40] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(rtdev::rt_scan_stats), z, sizeof(z)) != hipSuccess) return 1;
     }
     return 0;

@@ -62,6 +62,24 @@ def test_multi_device_scene_equals_single(devices):
     assert ms > 0
 
 
+def test_multi_device_eight_ranks_config4():
+    """The N = 8 band layout behind the drop-in seam: rt_scene_create_multi with devices =
+    [0] * 8 (eight band shares of one GPU, exchanged by device copies) renders the whole
+    config 4 frame (3840x2160, depth 8) bit-identical to the one-device rt_render, counters
+    equal -- the driver's 8-GPU run deals the same bands to eight devices (render.rs:32-37
+    tiled)."""
+    desc = SceneDesc.synth_config(4)
+    single = DeviceScene(desc, device=0)
+    ref, rcnt, _, _ = single.render(3840, 2160, 8)
+    single.close()
+    multi = DeviceScene(desc, devices=[0] * 8)
+    assert multi.device_count == 8
+    img, cnt, _, _ = multi.render(3840, 2160, 8)
+    multi.close()
+    assert same_bits(img, ref)
+    assert cnt == rcnt
+
+
 @pytest.mark.parametrize("w,h", [(320, 180), (3840, 2160)])
 def test_forced_rccl_one_rank(monkeypatch, w, h):
     """Tuning force_rccl=1 (RT_TUNE) with devices=[0]: rt_scene_create_multi builds a one-rank RCCL

@@ -12,7 +12,7 @@ cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 L = abi.lib()
 L.rt_debug_scan_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 s = DeviceScene(SceneDesc.synth_config(cfg))
-st = (C.c_ulonglong * 32)()
+st = (C.c_ulonglong * 40)()
 for depth in (1, 2, 8):
     L.rt_debug_scan_stats(st, 1)
     _, cnt, ms, _ = s.render(1920, 1080, depth)
@@ -31,5 +31,8 @@ for depth in (1, 2, 8):
           f"(12,25] (25,50] (50,inf): {v[16:22]}; light farther than 45: {v[22]}")
     print(f"  trace walks' lanes by D / R (same buckets): {v[23:29]}; leaf visits of trace waves whose farthest "
           f"lane is within 3 R / 12 R / beyond: {v[29:32]}")
+    print(f"  leaf-major planning (trace rays): leaves a ray's own box tests admit with no nearest-hit bound "
+          f"{v[32] / max(1, v[33]):.2f} per ray, with its final nearest hit as the bound {v[34] / max(1, v[33]):.2f} "
+          f"({v[33]} walks)")
     print(f"  hit paths per wave scan: dsph {v[1] / max(1, v[0]):.2f} gsph {v[2] / max(1, v[0]):.2f} "
           f"tri {v[3] / max(1, v[0]):.2f} cube-tri {v[4] / max(1, v[0]):.2f}")

@@ -14,7 +14,7 @@ L = abi.lib()
 L.rt_debug_scan_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 s = DeviceScene(SceneDesc.synth_config(cfg))
 s.render(1920, 1080, 1)
-st = (C.c_ulonglong * 32)()
+st = (C.c_ulonglong * 40)()
 L.rt_debug_scan_stats(st, 1)
 prev = [0] * 16
 prev_scans = 0
