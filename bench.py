@@ -314,6 +314,17 @@ def seam_stats(args, scene, pipe, tiler, dev):
     c = scene.clone(dev.index)
     out["scene_clone_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
     c.close()
+    # rt_scene_create again, the process's HIP runtime warm (the headline's scene_create_ms is
+    # the process's first, with the runtime's first allocations and stream in it)
+    from rust_tracer_amd import DeviceScene as _DS, SceneDesc as _SD
+    _desc = _SD.synth_config(args.config)
+    walls = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        _s = _DS(_desc, device=dev.index)
+        walls.append((time.perf_counter() - t0) * 1e3)
+        _s.close()
+    out["scene_create_warm_ms"] = round(min(walls), 2)
     if pipe.inflight > 1:
         scene.set_grid_share(pipe.grid_share)
     if args.spp == 1:
