@@ -615,6 +615,7 @@ struct LbJob {
         uint32_t code;
         int prev_same;  // the previous cone (nearest-first order) of the same record, or -1
         uint8_t faces;  // the cube-map faces the cone may meet
+        bool all;       // its record is in the tier's all-cell leaf instead of cell lists
     };
     std::vector<Cone> cones;
     struct Ent {
@@ -625,6 +626,12 @@ struct LbJob {
     std::vector<uint32_t> cell_start;  // [nc + 1] into `ent` (entries grouped by cell)
     std::vector<Ent> ent;
     std::vector<uint32_t> cell_first;  // [4 nc]: per cell and type its first copy (job-relative)
+    // the tier's all-cell leaf: every record one of whose cones covers every direction (its
+    // grown ball within LB_RHO of the light), once, nearest first -- instead of a copy in each
+    // of the 6 res^2 cells
+    std::vector<Ent> all_ent;
+    size_t all_first[4] = {0, 0, 0, 0};  // its first copy per type (job-relative)
+    uint32_t cell_leaf = 0, all_leaf = 0;  // leaf indices: the tier's first cell, the all-cell leaf
     size_t count[4] = {0, 0, 0, 0};  // copies per record type
     size_t first[4] = {0, 0, 0, 0};  // the job's first copy in each run array
 };
@@ -740,13 +747,16 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
         if (next_leaf >= (1u << 28)) continue;  // (the tier count sits in LightRec::lb_base's top bits)
         B.base[li] = next_leaf | ((uint32_t)tiers << 28);
         B.tiers = std::max(B.tiers, (uint32_t)tiers);
-        next_leaf += (uint32_t)(tiers * nc);
+        // a light's leaves: tier 0's cells, tier 1's, ..., then one all-cell leaf per tier
         for (int t = 0; t < tiers; t++) {
             LbJob jb;
             jb.li = (uint32_t)li;
             jb.tier = t;
+            jb.cell_leaf = next_leaf + (uint32_t)(t * nc);
+            jb.all_leaf = next_leaf + (uint32_t)(tiers * nc + t);
             jobs.push_back(std::move(jb));
         }
+        next_leaf += (uint32_t)(tiers * nc + tiers);
     }
     if (jobs.empty()) return;
     const int threads = build_thread_count(T);
@@ -775,6 +785,7 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
             c.code = p.code;
             c.prev_same = -1;
             c.faces = 0;
+            c.all = false;
             for (int f = 0; f < 6; f++) {  // the angle to the face's axis
                 const int k = f >> 1;
                 const double sg = (f & 1) ? -1.0 : 1.0;
@@ -791,6 +802,16 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
         std::sort(byc.begin(), byc.end());
         for (size_t i = 1; i < byc.size(); i++)
             if (byc[i].first == byc[i - 1].first) cones[byc[i].second].prev_same = byc[i - 1].second;
+        // records with a cone over every direction: into the all-cell leaf (every cone of the
+        // record leaves the cell lists), nearest first, at the record's nearest distance
+        for (size_t lo = 0, hi; lo < byc.size(); lo = hi) {
+            bool all = false;
+            for (hi = lo; hi < byc.size() && byc[hi].first == byc[lo].first; hi++) all = all || cones[byc[hi].second].alpha >= PI;
+            if (all)
+                for (size_t i = lo; i < hi; i++) cones[byc[i].second].all = true;
+        }
+        for (const LbJob::Cone& c : cones)  // nearest first: a record's first cone is its nearest
+            if (c.all && c.prev_same < 0) jb.all_ent.push_back(LbJob::Ent{c.code, reach_cut ? down_f(c.near) : 0.f});
     });
     // (2) per job and chunk of cones: the (cell, entry) pairs in cone order
     const int CONE_CHUNK = 64;
@@ -813,6 +834,7 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
         const size_t c0 = (size_t)units[ui].second * CONE_CHUNK, c1 = std::min(cones.size(), c0 + CONE_CHUNK);
         for (size_t ci = c0; ci < c1; ci++) {
             const LbJob::Cone& c = cones[ci];
+            if (c.all) continue;  // listed once, in the all-cell leaf
             const LbJob::Ent en{c.code, reach_cut ? down_f(c.near) : 0.f};
             for (int f = 0; f < 6; f++) {
                 if (!(c.faces >> f & 1)) continue;
@@ -858,6 +880,8 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
             for (int k = 0; k < 4; k++) jb.cell_first[4 * cc + k] = (uint32_t)jb.count[k];
             for (uint32_t e = jb.cell_start[cc]; e < jb.cell_start[cc + 1]; e++) jb.count[jb.ent[e].code >> 30]++;
         }
+        for (int k = 0; k < 4; k++) jb.all_first[k] = jb.count[k];
+        for (const LbJob::Ent& e : jb.all_ent) jb.count[e.code >> 30]++;
     });
     // the copies' places: each job's copies follow the previous job's, per run array, after
     // the array's own records
@@ -874,34 +898,45 @@ void build_light_buffers(RunLayout& L, const std::vector<LightRec>& lights, Ligh
         L.ext[k].lb_floats = (n_rec[k] - n_src[k]) * RUN_WIDTH[k];
         L.ext[k].lb.reset(new float[std::max<size_t>(1, L.ext[k].lb_floats)]);
     }
-    const size_t leaf0 = L.leaves.size();
-    L.leaves.resize(leaf0 + jobs.size() * (size_t)nc * 8);
+    L.leaves.resize((size_t)next_leaf * 8);
     // per cell, per type nearest first; each copy carries its nearest distance to the light
     // (down-rounded) in the record's spare slot: the device stops a run at the first record
     // no undecided lane can reach
     const int CELL_CHUNK = 512;
     const int n_cell_chunks = (nc + CELL_CHUNK - 1) / CELL_CHUNK;
+    // a leaf's runs, copies at first[k] on (each entry's record, its nearest distance in the spare slot)
+    auto emit = [&](uint32_t* leaf, const LbJob::Ent* e0, const LbJob::Ent* e1, const size_t first[4]) {
+        for (int k = 0; k < 4; k++) {
+            const size_t w = RUN_WIDTH[k];
+            size_t at = first[k];
+            leaf[2 * k] = (uint32_t)at;
+            const float* src = run[k]->data();
+            float* dst = L.ext[k].lb.get() - n_src[k] * w;  // record index -> its place
+            for (const LbJob::Ent* e = e0; e < e1; e++) {
+                if ((int)(e->code >> 30) != k) continue;
+                const size_t r = e->code & 0x3FFFFFFFu;  // a hierarchy record (< n_src)
+                std::memcpy(dst + w * at, src + w * r, w * sizeof(float));
+                dst[w * at + spare[k]] = e->near;
+                at++;
+            }
+            leaf[2 * k + 1] = (uint32_t)at;
+        }
+    };
     parallel_jobs((int)jobs.size() * n_cell_chunks, threads, [&](int ui) {
         const int ji = ui / n_cell_chunks, c0 = (ui % n_cell_chunks) * CELL_CHUNK, c1 = std::min(nc, c0 + CELL_CHUNK);
         const LbJob& jb = jobs[ji];
-        uint32_t* leaf = L.leaves.data() + leaf0 + ((size_t)ji * nc + c0) * 8;
+        uint32_t* leaf = L.leaves.data() + ((size_t)jb.cell_leaf + c0) * 8;
         for (int cc = c0; cc < c1; cc++, leaf += 8) {
-            for (int k = 0; k < 4; k++) {
-                const size_t w = RUN_WIDTH[k];
-                size_t at = jb.first[k] + jb.cell_first[4 * cc + k];
-                leaf[2 * k] = (uint32_t)at;
-                const float* src = run[k]->data();
-                float* dst = L.ext[k].lb.get() - n_src[k] * w;  // record index -> its place
-                for (uint32_t e = jb.cell_start[cc]; e < jb.cell_start[cc + 1]; e++) {
-                    const LbJob::Ent& en = jb.ent[e];
-                    if ((int)(en.code >> 30) != k) continue;
-                    const size_t r = en.code & 0x3FFFFFFFu;  // a hierarchy record (< n_src)
-                    std::memcpy(dst + w * at, src + w * r, w * sizeof(float));
-                    dst[w * at + spare[k]] = en.near;
-                    at++;
-                }
-                leaf[2 * k + 1] = (uint32_t)at;
-            }
+            size_t first[4];
+            for (int k = 0; k < 4; k++) first[k] = jb.first[k] + jb.cell_first[4 * cc + k];
+            emit(leaf, jb.ent.data() + jb.cell_start[cc], jb.ent.data() + jb.cell_start[cc + 1], first);
+            // bit 31 of the first run's start: the tier's all-cell leaf has records (rt_scan.hpp lb_leaf)
+            if (!jb.all_ent.empty()) leaf[0] |= 0x80000000u;
+        }
+        if (c0 == 0) {
+            size_t first[4];
+            for (int k = 0; k < 4; k++) first[k] = jb.first[k] + jb.all_first[k];
+            emit(L.leaves.data() + (size_t)jb.all_leaf * 8, jb.all_ent.data(), jb.all_ent.data() + jb.all_ent.size(), first);
         }
     });
 }

@@ -995,11 +995,13 @@ __device__ __forceinline__ float wave_max(float x) {
 // nearest distance to the light exceeds `reach` (no undecided lane's origin is farther
 // from the light, so nothing from there on can shadow one; the record's spare slot
 // holds that distance).
+// A cell's leaf record carries in bit 31 of its first run start whether its tier has an
+// all-cell leaf (the records whose grown ball comes within LB_RHO of the light, listed once
+// for the tier instead of in every cell): that leaf's runs follow the cell's.
 template <class C>
-__device__ __forceinline__ void lb_leaf(const DevScene& S, uint32_t li, V3 o, V3 d, float on, float tmax,
+__device__ __forceinline__ void lb_runs(const DevScene& S, uint4 a, uint4 b, V3 o, V3 d, float on, float tmax,
                                         float reach, float& bt, uint32_t& bk, C& c) {
-    cuint4* lp = (cuint4*)S.bvh_leaves + 2 * li;
-    const uint4 a = lp[0], b = lp[1];
+    a.x &= 0x7FFFFFFFu;
     if (a.x < a.y) {
         cfloat4* p = cptr(S.dsph) + 4 * a.x;
         RT_PF_INIT(SphPair, ld_sph, p)
@@ -1042,15 +1044,29 @@ __device__ __forceinline__ void lb_leaf(const DevScene& S, uint32_t li, V3 o, V3
         }
     }
 }
-
 template <class C>
-__device__ __forceinline__ void lb_pass(const DevScene& S, uint32_t base, V3 o, V3 d, float on, float tlim, float l2,
-                                        bool lb, float& bt, uint32_t& bk, C& c) {
+__device__ __forceinline__ void lb_leaf(const DevScene& S, uint32_t li, uint32_t all_li, V3 o, V3 d, float on,
+                                        float tmax, float reach, float& bt, uint32_t& bk, C& c) {
+    cuint4* lp = (cuint4*)S.bvh_leaves + 2 * li;
+    const uint4 a = lp[0], b = lp[1];
+    lb_runs(S, a, b, o, d, on, tmax, reach, bt, bk, c);
+    if (a.x >> 31) {  // the tier's all-cell leaf
+        cuint4* ap = (cuint4*)S.bvh_leaves + 2 * all_li;
+        lb_runs(S, ap[0], ap[1], o, d, on, tmax, reach, bt, bk, c);
+    }
+}
+
+// base: the lane's tier's first cell; all_leaf: that tier's all-cell leaf
+template <class C>
+__device__ __forceinline__ void lb_pass(const DevScene& S, uint32_t base, uint32_t all_leaf, V3 o, V3 d, float on,
+                                        float tlim, float l2, bool lb, float& bt, uint32_t& bk, C& c) {
     const uint32_t leaf = lb ? base + lb_cell(S.lb_res, neg(d)) : 0u;
     bool want = lb && !shadow_decided(o, d, bt, l2);
     uint64_t pend;
     while ((pend = __ballot(want)) != 0) {
-        const uint32_t cur = (uint32_t)__builtin_amdgcn_readlane((int)leaf, (int)__builtin_ctzll(pend));
+        const int owner = (int)__builtin_ctzll(pend);
+        const uint32_t cur = (uint32_t)__builtin_amdgcn_readlane((int)leaf, owner);
+        const uint32_t cur_all = (uint32_t)__builtin_amdgcn_readlane((int)all_leaf, owner);
         want = want && leaf != cur;
         RT_T0(C, t_l);
         const bool dec = shadow_decided(o, d, bt, l2);
@@ -1058,7 +1074,7 @@ __device__ __forceinline__ void lb_pass(const DevScene& S, uint32_t base, V3 o, 
         // whose cell this is (the others test these records too, which changes nothing for
         // them: their own cell's complete list is their pass)
         const float reach = wave_max((dec || leaf != cur) ? 0.f : sqrtf(l2) * 1.001f + 1e-4f);
-        lb_leaf(S, cur, o, d, on, dec ? -1.f : fminf(bt, tlim), reach, bt, bk, c);  // decided lanes do not vote
+        lb_leaf(S, cur, cur_all, o, d, on, dec ? -1.f : fminf(bt, tlim), reach, bt, bk, c);  // decided lanes do not vote
         RT_T1(C, c, cyc_leaf, t_l);
         want = want && !shadow_decided(o, d, bt, l2);
     }
@@ -1100,9 +1116,13 @@ __device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lp
             const int tier = lb_tier(S, lb_base, o, l2);
             lb = tier >= 0;
             RT_T0(C, t_lb);
-            if (__ballot(lb))
-                lb_pass(S, (lb_base & 0x0FFFFFFFu) + (tier > 0 ? (uint32_t)tier * 6u * S.lb_res * S.lb_res : 0u), o, d,
+            if (__ballot(lb)) {
+                // a light's leaves: its tiers' cells, then one all-cell leaf per tier
+                const uint32_t nc = 6u * S.lb_res * S.lb_res, lb0 = lb_base & 0x0FFFFFFFu;
+                const uint32_t tiers = (lb_base >> 28) & 7u;
+                lb_pass(S, lb0 + (tier > 0 ? (uint32_t)tier * nc : 0u), lb0 + tiers * nc + (uint32_t)max(tier, 0), o, d,
                         on, tlim, l2, lb, bt, bk, c);
+            }
             if (SPLIT) RT_T1(C, c, cyc_post, t_lb);
         }
         RT_T0(C, t_w);
