@@ -31,7 +31,9 @@ struct Tune {
     int bvh_tris = 1;         // loose triangles in the hierarchy (0: linear)
     int dark_skip = 1;        // shadowed lights skipped in the combine where exact
     double bvh_cnode = 400.0; // SAH node cost
-    int bvh_maxleaf = 16;     // primitives per leaf at most (32 until round 4: K = 20 +0.9%, K = 64 flat)
+    int bvh_maxleaf = 6;      // primitives per leaf at most (32 until round 4: K = 20 +0.9%, K = 64 flat; 16 in
+                              // round 4; round 5, profiles/r5ab/: 6 vs 16 +1.9% at K = 20, +2.2% at K = 64;
+                              // 4 / 8 / 12: -1.5% / +1.6% / +0.9% at K = 20)
     int force_rccl = 0;       // rt_scene_create_multi with one device: a one-rank communicator
     int build_threads = 0;    // host threads of the scene build (0: the CPUs the process may use, at most 32)
     // ---- per pass
