@@ -17,7 +17,8 @@
 struct Tune {
     // ---- scene build (fixed for the handle's life)
     int bvh = 1;              // culling hierarchy (0: every shape in the linear pass)
-    double graze_k = 1e-3;    // grazing threshold sin(phi_T) = k / sin(alpha)
+    double graze_k = 5e-4;    // grazing threshold sin(phi_T) = k / sin(alpha) (1e-3 until round 5; with 6-primitive
+                              // leaves 3e-4 / 5e-4 / 7e-4 +0.8% / +0.6 - 0.9% / +1.0% at K = 20, 2e-3 -1.4%, profiles/r5ab/)
     int graze_res = 64;       // grazing direction cells per cube-map face side (0: cone path)
     int graze_lane = 1;       // per-lane grazing sets (0: the wave-union path)
     int lb_res = 48;          // light-buffer cells per face side (0: no light buffers)
