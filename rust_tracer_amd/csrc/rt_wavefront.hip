@@ -320,22 +320,33 @@ __device__ __forceinline__ void task_clock_mark(const WaveParams& P, uint32_t le
 
 // wave-aggregated append of `n` (< 64) consecutive slots per lane to a device counter:
 // one atomic per wave, slots in lane order
-__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, uint32_t n, uint32_t lane) {
-    uint32_t total = 0, mine = 0;
+// ... split in two: the atomic is issued by wave_append_begin and its value read by
+// wave_append_end, so that work in between overlaps its round trip (a returning append
+// costs ~1.8% of the frame when waited for at once: RT_EXTRA_ATOMIC)
+struct AppendTicket {
+    uint32_t mine, base, first, total;
+};
+__device__ __forceinline__ AppendTicket wave_append_begin(uint32_t* counter, uint32_t n, uint32_t lane) {
+    AppendTicket t{0u, 0u, 0u, 0u};
     uint64_t lt = lanemask_lt();
     for (int b = 0; b < 6; b++) {
         uint64_t m = __ballot((n >> b) & 1u);
-        total += (uint32_t)__builtin_popcountll(m) << b;
-        mine += (uint32_t)__builtin_popcountll(m & lt) << b;
+        t.total += (uint32_t)__builtin_popcountll(m) << b;
+        t.mine += (uint32_t)__builtin_popcountll(m & lt) << b;
     }
-    uint32_t base = 0;
-    if (total) {
+    if (t.total) {
         uint64_t any = __ballot(n != 0);
-        uint32_t first = (uint32_t)__builtin_ctzll(any);
-        if (lane == first) base = atomicAdd(counter, total);
-        base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)first);
+        t.first = (uint32_t)__builtin_ctzll(any);
+        if (lane == t.first) t.base = atomicAdd(counter, t.total);
     }
-    return base + mine;
+    return t;
+}
+__device__ __forceinline__ uint32_t wave_append_end(const AppendTicket& t) {
+    if (!t.total) return t.mine;
+    return (uint32_t)__builtin_amdgcn_readlane((int)t.base, (int)t.first) + t.mine;
+}
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, uint32_t n, uint32_t lane) {
+    return wave_append_end(wave_append_begin(counter, n, lane));
 }
 
 // The shading point's own shape, tested first for its shadow rays (trace kernel): the
@@ -376,6 +387,12 @@ extern __shared__ float4 rt_dyn_lds[];
 #endif
 #ifndef RT_FIRST_WAVES
 #define RT_FIRST_WAVES RT_TRACE_WAVES  // level 0's instantiation (A/B builds: -DRT_FIRST_WAVES=4)
+#endif
+#ifndef RT_EXTRA_ATOMIC
+#define RT_EXTRA_ATOMIC 0  // measurement builds only: one more returning atomic per trace wave iteration
+#endif
+#ifndef RT_LATE_TASKS
+#define RT_LATE_TASKS 0    // deep levels: the children's append read after the own-shape shadow tests
 #endif
 template <bool COUNT, bool LDS, bool DEEP = false, bool FIRST = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_DEEP_WAVES : (FIRST ? RT_FIRST_WAVES : RT_TRACE_WAVES), 8))) void trace_level_kernel(
@@ -610,7 +627,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         }
         // ---- children -> level k+1 queue
         uint32_t nc = (want_refl ? 1u : 0u) + (want_refr ? 1u : 0u);
-        uint32_t my = wave_append(&P.levels[2 * (level + 1) + 1], nc, lane);
+        const AppendTicket child_ticket = wave_append_begin(&P.levels[2 * (level + 1) + 1], nc, lane);
+        // LATE (deep levels, whose own-shape shadow tests issue no vector-memory loads): the
+        // children's slots are read after those tests, which overlap the append's round trip
+        constexpr bool LATE = RT_LATE_TASKS && DEEP;
+        auto write_children = [&]() {
+        uint32_t my = wave_append_end(child_ticket);
         const uint32_t fkey = (P.frames > 1 && P.frame_keys) ? ((pix >> RT_FRAME_SHIFT) << P.task_frame_shift) : 0u;
         // inside keys: the children carry the frame bits and the enclosing shape + 1
         const uint32_t cpix = inside_keys ? (pix & ~RT_INSIDE_MASK) : pix, own = sh_key >> 4;
@@ -640,6 +662,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
             }
         }
         if (hit) P.node_flags[n] = hit_flags;
+        };
+        if constexpr (!LATE) write_children();
         // ---- shadow rays the own shape decides, and (levels < inline_levels) the rest:
         // after the node record and the children are out, so that little stays live
         // across the shadow scans
@@ -687,6 +711,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
             if constexpr (CntT::kCount) it_scan_self = cnt.cyc_scan - it_scan_self;
             P.node_lit[n] = lit_pre;
         }
+        if constexpr (LATE) write_children();
         // ---- one shadow entry per point light, grouped by light within the wave
         // ([light a: this wave's hits in lane order][light b: ...]) so that a shadow wave
         // holds rays from neighbouring points towards ONE light
@@ -744,6 +769,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 }
             }
         }
+#if RT_EXTRA_ATOMIC
+        {  // measurement only (tools: A/B of a build with -DRT_EXTRA_ATOMIC=1): one more returning
+           // append-style atomic per wave iteration, its value waited for -- what an append costs
+            uint32_t z = 0;
+            if (lane == 0) z = atomicAdd(&P.levels[RT_WORK_WORD(RT_MAX_DEPTH)], 1u);
+            z = (uint32_t)__builtin_amdgcn_readlane((int)z, 0);
+            if (z == 0xFFFFFFFFu) P.node_flags[n] = 0u;
+        }
+#endif
         if constexpr (CntT::kCount)  // the rest of the iteration: attributes, records, children, entries
             cnt.cyc_post += (rt_clock() - t_load) - it_load - (cnt.cyc_scan - it_scan0 - it_scan_self) -
                             (cnt.cyc_self - it_self0);
