@@ -174,8 +174,22 @@ Scene& Scene::operator=(const Scene& o) {
     }
     return *this;
 }
-Scene::Scene(Scene&&) noexcept = default;
-Scene& Scene::operator=(Scene&&) noexcept = default;
+Scene::Scene(Scene&& o) noexcept
+    : ambient_(o.ambient_), shapes_(std::move(o.shapes_)), lights_(std::move(o.lights_)), cache_(std::move(o.cache_)) {}
+Scene& Scene::operator=(Scene&& o) noexcept {
+    if (this != &o) {
+        ambient_ = o.ambient_;
+        shapes_ = std::move(o.shapes_);
+        lights_ = std::move(o.lights_);
+        cache_ = std::move(o.cache_);
+    }
+    return *this;
+}
+Scene::DeviceCache& Scene::device_cache() const {
+    std::lock_guard<std::mutex> lock(cache_init_);
+    if (!cache_) cache_.reset(new DeviceCache());
+    return *cache_;
+}
 
 Shape* Scene::find_shape_mut(const std::string& name) {
     for (auto& s : shapes_)

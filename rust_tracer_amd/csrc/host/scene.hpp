@@ -147,13 +147,14 @@ public:
     // edits in place (Rc<RefCell<Material>> edits through a MaterialRef land here too), a
     // rebuild after any other edit.  Freed with the Scene.
     struct DeviceCache;
-    DeviceCache& device_cache() const { return *cache_; }
+    DeviceCache& device_cache() const;
 
 private:
     Color ambient_ = colors::BLACK;
     std::vector<Shape> shapes_;
     std::vector<Light> lights_;
-    std::unique_ptr<DeviceCache> cache_;
+    mutable std::unique_ptr<DeviceCache> cache_;  // (a moved-from Scene gets a new one when rendered)
+    mutable std::mutex cache_init_;
 };
 
 struct Camera {  // render.rs:155-176

@@ -1819,9 +1819,12 @@ rt_status create_handle(const rt_scene_desc* d, int32_t device, const Tune& tn, 
     return RT_OK;
 }
 
-// Replaces the scene data of `dst` (its device allocation and DevScene) by a copy of src's,
-// on dst's device, after dst's renders have finished (the caller synchronised them).
-rt_status adopt_scene_data(rt_scene* dst, const rt_scene* src) {
+// rt_scene_update's rebuild, in two steps so that a failure leaves every handle as it was:
+// stage_scene_data waits for dst's renders and copies src's device scene into a new
+// allocation on dst's device; commit_scene_data then swaps it in (rebased DevScene, the
+// description, the light count's workspace consequences).
+rt_status stage_scene_data(rt_scene* dst, const rt_scene* src, void** out) {
+    *out = nullptr;
     HIP_TRY(hipSetDevice(dst->device));
     HIP_TRY(hipStreamSynchronize(dst->stream));
     for (auto& se : dst->ev_streams) HIP_TRY(hipEventSynchronize(se.second));  // renders on other streams
@@ -1837,6 +1840,14 @@ rt_status adopt_scene_data(rt_scene* dst, const rt_scene* src) {
         (void)hipFree(mem);
         return st;
     }
+    *out = mem;
+    return RT_OK;
+}
+
+void commit_scene_data(rt_scene* dst, const rt_scene* src, void* mem) {
+    (void)hipSetDevice(dst->device);
+    // a different light count changes the shadow queue's size and the node-index limit
+    const bool new_lights = dst->n_point_lights != src->n_point_lights || dst->S.n_lights != src->S.n_lights;
     if (dst->dmem) (void)hipFree(dst->dmem);
     dst->dmem = mem;
     dst->dbytes = src->dbytes;
@@ -1850,7 +1861,6 @@ rt_status adopt_scene_data(rt_scene* dst, const rt_scene* src) {
     rebase(S.dsph); rebase(S.gsph); rebase(S.tri); rebase(S.cube); rebase(S.plane); rebase(S.cubetri);
     rebase(S.shapes); rebase(S.mats); rebase(S.lights); rebase(S.bvh_nodes); rebase(S.bvh_leaves);
     rebase(S.graze_blk); rebase(S.graze_tri); rebase(S.graze_pn); rebase(S.graze_mask); rebase(S.scan_ops);
-    const bool new_lights = dst->n_point_lights != src->n_point_lights;
     dst->flops_per_scan = src->flops_per_scan;
     dst->normal_max = src->normal_max;
     dst->n_point_lights = src->n_point_lights;
@@ -1861,8 +1871,7 @@ rt_status adopt_scene_data(rt_scene* dst, const rt_scene* src) {
     // deeper ray trees may need a larger pool than any pass checked so far: check again
     dst->checked_items = 0;
     dst->checked_depth = 0;
-    if (new_lights) free_workspace(dst->ws);  // the shadow queue and the node-index limit follow the lights
-    return RT_OK;
+    if (new_lights) free_workspace(dst->ws);
 }
 
 }  // namespace
@@ -3216,10 +3225,26 @@ rt_status rt_scene_update(rt_scene* s, const rt_scene_desc* d, int32_t* what) {
     rt_scene* fresh = nullptr;
     st = create_handle(d, s->device, s->tune, &fresh);
     if (st != RT_OK) return st;
-    st = adopt_scene_data(s, fresh);
-    if (st == RT_OK && s->split) st = rt_multi_each(s->split, [&](rt_scene* c) { return adopt_scene_data(c, fresh); });
-    if (st == RT_OK && s->multi) st = rt_multi_each(s->multi, [&](rt_scene* c) { return adopt_scene_data(c, fresh); });
+    // every copy of the scene the handle renders with: its own, its band shares', its devices'
+    std::vector<rt_scene*> targets{s};
+    auto collect = [&](rt_scene* c) {
+        targets.push_back(c);
+        return RT_OK;
+    };
+    if (s->split) (void)rt_multi_each(s->split, collect);
+    if (s->multi) (void)rt_multi_each(s->multi, collect);
+    std::vector<void*> staged(targets.size(), nullptr);
+    for (size_t i = 0; i < targets.size() && st == RT_OK; i++) st = stage_scene_data(targets[i], fresh, &staged[i]);
+    if (st == RT_OK)
+        for (size_t i = 0; i < targets.size(); i++) commit_scene_data(targets[i], fresh, staged[i]);
+    else
+        for (size_t i = 0; i < targets.size(); i++)
+            if (staged[i]) {
+                (void)hipSetDevice(targets[i]->device);
+                (void)hipFree(staged[i]);
+            }
     rt_scene_destroy(fresh);
+    (void)hipSetDevice(s->device);
     if (st != RT_OK) return st;
     if (what) *what = 2;
     return RT_OK;
