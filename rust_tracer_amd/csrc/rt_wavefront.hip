@@ -391,6 +391,9 @@ extern __shared__ float4 rt_dyn_lds[];
 #ifndef RT_EXTRA_ATOMIC
 #define RT_EXTRA_ATOMIC 0  // measurement builds only: one more returning atomic per trace wave iteration
 #endif
+#if RT_EXTRA_ATOMIC
+__device__ uint32_t rt_extra_words[8 * 32];
+#endif
 #ifndef RT_LATE_TASKS
 #define RT_LATE_TASKS 0    // deep levels: the children's append read after the own-shape shadow tests
 #endif
@@ -773,7 +776,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         {  // measurement only (tools: A/B of a build with -DRT_EXTRA_ATOMIC=1): one more returning
            // append-style atomic per wave iteration, its value waited for -- what an append costs
             uint32_t z = 0;
-            if (lane == 0) z = atomicAdd(&P.levels[RT_WORK_WORD(RT_MAX_DEPTH)], 1u);
+            // 1: one word for the whole device; 2: one word per XCD (blockIdx % 8, 128 B apart)
+            if (lane == 0) z = atomicAdd(&rt_extra_words[RT_EXTRA_ATOMIC == 2 ? (blockIdx.x & 7u) * 32u : 0u], 1u);
             z = (uint32_t)__builtin_amdgcn_readlane((int)z, 0);
             if (z == 0xFFFFFFFFu) P.node_flags[n] = 0u;
         }
