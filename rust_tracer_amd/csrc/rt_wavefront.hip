@@ -388,6 +388,16 @@ extern __shared__ float4 rt_dyn_lds[];
 #ifndef RT_FIRST_WAVES
 #define RT_FIRST_WAVES RT_TRACE_WAVES  // level 0's instantiation (A/B builds: -DRT_FIRST_WAVES=4)
 #endif
+#ifndef RT_POST_CLOCK
+#define RT_POST_CLOCK 0  // diagnostic builds: wall-clock of the trace iteration's phases (tools/post_clock.py)
+#endif
+#if RT_POST_CLOCK
+// [level 0 / levels >= 1][load, scan, attributes + node record, children, self, shadow entries, iterations]
+__device__ unsigned long long rt_post_clock[2 * 8];
+#define RT_PC(v) v = __builtin_amdgcn_s_memtime()
+#else
+#define RT_PC(v)
+#endif
 #ifndef RT_EXTRA_ATOMIC
 #define RT_EXTRA_ATOMIC 0  // measurement builds only: one more returning atomic per trace wave iteration
 #endif
@@ -449,7 +459,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
     const uint32_t pf_stride = gridDim.x * (blockDim.x >> 6) * W;
     uint32_t pf_slot = 0;
     bool pf_have = false;
+#if RT_POST_CLOCK
+    uint64_t pc_acc[7] = {0, 0, 0, 0, 0, 0, 0};
+#endif
     for (uint32_t it = 0;; ++it) {
+#if RT_POST_CLOCK
+        uint64_t pc0, pc1, pc2 = 0, pc3, pc4, pc5, pc6;
+#endif
+        RT_PC(pc0);
         const uint32_t base = sched_base(P, &P.levels[RT_WORK_WORD(level)], count, it, W);
 #if RT_TASK_CLOCK_BUILD
         if (P.task_clock) task_clock_mark(P, level, it, clk_base, clk0, count);
@@ -533,6 +550,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
             it_scan0 = cnt.cyc_scan;
             it_self0 = cnt.cyc_self;
         }
+        RT_PC(pc1);
         if (active) {
             n_node++;
             float bt = __builtin_huge_valf();
@@ -561,6 +579,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 scan_from<LDS>(S, ro, rd, bt, bk, cnt, lnodes);
             else
                 scan_buffered<LDS>(S, ro, rd, bt, bk, cnt, lnodes, buf_ok, buf_leaf);
+            RT_PC(pc2);
             if (bk == 0xFFFFFFFFu) {
                 // trace_ray -> BLACK: the parent's child slot gets BLACK (forest: direction 0)
                 P.node_flags[n] = NODE_MISS;
@@ -628,6 +647,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 P.node_d[n] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(parent));
             }
         }
+        RT_PC(pc3);
         // ---- children -> level k+1 queue
         uint32_t nc = (want_refl ? 1u : 0u) + (want_refr ? 1u : 0u);
         const AppendTicket child_ticket = wave_append_begin(&P.levels[2 * (level + 1) + 1], nc, lane);
@@ -667,6 +687,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         if (hit) P.node_flags[n] = hit_flags;
         };
         if constexpr (!LATE) write_children();
+        RT_PC(pc4);
         // ---- shadow rays the own shape decides, and (levels < inline_levels) the rest:
         // after the node record and the children are out, so that little stays live
         // across the shadow scans
@@ -714,6 +735,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
             if constexpr (CntT::kCount) it_scan_self = cnt.cyc_scan - it_scan_self;
             P.node_lit[n] = lit_pre;
         }
+        RT_PC(pc5);
         if constexpr (LATE) write_children();
         // ---- one shadow entry per point light, grouped by light within the wave
         // ([light a: this wave's hits in lane order][light b: ...]) so that a shadow wave
@@ -772,6 +794,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 }
             }
         }
+#if RT_POST_CLOCK
+        RT_PC(pc6);
+        if (!pc2) pc2 = pc1;  // no lane traced
+        pc_acc[0] += pc1 - pc0;
+        pc_acc[1] += pc2 - pc1;
+        pc_acc[2] += pc3 - pc2;
+        pc_acc[3] += pc4 - pc3;
+        pc_acc[4] += pc5 - pc4;
+        pc_acc[5] += pc6 - pc5;
+        pc_acc[6] += 1;
+#endif
 #if RT_EXTRA_ATOMIC
         {  // measurement only (tools: A/B of a build with -DRT_EXTRA_ATOMIC=1): one more returning
            // append-style atomic per wave iteration, its value waited for -- what an append costs
@@ -788,6 +821,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         pf_slot = pf_next;
         pf_have = pf_on;
     }
+#if RT_POST_CLOCK
+    if (lane == 0)
+        for (int k = 0; k < 7; k++) atomicAdd(&rt_post_clock[(level == 0 ? 0 : 8) + k], (unsigned long long)pc_acc[k]);
+#endif
     for (int o = 32; o > 0; o >>= 1) {
         n_node += __shfl_xor(n_node, o);
         n_pix += __shfl_xor(n_pix, o);
@@ -1295,6 +1332,18 @@ hipError_t launch_wave_combine(const WaveParams& p, uint32_t level, int blocks, 
 
 }  // namespace rtdev
 
+#if RT_POST_CLOCK
+// tools/post_clock.py: read (and optionally reset) the trace iteration's phase clocks
+extern "C" int rt_debug_post_clock(unsigned long long* out16, int reset) {
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(rtdev::rt_post_clock), 16 * sizeof(unsigned long long)) != hipSuccess)
+        return 1;
+    if (reset) {
+        unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(rtdev::rt_post_clock), z, sizeof(z)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif
 #if RT_STATS
 // tools/scan_stats.py: read (and optionally reset) the wavefront pipeline's scan counters
 extern "C" int rt_debug_scan_stats(unsigned long long* out40, int reset) {
