@@ -90,6 +90,24 @@ typedef const __attribute__((address_space(4))) float4 cfloat4;
 typedef const float4 cfloat4;  // host pass: the kernel body is never executed there
 #endif
 __device__ __forceinline__ cfloat4* cptr(const float4* p) { return (cfloat4*)p; }
+// A light record (wave-uniform index): two scalar loads.  Read through a generic pointer the
+// loop over the lights became a chain of vector loads, each waited for with vmcnt(0) -- after
+// every store the wave had outstanding.
+__device__ __forceinline__ LightRec light_at(const DevScene& S, int i) {
+    static_assert(sizeof(LightRec) == 32, "LightRec is two float4");
+    cfloat4* p = cptr(reinterpret_cast<const float4*>(S.lights)) + 2 * i;
+    const float4 a = p[0], b = p[1];
+    LightRec L;
+    L.kind = __float_as_int(a.x);
+    L.px = a.y;
+    L.py = a.z;
+    L.pz = a.w;
+    L.r = b.x;
+    L.g = b.y;
+    L.b = b.z;
+    L.lb_base = __float_as_uint(b.w);
+    return L;
+}
 
 // Nearest-hit bookkeeping: (t, key) lexicographic minimum == Scene::intersect's strict `<`
 // in insertion order (ties keep the earlier shape / earlier cube triangle).

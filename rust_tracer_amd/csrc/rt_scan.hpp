@@ -731,15 +731,18 @@ __device__ __forceinline__ uint32_t lb_cell(uint32_t res, V3 v) {
 // direction error, rt_api.cpp build_light_buffers) -- or -1: no buffer (the light has none,
 // or the origin lies beyond its tiers) -- walk.  LightRec::lb_base: the light's first cell in
 // bits 0-27, its tier count in bits 28-30 (~0: no buffer).
-__device__ __forceinline__ int lb_tier(const DevScene& S, uint32_t lb_base, V3 o, float l2) {
+// ... for the origin's D = |o - c| + R given (the trace kernel's queue keys: D once per hit)
+__device__ __forceinline__ int lb_tier_at(const DevScene& S, uint32_t lb_base, float D, float l2) {
     if (!S.lb_res || lb_base == 0xFFFFFFFFu) return -1;
     const int tiers = (int)((lb_base >> 28) & 7u);
-    const float dx = o.x - S.bvh_cx, dy = o.y - S.bvh_cy, dz = o.z - S.bvh_cz;
-    const float D = sqrtf(dx * dx + dy * dy + dz * dz) + S.bvh_r;
     float thr = S.lb_dmax, lm2 = RT_LB_LMAX * RT_LB_LMAX;
     for (int t = 0; t < tiers; t++, thr *= 2.f, lm2 *= 4.f)
         if (D <= thr && l2 <= lm2) return t;
     return -1;
+}
+__device__ __forceinline__ int lb_tier(const DevScene& S, uint32_t lb_base, V3 o, float l2) {
+    const float dx = o.x - S.bvh_cx, dy = o.y - S.bvh_cy, dz = o.z - S.bvh_cz;
+    return lb_tier_at(S, lb_base, sqrtf(dx * dx + dy * dy + dz * dz) + S.bvh_r, l2);
 }
 
 // Grazing pass: every hierarchy triangle whose plane some lane's ray meets at

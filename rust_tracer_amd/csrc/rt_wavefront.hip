@@ -102,8 +102,16 @@ __device__ __forceinline__ uint32_t spread5(uint32_t v) {  // abcde -> a..b..c..
     v = (v | (v << 2)) & 0x09249249u;
     return v;
 }
+// Queue keys order the queues and nothing else (a key never reaches a result), so their
+// arithmetic takes the hardware's approximate reciprocal and square root instead of the
+// correctly rounded sequences the render's own arithmetic needs (RT_FAST_KEYS=0: exact forms)
+#ifndef RT_FAST_KEYS
+#define RT_FAST_KEYS 1
+#endif
+__device__ __forceinline__ float key_rcp(float x) { return RT_FAST_KEYS ? __builtin_amdgcn_rcpf(x) : 1.f / x; }
+__device__ __forceinline__ float key_sqrt(float x) { return RT_FAST_KEYS ? __builtin_amdgcn_sqrtf(x) : sqrtf(x); }
 __device__ __forceinline__ uint32_t morton15(const DevScene& S, V3 p) {
-    float sc = 16.f / S.bvh_r;
+    float sc = 16.f * key_rcp(S.bvh_r);
     int x = (int)fminf(fmaxf((p.x - S.bvh_cx) * sc + 16.f, 0.f), 31.f);
     int y = (int)fminf(fmaxf((p.y - S.bvh_cy) * sc + 16.f, 0.f), 31.f);
     int z = (int)fminf(fmaxf((p.z - S.bvh_cz) * sc + 16.f, 0.f), 31.f);
@@ -120,7 +128,7 @@ __device__ __forceinline__ uint32_t spread6(uint32_t v) {  // abcdef -> a..b..c.
 }
 // 18-bit Morton code over the 64^3 grid of the same cube
 __device__ __forceinline__ uint32_t morton18(const DevScene& S, V3 p) {
-    float sc = 32.f / S.bvh_r;
+    float sc = 32.f * key_rcp(S.bvh_r);
     int x = (int)fminf(fmaxf((p.x - S.bvh_cx) * sc + 32.f, 0.f), 63.f);
     int y = (int)fminf(fmaxf((p.y - S.bvh_cy) * sc + 32.f, 0.f), 63.f);
     int z = (int)fminf(fmaxf((p.z - S.bvh_cz) * sc + 32.f, 0.f), 63.f);
@@ -136,7 +144,7 @@ __device__ __forceinline__ uint32_t spread7(uint32_t v) {  // 7 bits -> every th
 }
 // 21-bit Morton code over the 128^3 grid of the same cube
 __device__ __forceinline__ uint32_t morton21(const DevScene& S, V3 p) {
-    float sc = 64.f / S.bvh_r;
+    float sc = 64.f * key_rcp(S.bvh_r);
     int x = (int)fminf(fmaxf((p.x - S.bvh_cx) * sc + 64.f, 0.f), 127.f);
     int y = (int)fminf(fmaxf((p.y - S.bvh_cy) * sc + 64.f, 0.f), 127.f);
     int z = (int)fminf(fmaxf((p.z - S.bvh_cz) * sc + 64.f, 0.f), 127.f);
@@ -159,8 +167,9 @@ __device__ __forceinline__ uint32_t dir_cell16(V3 d) {
     if (ax >= ay && ax >= az) { face = d.x < 0.f; u = d.y; v = d.z; m = ax; }
     else if (ay >= az) { face = 2u + (d.y < 0.f); u = d.x; v = d.z; m = ay; }
     else { face = 4u + (d.z < 0.f); u = d.x; v = d.y; m = az; }
-    const uint32_t qu = (uint32_t)fminf(fmaxf((u / m + 1.f) * 2.f, 0.f), 3.f);
-    const uint32_t qv = (uint32_t)fminf(fmaxf((v / m + 1.f) * 2.f, 0.f), 3.f);
+    const float im = key_rcp(m);
+    const uint32_t qu = (uint32_t)fminf(fmaxf((u * im + 1.f) * 2.f, 0.f), 3.f);
+    const uint32_t qv = (uint32_t)fminf(fmaxf((v * im + 1.f) * 2.f, 0.f), 3.f);
     return (face << 4) | (qu << 2) | qv;
 }
 __device__ __forceinline__ uint32_t inside_key(const WaveParams& P, uint32_t center_key, V3 d) {
@@ -398,6 +407,9 @@ __device__ unsigned long long rt_post_clock[2 * 8];
 #else
 #define RT_PC(v)
 #endif
+#ifndef RT_DIAG_ENTRIES
+#define RT_DIAG_ENTRIES 0  // diagnostic builds (wrong frames): 1 no shadow-entry stores, 2 no shadow append
+#endif
 #ifndef RT_EXTRA_ATOMIC
 #define RT_EXTRA_ATOMIC 0  // measurement builds only: one more returning atomic per trace wave iteration
 #endif
@@ -406,6 +418,12 @@ __device__ uint32_t rt_extra_words[8 * 32];
 #endif
 #ifndef RT_LATE_TASKS
 #define RT_LATE_TASKS 0    // deep levels: the children's append read after the own-shape shadow tests
+#endif
+#ifndef RT_DEFER_STORES
+// deep levels: both appends issued and read before the wave iteration's first store.  Stores
+// count in vmcnt on gfx9 and the compiler waits with vmcnt(0) once loads and stores are both
+// outstanding, so an append read after a store waits for that store's acknowledgement
+#define RT_DEFER_STORES 1
 #endif
 template <bool COUNT, bool LDS, bool DEEP = false, bool FIRST = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_DEEP_WAVES : (FIRST ? RT_FIRST_WAVES : RT_TRACE_WAVES), 8))) void trace_level_kernel(
@@ -542,6 +560,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         V3 sh_ps = v3(0, 0, 0), sh_n = v3(0, 0, 0);  // the hit's shadow-ray origin and normal
         bool sh_entering = false;
         uint32_t sh_key = 0;
+        constexpr bool DEFER = DEEP && RT_DEFER_STORES;  // (level 0 too: -4%, its inline scans spill the stores' data)
+        int32_t sh_kind = 0;             // DEFER: the hit shape's kind,
+        uint32_t own_ck = 0;             // ... its centre key (inside keys),
+        float sh_tu = 0.f, sh_tv = 0.f;  // ... the hit's texture coordinates (node record)
+        bool missed = false;             // ... and a miss whose stores are still to do
         uint32_t it_load = 0, it_scan0 = 0, it_self0 = 0;  // phase accounting (instrumented variant)
         uint32_t it_scan_self = 0;  // scan cycles spent inside the self phase (inline shadow scans)
         if constexpr (CntT::kCount) {
@@ -582,10 +605,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
             RT_PC(pc2);
             if (bk == 0xFFFFFFFFu) {
                 // trace_ray -> BLACK: the parent's child slot gets BLACK (forest: direction 0)
-                P.node_flags[n] = NODE_MISS;
-                if (level > 0) {
-                    P.node_ec[parent] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (P.node_dc) P.node_dc[parent] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if constexpr (DEFER) {
+                    missed = true;
+                } else {
+                    P.node_flags[n] = NODE_MISS;
+                    if (level > 0) {
+                        P.node_ec[parent] = make_float4(0.f, 0.f, 0.f, 0.f);
+                        if (P.node_dc) P.node_dc[parent] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
                 }
             } else {
                 hit = true;
@@ -619,6 +646,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 sh_n = h.n;
                 sh_entering = h.entering;
                 sh_key = bk;
+                if constexpr (DEFER) {  // read now: no load after the iteration's first store
+#if RT_HIT_BULK
+                    sh_kind = SR.kind();
+                    own_ck = __float_as_uint(SR.w[0].z);
+#else
+                    sh_kind = S.shapes[bk >> 4].kind;
+                    own_ck = S.shapes[bk >> 4].center_key;
+#endif
+                    sh_tu = h.tu;
+                    sh_tv = h.tv;
+                }
                 if (P.node_dc) {  // ray forest: the shape id as the reference records it, the pixel
                     uint32_t shape = bk >> 4;
                     P.node_key[n] = (S.shapes[shape].kind == RT_SHAPE_CUBE) ? (bk & 15u) : shape;
@@ -626,7 +664,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 }
                 const bool child_ok = level + 1 < P.depth;
                 if (inside_keys) {  // closed shapes: refraction enters from outside, reflection stays inside
-                    const int32_t kind = S.shapes[bk >> 4].kind;
+                    const int32_t kind = DEFER ? sh_kind : S.shapes[bk >> 4].kind;
                     const bool closed = kind == RT_SHAPE_SPHERE || kind == RT_SHAPE_CUBE;
                     refr_in = closed && h.entering;
                     refl_in = closed && !h.entering;
@@ -642,20 +680,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 }
                 // the node record: what the combine pass cannot re-derive (rt_device.hpp)
                 hit_flags = NODE_HIT | (h.entering ? F_ENTER : 0u) | ((uint32_t)h.mat << F_MAT_SHIFT);
-                P.node_ps[n] = make_float4(ps.x, ps.y, ps.z, h.tu);
-                P.node_n[n] = make_float4(h.n.x, h.n.y, h.n.z, h.tv);
-                P.node_d[n] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(parent));
+                if constexpr (!DEFER) {
+                    P.node_ps[n] = make_float4(ps.x, ps.y, ps.z, h.tu);
+                    P.node_n[n] = make_float4(h.n.x, h.n.y, h.n.z, h.tv);
+                    P.node_d[n] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(parent));
+                }
             }
         }
         RT_PC(pc3);
         // ---- children -> level k+1 queue
-        uint32_t nc = (want_refl ? 1u : 0u) + (want_refr ? 1u : 0u);
-        const AppendTicket child_ticket = wave_append_begin(&P.levels[2 * (level + 1) + 1], nc, lane);
+        const uint32_t nc = (want_refl ? 1u : 0u) + (want_refr ? 1u : 0u);
         // LATE (deep levels, whose own-shape shadow tests issue no vector-memory loads): the
         // children's slots are read after those tests, which overlap the append's round trip
-        constexpr bool LATE = RT_LATE_TASKS && DEEP;
-        auto write_children = [&]() {
-        uint32_t my = wave_append_end(child_ticket);
+        constexpr bool LATE = RT_LATE_TASKS && DEEP && !DEFER;
+        // my: the lane's first child slot past next_off (wave_append_end)
+        auto write_children = [&](uint32_t my) {
         const uint32_t fkey = (P.frames > 1 && P.frame_keys) ? ((pix >> RT_FRAME_SHIFT) << P.task_frame_shift) : 0u;
         // inside keys: the children carry the frame bits and the enclosing shape + 1
         const uint32_t cpix = inside_keys ? (pix & ~RT_INSIDE_MASK) : pix, own = sh_key >> 4;
@@ -665,7 +704,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 Task T = {rro.x, rro.y, rro.z, rrd.x, rrd.y, rrd.z, (n << 1) | 0u, refl_in ? cpix | (own + 1u) : cpix};
                 P.tasks[slot] = T;
                 if (P.task_keys)
-                    P.task_keys[slot] = (refl_in ? inside_key(P, S.shapes[own].center_key, rrd) : task_key(P, rro, rrd)) | fkey;
+                    P.task_keys[slot] = (refl_in ? inside_key(P, DEFER ? own_ck : S.shapes[own].center_key, rrd) : task_key(P, rro, rrd)) | fkey;
                 hit_flags |= F_HAS_R;
             } else {
                 atomicOr(P.overflow, 1u);
@@ -678,7 +717,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 Task T = {tro.x, tro.y, tro.z, trd.x, trd.y, trd.z, (n << 1) | 1u, refr_in ? cpix | (own + 1u) : cpix};
                 P.tasks[slot] = T;
                 if (P.task_keys)
-                    P.task_keys[slot] = (refr_in ? inside_key(P, S.shapes[own].center_key, trd) : task_key(P, tro, trd)) | fkey;
+                    P.task_keys[slot] = (refr_in ? inside_key(P, DEFER ? own_ck : S.shapes[own].center_key, trd) : task_key(P, tro, trd)) | fkey;
                 hit_flags |= F_HAS_T;
             } else {
                 atomicOr(P.overflow, 1u);
@@ -686,24 +725,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         }
         if (hit) P.node_flags[n] = hit_flags;
         };
-        if constexpr (!LATE) write_children();
-        RT_PC(pc4);
         // ---- shadow rays the own shape decides, and (levels < inline_levels) the rest:
         // after the node record and the children are out, so that little stays live
-        // across the shadow scans
+        // across the shadow scans (DEFER: before the appends and every store)
+        uint32_t lit_pre = 0u;
+        auto self_tests = [&]() {
         if (hit) {
-            uint32_t lit_pre = 0u;
             if constexpr (CntT::kCount) it_scan_self = cnt.cyc_scan;
             RT_T0(CntT, t_self);
             if (P.self_shadow) {
                 // the own shape can only shadow a light behind the offset point's
                 // surface (or any light, from inside a sphere); elsewhere the test is
                 // skipped (never deciding is always exact: the shadow pass decides)
-                const uint32_t own_kind = (uint32_t)S.shapes[sh_key >> 4].kind;
+                const uint32_t own_kind = (uint32_t)(DEFER ? sh_kind : S.shapes[sh_key >> 4].kind);
                 const bool own_any = own_kind == RT_SHAPE_SPHERE && !sh_entering;
                 const bool own_ok = own_kind == RT_SHAPE_SPHERE || own_kind == RT_SHAPE_TRIANGLE;
                 for (int li = 0; li < S.n_lights; ++li) {
-                    const LightRec& L = S.lights[li];
+                    const LightRec L = light_at(S, li);
                     if (L.kind != RT_LIGHT_POINT) continue;
                     const V3 lpos = v3(L.px, L.py, L.pz);
                     if (!own_ok || !(own_any || dot(sub(lpos, sh_ps), sh_n) <= 0.f)) continue;
@@ -722,7 +760,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
             }
             if (!DEEP && level < P.inline_levels) {  // the level's remaining shadow rays, right here
                 for (int li = 0; li < S.n_lights; ++li) {
-                    const LightRec& L = S.lights[li];
+                    const LightRec L = light_at(S, li);
                     if (L.kind != RT_LIGHT_POINT || ((decided >> li) & 1u)) continue;
                     const V3 lpos = v3(L.px, L.py, L.pz);
                     const V3 ldir = norm(sub(lpos, sh_ps));  // mod.rs:191
@@ -733,32 +771,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
             }
             RT_T1(CntT, cnt, cyc_self, t_self);
             if constexpr (CntT::kCount) it_scan_self = cnt.cyc_scan - it_scan_self;
-            P.node_lit[n] = lit_pre;
+            if constexpr (!DEFER) P.node_lit[n] = lit_pre;
         }
-        RT_PC(pc5);
-        if constexpr (LATE) write_children();
+        };
         // ---- one shadow entry per point light, grouped by light within the wave
         // ([light a: this wave's hits in lane order][light b: ...]) so that a shadow wave
-        // holds rays from neighbouring points towards ONE light
-        uint64_t hits = __ballot(hit);
+        // holds rays from neighbouring points towards ONE light.  shadow_begin issues the
+        // append, shadow_entries(base) writes the entries from the slot base it returned.
+        uint64_t hits = 0;
+        uint32_t s_first = 0, s_raw = 0;
+        auto shadow_begin = [&]() {
+            hits = __ballot(hit);
+            if (hits) {
+                // entries still to trace: per point light, the hit lanes it was not decided for
+                uint32_t total = 0;
+                for (int li = 0; li < S.n_lights; ++li)
+                    if (light_at(S, li).kind == RT_LIGHT_POINT)
+                        total += (uint32_t)__builtin_popcountll(__ballot(hit && !((decided >> li) & 1u)));
+                s_first = (uint32_t)__builtin_ctzll(hits);
+#if RT_DIAG_ENTRIES == 2  // diagnostic: no append (slots overlap; the frame is wrong, the trace's timing is not)
+                s_raw = (n - lane) * 3u % (P.shadow_capacity - 256u);
+#else
+                if (lane == s_first && total) s_raw = atomicAdd(&RT_SHADOW_COUNT(P), total);
+#endif
+            }
+        };
+        auto shadow_base = [&]() -> uint32_t {
+            if (!hits || RT_DIAG_ENTRIES == 2) return s_raw;
+            return (uint32_t)__builtin_amdgcn_readlane((int)s_raw, (int)s_first);
+        };
+        auto shadow_entries = [&](uint32_t sbase) {
         if (hits) {
-            // entries still to trace: per point light, the hit lanes it was not decided for
-            uint32_t total = 0;
-            for (int li = 0; li < S.n_lights; ++li)
-                if (S.lights[li].kind == RT_LIGHT_POINT)
-                    total += (uint32_t)__builtin_popcountll(__ballot(hit && !((decided >> li) & 1u)));
-            uint32_t first = (uint32_t)__builtin_ctzll(hits);
-            uint32_t sbase = 0;
-            if (lane == first && total) sbase = atomicAdd(&RT_SHADOW_COUNT(P), total);
-            sbase = (uint32_t)__builtin_amdgcn_readlane((int)sbase, (int)first);
             uint32_t group = 0;  // entries of the earlier lights
+            // the key's light-buffer tier test (rt_scan.hpp lb_tier): D once per lane
+            const float key_d = P.shadow_cell ? key_sqrt(len2(v3(sh_ps.x - S.bvh_cx, sh_ps.y - S.bvh_cy,
+                                                                     sh_ps.z - S.bvh_cz))) + S.bvh_r
+                                              : 0.f;
             for (int li = 0; li < S.n_lights; ++li) {
-                if (S.lights[li].kind != RT_LIGHT_POINT) continue;
+                if (light_at(S, li).kind != RT_LIGHT_POINT) continue;
                 const bool want = hit && !((decided >> li) & 1u);
                 const uint64_t m = __ballot(want);
                 const uint32_t slot = sbase + group + (uint32_t)__builtin_popcountll(m & lanemask_lt());
                 group += (uint32_t)__builtin_popcountll(m);
-                if (want) {
+                if (want && !(RT_DIAG_ENTRIES == 1)) {  // (diagnostic 1: no entry stores)
                     if (slot < P.shadow_capacity) {
                         P.shadow[slot] = (n << P.light_bits) | (uint32_t)li;
                         if (P.shadow_keys) {
@@ -766,23 +821,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                             if (P.shadow_cell) {
                                 // the light-buffer cell this shadow ray will test (its direction
                                 // seen from the light), or flag | Morton for rays that walk
-                                const LightRec& L = S.lights[li];
+                                // (the cell of the unnormalised direction: lb_cell divides by the
+                                // largest component, so the length cancels up to rounding)
+                                const LightRec L = light_at(S, li);
                                 const V3 raw = sub(v3(L.px, L.py, L.pz), sh_ps);
-                                const bool lb = lb_tier(S, L.lb_base, sh_ps, len2(raw)) >= 0;
+                                const float l2 = len2(raw);
+                                const V3 dir = RT_FAST_KEYS ? neg(raw) : neg(norm(raw));
+                                const bool lb = RT_FAST_KEYS ? lb_tier_at(S, L.lb_base, key_d, l2) >= 0
+                                                             : lb_tier(S, L.lb_base, sh_ps, l2) >= 0;
                                 if (!lb) {
                                     low = (1u << (P.shadow_fine - 1u)) |
                                           (P.shadow_fine >= 19u ? mort << (P.shadow_fine - 19u) : mort >> (19u - P.shadow_fine));
                                 } else if (P.shadow_cell == 2u) {  // cell | 3-bit distance from the light
-                                    const float dl = sqrtf(len2(raw)) * (8.f / RT_LB_LMAX);
-                                    low = (lb_cell(S.lb_res, neg(norm(raw))) << 3) | (uint32_t)fminf(dl, 7.f);
+                                    const float dl = key_sqrt(l2) * (8.f / RT_LB_LMAX);
+                                    low = (lb_cell(S.lb_res, dir) << 3) | (uint32_t)fminf(dl, 7.f);
                                 } else if (P.shadow_cell == 4u) {  // cell | 7-bit distance (24-bit keys)
-                                    const float dl = sqrtf(len2(raw)) * (128.f / RT_LB_LMAX);
-                                    low = (lb_cell(S.lb_res, neg(norm(raw))) << 7) | (uint32_t)fminf(dl, 127.f);
+                                    const float dl = key_sqrt(l2) * (128.f / RT_LB_LMAX);
+                                    low = (lb_cell(S.lb_res, dir) << 7) | (uint32_t)fminf(dl, 127.f);
                                 } else if (P.shadow_cell == 3u) {  // cell | 4-bit distance (frame batches)
-                                    const float dl = sqrtf(len2(raw)) * (16.f / RT_LB_LMAX);
-                                    low = (lb_cell(S.lb_res, neg(norm(raw))) << 4) | (uint32_t)fminf(dl, 15.f);
+                                    const float dl = key_sqrt(l2) * (16.f / RT_LB_LMAX);
+                                    low = (lb_cell(S.lb_res, dir) << 4) | (uint32_t)fminf(dl, 15.f);
                                 } else {
-                                    low = lb_cell(S.lb_res, neg(norm(raw)));
+                                    low = lb_cell(S.lb_res, dir);
                                 }
                             }
                             P.shadow_keys[slot] = (P.shadow_fine ? (((uint32_t)li << P.shadow_fine) | low)
@@ -793,6 +853,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                         atomicOr(P.overflow, 2u);
                 }
             }
+        }
+        };
+        if constexpr (DEFER) {
+            // every load and both appends' values first, then the stores
+            self_tests();
+            RT_PC(pc4);
+            const AppendTicket child_ticket = wave_append_begin(&P.levels[2 * (level + 1) + 1], nc, lane);
+            shadow_begin();
+            const uint32_t my = wave_append_end(child_ticket);
+            const uint32_t sbase = shadow_base();
+            write_children(my);
+            if (hit) {
+                P.node_ps[n] = make_float4(sh_ps.x, sh_ps.y, sh_ps.z, sh_tu);
+                P.node_n[n] = make_float4(sh_n.x, sh_n.y, sh_n.z, sh_tv);
+                P.node_d[n] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(parent));
+                P.node_lit[n] = lit_pre;
+            } else if (missed) {
+                P.node_flags[n] = NODE_MISS;
+                if (level > 0) {
+                    P.node_ec[parent] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (P.node_dc) P.node_dc[parent] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
+            RT_PC(pc5);
+            shadow_entries(sbase);
+        } else {
+            const AppendTicket child_ticket = wave_append_begin(&P.levels[2 * (level + 1) + 1], nc, lane);
+            if constexpr (!LATE) write_children(wave_append_end(child_ticket));
+            RT_PC(pc4);
+            self_tests();
+            RT_PC(pc5);
+            if constexpr (LATE) write_children(wave_append_end(child_ticket));
+            shadow_begin();
+            shadow_entries(shadow_base());
         }
 #if RT_POST_CLOCK
         RT_PC(pc6);
@@ -847,6 +941,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
 #endif
 template <bool LDS, bool COUNT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_WAVES, 8))) void shadow_kernel(WaveParams P) {
+    if (RT_DIAG_ENTRIES) return;  // diagnostic builds whose shadow queue holds no valid entries
     const DevScene& S = P.S;
     if (LDS) {  // stage the hierarchy's node records in LDS
         for (int i = threadIdx.x; i < 4 * S.n_bvh_nodes; i += blockDim.x) rt_dyn_lds[i] = S.bvh_nodes[i];
@@ -886,7 +981,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
             const uint32_t n = e >> P.light_bits, li = e & lmask;
             if (t < count) {
                 V3 ps = v3(q.x, q.y, q.z);
-                const LightRec& L = S.lights[li];
+                const LightRec L = light_at(S, (int)li);
                 V3 lpos = v3(L.px, L.py, L.pz);
                 V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
                 n_shadow++;
@@ -911,7 +1006,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
                 uint32_t n = e >> P.light_bits, li = e & lmask;
                 const float4 q = P.node_ps[n];
                 V3 ps = v3(q.x, q.y, q.z);
-                const LightRec& L = S.lights[li];
+                const LightRec L = light_at(S, li);
                 V3 lpos = v3(L.px, L.py, L.pz);
                 V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
                 n_shadow++;
@@ -970,7 +1065,7 @@ __device__ __forceinline__ V3 light_sum(const DevScene& S, const MatRec& M, cons
     V3 lsum = v3(0.f, 0.f, 0.f);
     const bool dark_ok = S.dark_skip && M.dark_zero;
     for (int li = 0; li < S.n_lights; ++li) {
-        const LightRec& L = S.lights[li];
+        const LightRec L = light_at(S, li);
         V3 ldir = v3(0.f, 0.f, 0.f);
         V3 E = v3(L.r, L.g, L.b);
         if (L.kind == RT_LIGHT_POINT) {

@@ -9,10 +9,12 @@ NAME=$1; FLAGS=$2
 R=$(cd "$(dirname "$0")/.." && pwd)
 C=$R/rust_tracer_amd/csrc
 B=/tmp/rt_variant_$NAME
-mkdir -p $B
+rm -rf $B && mkdir -p $B  # (a stale object of an older layout would link twice)
 HF="-O3 -std=c++17 -fPIC -ffp-contract=off -Wall --offload-arch=gfx950 -munsafe-fp-atomics $FLAGS"
 CF="-O3 -std=c++17 -fPIC -ffp-contract=off -Wall $FLAGS"
-for f in rt_frame rt_wavefront rt_order; do /opt/rocm/bin/hipcc $HF -c -o $B/$f.o $C/$f.hip & done
+WFFLAGS=${WFFLAGS--mllvm -amdgpu-atomic-optimizer-strategy=None}  # as the Makefile (WFFLAGS= : the compiler's default)
+/opt/rocm/bin/hipcc $HF $WFFLAGS -c -o $B/rt_wavefront.o $C/rt_wavefront.hip &
+for f in rt_frame rt_order; do /opt/rocm/bin/hipcc $HF -c -o $B/$f.o $C/$f.hip & done
 for f in rt_api rt_multi; do /opt/rocm/bin/hipcc $HF -c -o $B/$f.o $C/$f.cpp & done
 /opt/rocm/bin/hipcc $CF -x c++ -c -o $B/rt_bvh.o $C/rt_bvh.cpp &
 /opt/rocm/bin/hipcc $CF -x c++ -c -o $B/rt_tune.o $C/rt_tune.cpp &

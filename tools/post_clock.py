@@ -5,10 +5,11 @@ Phases (rt_wavefront.hip RT_POST_CLOCK): load (task / pixel), scan, attributes +
 children (append + tasks), self (own-shape and inline shadow tests), shadow entries (append +
 keys).  s_memtime ticks summed over waves: a wave's time includes the other waves' issue on its
 SIMD, so the shares, not the totals, are the result.  Config 3 at 1080p, depth 8: one frame at
-a time, then a 20-frame batch (one pass, like the bench's).  Round 5 (profiles/r5ab/r5d2_*): at
-levels >= 1 the scan is a third of a wave iteration's time, the own-shape tests a fifth and
-the shadow entries' keys a fifth -- VALU work: with every store of the iteration moved after
-its loads and appends the shares moved, the time per iteration and the frame rate did not."""
+a time, then a 20-frame batch (one pass, like the bench's).  Round 5 (profiles/r5ab/r5d2_*,
+r5l1_post_clock.log): the own-shape tests and the shadow entries took two fifths of a deep
+iteration, waiting on light records read as vector loads behind the iteration's stores
+(DESIGN.md round 5, item 8).  With RT_DEFER_STORES (deep levels) the columns "children" and
+"self" hold the own-shape tests and the appends + stores, in that order."""
 import ctypes as C
 import os
 import sys
