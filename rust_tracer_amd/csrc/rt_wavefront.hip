@@ -936,6 +936,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
 // Every shadow ray of the frame: PointLight::get_energy's scan + distance test, result as
 // a bit in the node record.
 
+#ifndef RT_LDS_LIGHTS
+#define RT_LDS_LIGHTS 64  // the shadow kernel stages up to this many lights in LDS (0: never)
+#endif
 #ifndef RT_SHADOW_WAVES
 #define RT_SHADOW_WAVES 5  // 96 VGPRs (round 4, light-buffer tiers: 5 / 6 / 8 waves 1236 / 1229 / 1196 Mpixels/s at K = 20, 3 runs each; round 3: 6 was +0.5 - 1% over 5)
 #endif
@@ -953,6 +956,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
         {
             float4* dst = rt_dyn_lds + 4 * S.n_bvh_nodes + ((S.graze_lane && S.graze_res) ? 8 * S.n_graze_blk : 0);
             for (int i = threadIdx.x; i < 4 * S.n_dsph_bvh; i += blockDim.x) dst[i] = S.dsph[i];
+        }
+        __syncthreads();
+    }
+    // the lights' positions and light-buffer bases in LDS (an entry's light is per lane): read
+    // with an LDS load, not a vector load that would wait for the previous lit-bit atomic
+    __shared__ float4 lds_lights[RT_LDS_LIGHTS > 0 ? RT_LDS_LIGHTS : 1];
+    const bool lights_lds = RT_LDS_LIGHTS > 0 && S.n_lights <= RT_LDS_LIGHTS;
+    if (lights_lds) {
+        for (int i = threadIdx.x; i < S.n_lights; i += blockDim.x) {
+            const LightRec L = light_at(S, i);
+            lds_lights[i] = make_float4(L.px, L.py, L.pz, __uint_as_float(L.lb_base));
         }
         __syncthreads();
     }
@@ -981,11 +995,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
             const uint32_t n = e >> P.light_bits, li = e & lmask;
             if (t < count) {
                 V3 ps = v3(q.x, q.y, q.z);
-                const LightRec L = light_at(S, (int)li);
-                V3 lpos = v3(L.px, L.py, L.pz);
+                float4 lq;
+                if (lights_lds) {
+                    lq = lds_lights[li];
+                } else {
+                    const LightRec L = light_at(S, (int)li);
+                    lq = make_float4(L.px, L.py, L.pz, __uint_as_float(L.lb_base));
+                }
+                V3 lpos = v3(lq.x, lq.y, lq.z);
                 V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
                 n_shadow++;
-                lit = !shadow_scan<LDS, decltype(cnt), true>(S, ps, ldir, lpos, cnt, lnodes, L.lb_base);
+                lit = !shadow_scan<LDS, decltype(cnt), true>(S, ps, ldir, lpos, cnt, lnodes, __float_as_uint(lq.w));
             }
             q = tn < count ? P.node_ps[en >> P.light_bits] : make_float4(0.f, 0.f, 0.f, 0.f);
             if (lit) atomicOr(&P.node_lit[n], 1u << li);
