@@ -561,9 +561,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         bool sh_entering = false;
         uint32_t sh_key = 0;
         constexpr bool DEFER = DEEP && RT_DEFER_STORES;  // (level 0 too: -4%, its inline scans spill the stores' data)
-        int32_t sh_kind = 0;             // DEFER: the hit shape's kind,
+        int32_t sh_kind = 0;             // the hit shape's kind,
         uint32_t own_ck = 0;             // ... its centre key (inside keys),
-        float sh_tu = 0.f, sh_tv = 0.f;  // ... the hit's texture coordinates (node record)
+        float sh_tu = 0.f, sh_tv = 0.f;  // DEFER: the hit's texture coordinates (node record)
         bool missed = false;             // ... and a miss whose stores are still to do
         uint32_t it_load = 0, it_scan0 = 0, it_self0 = 0;  // phase accounting (instrumented variant)
         uint32_t it_scan_self = 0;  // scan cycles spent inside the self phase (inline shadow scans)
@@ -646,14 +646,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 sh_n = h.n;
                 sh_entering = h.entering;
                 sh_key = bk;
-                if constexpr (DEFER) {  // read now: no load after the iteration's first store
+                // the shape's kind and centre key from its record now: no load after the
+                // iteration's first store (it would wait for that store's acknowledgement)
 #if RT_HIT_BULK
-                    sh_kind = SR.kind();
-                    own_ck = __float_as_uint(SR.w[0].z);
+                sh_kind = SR.kind();
+                own_ck = __float_as_uint(SR.w[0].z);
 #else
-                    sh_kind = S.shapes[bk >> 4].kind;
-                    own_ck = S.shapes[bk >> 4].center_key;
+                sh_kind = S.shapes[bk >> 4].kind;
+                own_ck = S.shapes[bk >> 4].center_key;
 #endif
+                if constexpr (DEFER) {
                     sh_tu = h.tu;
                     sh_tv = h.tv;
                 }
@@ -664,7 +666,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 }
                 const bool child_ok = level + 1 < P.depth;
                 if (inside_keys) {  // closed shapes: refraction enters from outside, reflection stays inside
-                    const int32_t kind = DEFER ? sh_kind : S.shapes[bk >> 4].kind;
+                    const int32_t kind = sh_kind;
                     const bool closed = kind == RT_SHAPE_SPHERE || kind == RT_SHAPE_CUBE;
                     refr_in = closed && h.entering;
                     refl_in = closed && !h.entering;
@@ -704,7 +706,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 Task T = {rro.x, rro.y, rro.z, rrd.x, rrd.y, rrd.z, (n << 1) | 0u, refl_in ? cpix | (own + 1u) : cpix};
                 P.tasks[slot] = T;
                 if (P.task_keys)
-                    P.task_keys[slot] = (refl_in ? inside_key(P, DEFER ? own_ck : S.shapes[own].center_key, rrd) : task_key(P, rro, rrd)) | fkey;
+                    P.task_keys[slot] = (refl_in ? inside_key(P, own_ck, rrd) : task_key(P, rro, rrd)) | fkey;
                 hit_flags |= F_HAS_R;
             } else {
                 atomicOr(P.overflow, 1u);
@@ -717,7 +719,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 Task T = {tro.x, tro.y, tro.z, trd.x, trd.y, trd.z, (n << 1) | 1u, refr_in ? cpix | (own + 1u) : cpix};
                 P.tasks[slot] = T;
                 if (P.task_keys)
-                    P.task_keys[slot] = (refr_in ? inside_key(P, DEFER ? own_ck : S.shapes[own].center_key, trd) : task_key(P, tro, trd)) | fkey;
+                    P.task_keys[slot] = (refr_in ? inside_key(P, own_ck, trd) : task_key(P, tro, trd)) | fkey;
                 hit_flags |= F_HAS_T;
             } else {
                 atomicOr(P.overflow, 1u);
@@ -737,7 +739,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 // the own shape can only shadow a light behind the offset point's
                 // surface (or any light, from inside a sphere); elsewhere the test is
                 // skipped (never deciding is always exact: the shadow pass decides)
-                const uint32_t own_kind = (uint32_t)(DEFER ? sh_kind : S.shapes[sh_key >> 4].kind);
+                const uint32_t own_kind = (uint32_t)sh_kind;
                 const bool own_any = own_kind == RT_SHAPE_SPHERE && !sh_entering;
                 const bool own_ok = own_kind == RT_SHAPE_SPHERE || own_kind == RT_SHAPE_TRIANGLE;
                 for (int li = 0; li < S.n_lights; ++li) {
