@@ -119,7 +119,9 @@ typedef struct rt_scene_desc {
     const rt_material* materials;
     uint32_t n_shapes;
     const rt_shape* shapes;
-    uint32_t n_lights;
+    uint32_t n_lights;             /* at most 32 (a node's shadow results are one 32-bit mask):
+                                      more -> RT_ERR_UNSUPPORTED from rt_scene_create*; the
+                                      reference has no limit (scene/mod.rs:189-206 loops over all) */
     const rt_light* lights;
     rt_color ambient;              /* Scene::set_ambient (mod.rs:50-52) */
 } rt_scene_desc;

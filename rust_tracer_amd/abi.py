@@ -17,6 +17,7 @@ STATUS_NAMES = {
     6: "RT_ERR_OUT_OF_MEMORY", 7: "RT_ERR_BAD_MATERIAL", 8: "RT_ERR_CAPACITY",
 }
 RT_ERR_INVALID_ARG = 1
+RT_ERR_UNSUPPORTED = 3
 RT_ERR_NO_DEVICE = 4
 RT_ERR_CAPACITY = 8
 RT_MAX_DEPTH = 1024

@@ -199,3 +199,13 @@ def test_scene_build_is_deterministic_over_host_threads(which):
     assert one == _layout_digest(desc, "build_threads=5")
     assert one == _layout_digest(desc, "")
     assert one[1] > 0
+
+
+def test_more_than_32_lights_are_refused_on_the_host():
+    """A node's shadow results are one 32-bit mask (rt_api.h rt_scene_desc.n_lights): 32
+    lights build, 33 are refused with RT_ERR_UNSUPPORTED before any device work."""
+    from tests.test_gpu_many_lights import _scene
+    assert _layout_digest(_scene(32), "lb_res=8")[1] > 0
+    dg, nb = C.c_uint64(), C.c_uint64()
+    st = abi.lib().rt_scene_layout_digest(_scene(33).ptr(), b"lb_res=8", C.byref(dg), C.byref(nb))
+    assert st == abi.RT_ERR_UNSUPPORTED
