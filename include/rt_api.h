@@ -54,6 +54,7 @@ enum {
  * ray trees end where every branch missed, which the level-synchronous pipeline detects:
  * rt_render stops enqueuing levels once one is empty). */
 #define RT_MAX_DEPTH 1024
+#define RT_MAX_LIGHTS 256   /* lights per scene (a shadow entry holds its light index beside its node) */
 
 /* ---------------------------------------------------------------- scene description */
 
@@ -119,9 +120,9 @@ typedef struct rt_scene_desc {
     const rt_material* materials;
     uint32_t n_shapes;
     const rt_shape* shapes;
-    uint32_t n_lights;             /* at most 32 (a node's shadow results are one 32-bit mask):
-                                      more -> RT_ERR_UNSUPPORTED from rt_scene_create*; the
-                                      reference has no limit (scene/mod.rs:189-206 loops over all) */
+    uint32_t n_lights;             /* at most RT_MAX_LIGHTS (more -> RT_ERR_UNSUPPORTED from
+                                      rt_scene_create*; the reference has no limit,
+                                      scene/mod.rs:189-206 loops over all) */
     const rt_light* lights;
     rt_color ambient;              /* Scene::set_ambient (mod.rs:50-52) */
 } rt_scene_desc;

@@ -1286,7 +1286,9 @@ struct Workspace {
     float4* node_ps = nullptr;       // [capacity] shadow-ray origins, texture u
     float4* node_n = nullptr;        // [capacity] normals, texture v
     float4* node_d = nullptr;        // [capacity] ray directions, parents
-    uint32_t* node_lit = nullptr;    // [capacity] unshadowed-light bits
+    uint32_t* node_lit = nullptr;    // [capacity] unshadowed-light bits (lights 0-31)
+    uint32_t* node_lit_hi = nullptr; // [(lit_words - 1) x capacity] lights 32 and up
+    uint32_t lit_words = 1;          // ceil(lights / 32) (rt_device.hpp WaveParams::lit_words)
     float4* node_ec = nullptr;       // [2 x capacity] children's colours
     uint32_t capacity = 0;
     uint32_t* shadow = nullptr;      // shadow queue
@@ -1447,7 +1449,7 @@ rt_status ensure_ws(rt_scene* s, size_t out_floats, size_t out8_bytes) {
 // the shadow queue from capacity * point lights.
 rt_status grow_node_pool(Workspace& w, uint32_t cap) {
     for (void** b : {(void**)&w.tasks, (void**)&w.node_flags, (void**)&w.node_ps, (void**)&w.node_n,
-                     (void**)&w.node_d, (void**)&w.node_lit, (void**)&w.node_ec, (void**)&w.node_dc,
+                     (void**)&w.node_d, (void**)&w.node_lit, (void**)&w.node_lit_hi, (void**)&w.node_ec, (void**)&w.node_dc,
                      (void**)&w.node_key, (void**)&w.node_pixel}) {
         if (*b) (void)hipFree(*b);
         *b = nullptr;
@@ -1459,6 +1461,7 @@ rt_status grow_node_pool(Workspace& w, uint32_t cap) {
     HIP_TRY(hipMalloc(&w.node_n, (size_t)cap * sizeof(float4)));
     HIP_TRY(hipMalloc(&w.node_d, (size_t)cap * sizeof(float4)));
     HIP_TRY(hipMalloc(&w.node_lit, (size_t)cap * sizeof(uint32_t)));
+    if (w.lit_words > 1) HIP_TRY(hipMalloc(&w.node_lit_hi, (size_t)(w.lit_words - 1) * cap * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&w.node_ec, 2 * (size_t)cap * sizeof(float4)));
     if (w.forest) {
         HIP_TRY(hipMalloc(&w.node_dc, 2 * (size_t)cap * sizeof(float4)));
@@ -1473,7 +1476,7 @@ rt_status grow_node_pool(Workspace& w, uint32_t cap) {
 void free_workspace(Workspace& w) {
     for (void* b : {(void*)w.out, (void*)w.out8, (void*)w.counters, (void*)w.work, (void*)w.tasks, (void*)w.shadow,
                     (void*)w.node_flags, (void*)w.levels, (void*)w.overflow, (void*)w.node_ps, (void*)w.node_n,
-                    (void*)w.node_d, (void*)w.node_lit, (void*)w.node_ec, (void*)w.task_keys, (void*)w.perm,
+                    (void*)w.node_d, (void*)w.node_lit, (void*)w.node_lit_hi, (void*)w.node_ec, (void*)w.task_keys, (void*)w.perm,
                     (void*)w.shadow_keys, (void*)w.shadow_sorted, (void*)w.sort_tmp, (void*)w.node_dc,
                     (void*)w.node_key, (void*)w.node_pixel, (void*)w.spp_buf, (void*)w.ctr_save})
         if (b) (void)hipFree(b);
@@ -1596,7 +1599,7 @@ rt_status prepare_scene(const rt_scene_desc* d, const Tune& tn, HostScene& H) {
                 return RT_ERR_INVALID_ARG;
         }
     }
-    if (d->n_lights > 32) return RT_ERR_UNSUPPORTED;  // shadow results are a 32-bit mask per node
+    if (d->n_lights > RT_MAX_LIGHTS) return RT_ERR_UNSUPPORTED;  // a shadow entry's light index beside its node
     std::vector<LightRec>& lights = H.lights;
     lights.resize(d->n_lights);
     for (uint32_t i = 0; i < d->n_lights; i++) {
@@ -1945,7 +1948,7 @@ uint64_t rt_scene_workspace_bytes(const rt_scene* s) {
     if (!s) return 0;
     const Workspace& w = s->ws;
     uint64_t b = (uint64_t)w.out_floats * 4 + w.out8_bytes + 4 * 8 + 64;
-    b += (uint64_t)w.capacity * (sizeof(Task) + 4 + 3 * 16 + 4 + 2 * 16);  // tasks, node arrays
+    b += (uint64_t)w.capacity * (sizeof(Task) + 4 + 3 * 16 + 4 * w.lit_words + 2 * 16);  // tasks, node arrays
     if (w.forest) b += (uint64_t)w.capacity * (2 * 16 + 4 + 4);
     b += (uint64_t)w.sort_capacity * 8;                                      // task keys, permutation
     b += (uint64_t)w.shadow_capacity * 4 + (uint64_t)w.sort_shadow_capacity * 8;
@@ -2185,8 +2188,10 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     if (tn.node_cap) want = std::max<uint64_t>(total + 1, tn.node_cap);  // test knob
     if (&w == &s->ws) want = std::max<uint64_t>(want, s->pool_floor);
     if (want > max_cap) want = max_cap;
-    if (w.capacity < want) {  // grows only (rt_render may have grown it after an overflow)
-        rt_status st = grow_node_pool(w, (uint32_t)want);
+    const uint32_t lit_words = ((uint32_t)s->S.n_lights + 31u) / 32u > 1u ? ((uint32_t)s->S.n_lights + 31u) / 32u : 1u;
+    if (w.capacity < want || w.lit_words != lit_words) {  // grows only (rt_render may have grown it after an overflow)
+        w.lit_words = lit_words;
+        rt_status st = grow_node_pool(w, (uint32_t)std::max<uint64_t>(want, w.capacity));
         if (st != RT_OK) return st;
     }
     if (!w.levels) {
@@ -2366,6 +2371,8 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     p.node_n = w.node_n;
     p.node_d = w.node_d;
     p.node_lit = w.node_lit;
+    p.node_lit_hi = w.node_lit_hi;
+    p.lit_words = w.lit_words;
     p.node_ec = w.node_ec;
     p.levels = w.levels;
     p.overflow = w.overflow;
@@ -2410,6 +2417,8 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     // enqueued without a host round trip (levels past the deepest non-empty one are no-ops).
     HIP_TRY(launch_wave_init(w.levels, RT_LEVEL_TABLE_WORDS, p.total_items, sample == 0 ? w.overflow : nullptr,
                              stream));
+    if (w.lit_words > 1)  // lights 32 and up: their bits start at 0 (the trace kernel stores word 0 only)
+        HIP_TRY(hipMemsetAsync(w.node_lit_hi, 0, (size_t)(w.lit_words - 1) * w.capacity * sizeof(uint32_t), stream));
     HIP_TRY(launch_wave_trace(p, 0, tb, stream, s->occ_trace_each, s->occ_trace));
     // every level's queue is sorted (leaving any level unsorted lost: DESIGN.md)
     const uint64_t sort_levels = ~0ull;

@@ -154,7 +154,7 @@ struct Task {
 //   node_ps[n]     {shadow-ray origin p + 0.0002 n (render.rs:147), texture u}
 //   node_n[n]      {hit normal, texture v}
 //   node_d[n]      {the ray's direction, parent = (parent node << 1) | slot}
-//   node_lit[n]    bit l: point light l is NOT shadowed
+//   node_lit[n]    bit l: point light l is NOT shadowed (lights 32 and up: node_lit_hi)
 //   node_ec[2n+s]  colour the node's child in slot s (0 reflected, 1 refracted) reports
 // That is 52 B written per hit node.  Everything else render.rs:57-100 needs (eye_dir,
 // n1 / n2, the material's textures at (u, v), the reflected direction, Schlick weights,
@@ -205,7 +205,10 @@ struct WaveParams {
     float4* node_ps;                   // [capacity]
     float4* node_n;                    // [capacity]
     float4* node_d;                    // [capacity]
-    uint32_t* node_lit;                // [capacity]: unshadowed-light bits
+    uint32_t* node_lit;                // [capacity]: unshadowed-light bits of lights 0-31
+    uint32_t* node_lit_hi;             // [(lit_words - 1) x capacity]: lights 32 and up, word w of
+                                       // node n at (lit_words - 1) n + w - 1 (bit l % 32: light l)
+    uint32_t lit_words;                // ceil(lights / 32), at least 1
     float4* node_ec;                   // [2 x capacity]: children's colours
     uint32_t* shadow;                  // [shadow_capacity]: (node << light_bits) | light
     uint32_t light_bits;               // bits of the light index in a shadow entry

@@ -358,6 +358,15 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, uint32_t n, u
     return wave_append_end(wave_append_begin(counter, n, lane));
 }
 
+// A node's unshadowed-light word for light li: node_lit[n] for lights 0-31, node_lit_hi for
+// the rest (scenes of more than 32 lights)
+__device__ __forceinline__ uint32_t* lit_word(const WaveParams& P, uint32_t n, uint32_t li) {
+    return li < 32u ? &P.node_lit[n] : &P.node_lit_hi[(size_t)(P.lit_words - 1u) * n + ((li >> 5) - 1u)];
+}
+__device__ __forceinline__ const uint32_t* lit_more(const WaveParams& P, uint32_t n) {
+    return P.node_lit_hi + (size_t)(P.lit_words > 1u ? P.lit_words - 1u : 0u) * n;
+}
+
 // The shading point's own shape, tested first for its shadow rays (trace kernel): the
 // same arithmetic the scan runs for it (sph_general / the triangle test; bit-identical
 // results up to the sign of a zero t, which no distance test can see).  Cubes are left
@@ -731,6 +740,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         // after the node record and the children are out, so that little stays live
         // across the shadow scans (DEFER: before the appends and every store)
         uint32_t lit_pre = 0u;
+        // lights 32 and up (scenes of more than 32 lights) are never decided here: their
+        // shadow rays all go to the shadow queue, their bits start at 0 (node_lit words 1..)
+        const int lights32 = min(S.n_lights, 32);
+        // (a 64-bit shift: lights 32 and up read a 0 bit, undecided)
+        auto undecided = [&](int li) { return !(((uint64_t)decided >> min(li, 63)) & 1u); };
+        auto store_lit = [&]() { P.node_lit[n] = lit_pre; };  // (node_lit_hi: zeroed per pass by the host)
         auto self_tests = [&]() {
         if (hit) {
             if constexpr (CntT::kCount) it_scan_self = cnt.cyc_scan;
@@ -742,7 +757,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 const uint32_t own_kind = (uint32_t)sh_kind;
                 const bool own_any = own_kind == RT_SHAPE_SPHERE && !sh_entering;
                 const bool own_ok = own_kind == RT_SHAPE_SPHERE || own_kind == RT_SHAPE_TRIANGLE;
-                for (int li = 0; li < S.n_lights; ++li) {
+                for (int li = 0; li < lights32; ++li) {
                     const LightRec L = light_at(S, li);
                     if (L.kind != RT_LIGHT_POINT) continue;
                     const V3 lpos = v3(L.px, L.py, L.pz);
@@ -761,7 +776,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 n_pre += (uint32_t)__builtin_popcount(decided);
             }
             if (!DEEP && level < P.inline_levels) {  // the level's remaining shadow rays, right here
-                for (int li = 0; li < S.n_lights; ++li) {
+                for (int li = 0; li < lights32; ++li) {
                     const LightRec L = light_at(S, li);
                     if (L.kind != RT_LIGHT_POINT || ((decided >> li) & 1u)) continue;
                     const V3 lpos = v3(L.px, L.py, L.pz);
@@ -773,7 +788,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
             }
             RT_T1(CntT, cnt, cyc_self, t_self);
             if constexpr (CntT::kCount) it_scan_self = cnt.cyc_scan - it_scan_self;
-            if constexpr (!DEFER) P.node_lit[n] = lit_pre;
+            if constexpr (!DEFER) store_lit();
         }
         };
         // ---- one shadow entry per point light, grouped by light within the wave
@@ -789,7 +804,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 uint32_t total = 0;
                 for (int li = 0; li < S.n_lights; ++li)
                     if (light_at(S, li).kind == RT_LIGHT_POINT)
-                        total += (uint32_t)__builtin_popcountll(__ballot(hit && !((decided >> li) & 1u)));
+                        total += (uint32_t)__builtin_popcountll(__ballot(hit && undecided(li)));
                 s_first = (uint32_t)__builtin_ctzll(hits);
 #if RT_DIAG_ENTRIES == 2  // diagnostic: no append (slots overlap; the frame is wrong, the trace's timing is not)
                 s_raw = (n - lane) * 3u % (P.shadow_capacity - 256u);
@@ -811,7 +826,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                                               : 0.f;
             for (int li = 0; li < S.n_lights; ++li) {
                 if (light_at(S, li).kind != RT_LIGHT_POINT) continue;
-                const bool want = hit && !((decided >> li) & 1u);
+                const bool want = hit && undecided(li);
                 const uint64_t m = __ballot(want);
                 const uint32_t slot = sbase + group + (uint32_t)__builtin_popcountll(m & lanemask_lt());
                 group += (uint32_t)__builtin_popcountll(m);
@@ -870,7 +885,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 P.node_ps[n] = make_float4(sh_ps.x, sh_ps.y, sh_ps.z, sh_tu);
                 P.node_n[n] = make_float4(sh_n.x, sh_n.y, sh_n.z, sh_tv);
                 P.node_d[n] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(parent));
-                P.node_lit[n] = lit_pre;
+                store_lit();
             } else if (missed) {
                 P.node_flags[n] = NODE_MISS;
                 if (level > 0) {
@@ -1010,7 +1025,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
                 lit = !shadow_scan<LDS, decltype(cnt), true>(S, ps, ldir, lpos, cnt, lnodes, __float_as_uint(lq.w));
             }
             q = tn < count ? P.node_ps[en >> P.light_bits] : make_float4(0.f, 0.f, 0.f, 0.f);
-            if (lit) atomicOr(&P.node_lit[n], 1u << li);
+            if (lit) atomicOr(lit_word(P, n, li), 1u << (li & 31u));
             base += stride;
             t = tn;
             e = en;
@@ -1033,7 +1048,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
                 V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
                 n_shadow++;
                 if (!shadow_scan<LDS, decltype(cnt), true>(S, ps, ldir, lpos, cnt, lnodes, L.lb_base))
-                    atomicOr(&P.node_lit[n], 1u << li);
+                    atomicOr(lit_word(P, n, li), 1u << (li & 31u));
             }
         }
     }
@@ -1082,8 +1097,9 @@ __device__ __forceinline__ NodeIn node_in(float4 a, float4 b, float4 c, uint32_t
 // half vector norm(ne + norm(ldir)) cannot degenerate (ldir not within ~8 degrees of -ne;
 // exactly opposite vectors give 0 / 0 = NaN, which the reference propagates).  A shadowed
 // light's direction is finite: a NaN direction hits nothing, so it is never shadowed.
+// (lit_more: the node's node_lit_hi words, lights 32 and up)
 __device__ __forceinline__ V3 light_sum(const DevScene& S, const MatRec& M, const NodeIn& q, V3 ne, uint32_t litmask,
-                                        V3 kd, V3 ks, float power) {
+                                        V3 kd, V3 ks, float power, const uint32_t* lit_more) {
     V3 lsum = v3(0.f, 0.f, 0.f);
     const bool dark_ok = S.dark_skip && M.dark_zero;
     for (int li = 0; li < S.n_lights; ++li) {
@@ -1092,7 +1108,7 @@ __device__ __forceinline__ V3 light_sum(const DevScene& S, const MatRec& M, cons
         V3 E = v3(L.r, L.g, L.b);
         if (L.kind == RT_LIGHT_POINT) {
             const V3 raw = sub(v3(L.px, L.py, L.pz), q.ps);
-            if (!((litmask >> li) & 1u)) {
+            if (!(((li < 32 ? litmask : lit_more[(li >> 5) - 1]) >> (li & 31)) & 1u)) {
                 if (dark_ok) {
                     const float r2 = len2(raw), c = dot(raw, ne);
                     if (r2 > 1e-30f && r2 < 1e30f && !(c < 0.f && c * c > 0.98f * r2)) continue;
@@ -1175,7 +1191,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_COMBINE_
             const V3 kd = tex_eval(M.diffuse, q.h.tu, q.h.tv);
             const V3 ks = tex_eval(M.specular, q.h.tu, q.h.tv);
             const V3 ne = norm(q.h.eye);
-            const V3 lsum = light_sum(S, M, q, ne, litmask, kd, ks, M.power);
+            const V3 lsum = light_sum(S, M, q, ne, litmask, kd, ks, M.power, lit_more(P, n));
             // ambient = mat.ambient(tex) * scene.ambient (render.rs:57), then + lights
             const V3 loc = add(v3(ka.x * S.amb_r, ka.y * S.amb_g, ka.z * S.amb_b), lsum);
             Frame f;
@@ -1261,7 +1277,7 @@ __global__ __launch_bounds__(256) void forest_shade_level_kernel(WaveParams P, u
         const NodeIn q = node_in(P.node_ps[n], P.node_n[n], P.node_d[n], flags, M);
         const V3 kd = tex_eval(M.diffuse, q.h.tu, q.h.tv), ks = tex_eval(M.specular, q.h.tu, q.h.tv);
         const V3 ne = norm(q.h.eye);
-        const V3 lsum = light_sum(S, M, q, ne, P.node_lit[n], kd, ks, M.power);
+        const V3 lsum = light_sum(S, M, q, ne, P.node_lit[n], kd, ks, M.power, lit_more(P, n));
         const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
         const bool has_r = (flags & F_HAS_R) != 0u, has_t = (flags & F_HAS_T) != 0u;
         const V3 er = xyz(has_r ? P.node_ec[2u * n] : zero), dr = xyz(has_r ? P.node_dc[2u * n] : zero);

@@ -201,11 +201,11 @@ def test_scene_build_is_deterministic_over_host_threads(which):
     assert one[1] > 0
 
 
-def test_more_than_32_lights_are_refused_on_the_host():
-    """A node's shadow results are one 32-bit mask (rt_api.h rt_scene_desc.n_lights): 32
-    lights build, 33 are refused with RT_ERR_UNSUPPORTED before any device work."""
+def test_more_than_max_lights_are_refused_on_the_host():
+    """rt_api.h RT_MAX_LIGHTS (256): a shadow entry holds its light index beside its node.
+    256 lights build, 257 are refused with RT_ERR_UNSUPPORTED before any device work."""
     from tests.test_gpu_many_lights import _scene
-    assert _layout_digest(_scene(32), "lb_res=8")[1] > 0
+    assert _layout_digest(_scene(256), "lb_res=4")[1] > 0
     dg, nb = C.c_uint64(), C.c_uint64()
-    st = abi.lib().rt_scene_layout_digest(_scene(33).ptr(), b"lb_res=8", C.byref(dg), C.byref(nb))
+    st = abi.lib().rt_scene_layout_digest(_scene(257).ptr(), b"lb_res=4", C.byref(dg), C.byref(nb))
     assert st == abi.RT_ERR_UNSUPPORTED

@@ -1,8 +1,9 @@
-"""GPU tests of scenes with many point lights (mod.rs:189-206 per light).  A node's shadow
-results are one 32-bit mask, so a scene holds at most 32 lights (rt_api.h rt_scene_desc; more:
-RT_ERR_UNSUPPORTED at creation, nothing rendered).  At that maximum -- every light in the shadow
-kernel's LDS copy, the trace kernel's own-shape tests and shadow-entry keys looping over all 32,
-6-bit light fields in the shadow queue -- the frame and counters meet the oracle's."""
+"""GPU tests of scenes with many point lights (mod.rs:189-206 per light).  Lights 0-31 keep
+their shadow results in each node's node_lit word, lights 32 and up in node_lit_hi (zeroed per
+pass); the trace kernel's own-shape tests and inline scans decide lights 0-31 only, the rest
+always go to the shadow queue; the shadow kernel keeps up to 64 lights' positions in LDS
+(rt_wavefront.hip RT_LDS_LIGHTS) and reads the rest from the scene's records.  Frames and
+counters against the oracle at 32, 33, 64 and 70 lights; RT_MAX_LIGHTS + 1 lights are refused."""
 import numpy as np
 import pytest
 
@@ -25,21 +26,24 @@ def _scene(n_lights, seed=5):
     return d
 
 
-@pytest.mark.parametrize("tuning", [None, "lb_res=16"])
-def test_thirty_two_lights_match_the_oracle(tuning):
-    desc = _scene(32)
+@pytest.mark.parametrize("n_lights,tuning", [(32, None), (33, None), (64, "lb_res=16"), (70, "lb_res=16"),
+                                             (70, "lb_res=16,inline_shadow=0,self_shadow=0")])
+def test_many_lights_match_the_oracle(n_lights, tuning):
+    desc = _scene(n_lights)
     w, h, depth = 96, 72, 4
     ref, rcnt = OracleScene(desc).render(w, h, depth, threads=8)
     s = DeviceScene(desc, tuning=tuning)
     try:
         img, cnt, _, _ = s.render(w, h, depth)
+        img2, cnt2, _, _ = s.render(w, h, depth)  # a second pass on the same pools
     finally:
         s.close()
     compare(img, ref)
     assert cnt == rcnt
+    assert np.array_equal(img.view(np.uint32), img2.view(np.uint32)) and cnt2 == cnt
 
 
-def test_thirty_three_lights_are_refused():
+def test_too_many_lights_are_refused():
     with pytest.raises(RtError) as e:
-        DeviceScene(_scene(33))
+        DeviceScene(_scene(257))  # rt_api.h RT_MAX_LIGHTS + 1
     assert e.value.status == abi.RT_ERR_UNSUPPORTED
