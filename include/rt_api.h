@@ -400,6 +400,7 @@ int32_t rt_scene_uses_bvh(const rt_scene* scene);
  * render.rs) once and keeps every intersection on the device. */
 typedef struct rt_forest rt_forest;
 rt_status rt_forest_create(rt_scene* scene, const rt_camera* camera, uint32_t depth, rt_forest** out);
+/* A forest uses its scene's stream and materials: destroy it before its scene. */
 rt_status rt_forest_destroy(rt_forest* forest);
 
 /* render_forest(&forest, &mut buffer, ambient) (render_tree.rs:121-127, render_ray_tree
@@ -440,8 +441,12 @@ rt_status rt_scene_set_material(rt_scene* scene, uint32_t index, const rt_materi
  *    the handle, its stream, workspace, band shares and devices stay valid; *what = 2.
  * Renders on the handle must not run concurrently with it; it waits for the handle's streams.
  * A stream-ordered render's unreported status (rt_scene_sync_status) is returned first and
- * the update is then not made.  Forests created before a rebuild describe the old scene.
- * `what` may be NULL.  Errors of the rebuild (e.g. RT_ERR_SINGULAR_MATRIX) leave the handle
+ * the update is then not made.  A forest created before a rebuild (*what = 2) keeps its trees
+ * (rt_forest_tree_sizes / _trees_with / _counters still answer for them) but can no longer be
+ * shaded: rt_forest_render / _render_filter return RT_ERR_INVALID_ARG -- its nodes hold the old
+ * scene's material indices and light count; create a new forest.  Material edits in place
+ * (*what = 1) keep forests valid and are seen by their next shade.  Every edited material is
+ * validated before the first is applied.  `what` may be NULL.  Errors of the rebuild (e.g. RT_ERR_SINGULAR_MATRIX) leave the handle
  * rendering its previous scene. */
 rt_status rt_scene_update(rt_scene* scene, const rt_scene_desc* desc, int32_t* what);
 

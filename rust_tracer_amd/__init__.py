@@ -6,6 +6,7 @@ It mirrors the reference's seam ``render(camera, scene, buffer, depth)``
 CPU render path here: without the built library every call raises.
 """
 import ctypes as C
+import weakref
 import math
 
 import numpy as np
@@ -295,6 +296,10 @@ class DeviceScene:
 
     def close(self):
         if self.h:
+            # forests of this scene first: rt_forest_destroy uses its scene's stream.  (A cycle
+            # holding both -- e.g. a test frame kept by a traceback -- is finalised in any order)
+            for f in list(getattr(self, "_forests", ())):
+                f.close()
             self._L.rt_scene_destroy(self.h)
             self.h = C.c_void_p()
 
@@ -441,6 +446,9 @@ class DeviceForest:
         self.h = C.c_void_p()
         cam = camera(x_res, y_res)
         check(self._L.rt_forest_create(scene.h, C.byref(cam), depth, C.byref(self.h)), "rt_forest_create")
+        if not hasattr(scene, "_forests"):
+            scene._forests = weakref.WeakSet()
+        scene._forests.add(self)
 
     def close(self):
         if self.h:

@@ -1374,6 +1374,9 @@ struct rt_scene {
     std::vector<rt_shape> d_shapes;
     std::vector<rt_light> d_lights;
     rt_color d_ambient{0.f, 0.f, 0.f};
+    // bumped by every rebuild rt_scene_update adopts: a forest made before it refuses to shade
+    // (its trees hold the old scene's material indices and light count)
+    uint64_t generation = 0;
 };
 
 rt_multi_state*& rt_scene_multi(rt_scene* s) { return s->multi; }
@@ -1874,6 +1877,10 @@ void commit_scene_data(rt_scene* dst, const rt_scene* src, void* mem) {
     // deeper ray trees may need a larger pool than any pass checked so far: check again
     dst->checked_items = 0;
     dst->checked_depth = 0;
+    // the kernels' LDS staging depends on the scene (node records, grazing normals, sphere
+    // pairs): the persistent grids are sized from the occupancy measured again
+    dst->occ_trace = 0;
+    dst->generation++;
     if (new_lights) free_workspace(dst->ws);
 }
 
@@ -2992,6 +2999,7 @@ rt_status rt_render_spp(const rt_scene* scene, const rt_camera* cam, uint32_t de
 
 struct rt_forest {
     rt_scene* s = nullptr;
+    uint64_t generation = 0;    // the scene's rt_scene::generation at creation
     rt_camera cam{};
     uint32_t depth = 0;
     Workspace ws;
@@ -3011,6 +3019,9 @@ namespace {
 size_t forest_pixels(const rt_forest* f) { return (size_t)f->cam.x_res * f->cam.y_res; }
 
 rt_status forest_shade(rt_forest* f, const uint8_t* dirty) {
+    // a rebuild since the forest was made: its nodes' material indices and lit words describe
+    // the old scene, which the handle no longer holds (rt_api.h rt_scene_update)
+    if (f->generation != f->s->generation) return RT_ERR_INVALID_ARG;
     WaveParams p = f->p;
     p.S = f->s->S;  // current material table
     p.dirty = dirty;
@@ -3053,6 +3064,7 @@ rt_status rt_forest_create(rt_scene* s, const rt_camera* cam, uint32_t depth, rt
     std::unique_ptr<rt_forest> f(new (std::nothrow) rt_forest());
     if (!f) return RT_ERR_OUT_OF_MEMORY;
     f->s = s;
+    f->generation = s->generation;
     f->cam = *cam;
     f->depth = depth;
     f->ws.forest = true;
@@ -3183,12 +3195,17 @@ rt_status rt_scene_set_material(rt_scene* s, uint32_t index, const rt_material* 
     // on the handle's stream, waited for: the next render on any caller stream sees the edit
     HIP_TRY(hipMemcpyAsync(const_cast<MatRec*>(s->S.mats) + index, &M, sizeof(M), hipMemcpyHostToDevice, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    // the handle's own copy is written first: rt_scene_update compares against it, so an edit
+    // that reached this device must be recorded even if a band share or device below fails
+    s->d_mats[index] = *m;
     if (s->split) {
         rt_status e = rt_multi_each(s->split, [&](rt_scene* c) { return rt_scene_set_material(c, index, m); });
         if (e != RT_OK) return e;
     }
-    if (s->multi) return rt_multi_each(s->multi, [&](rt_scene* c) { return rt_scene_set_material(c, index, m); });
-    s->d_mats[index] = *m;
+    if (s->multi) {
+        rt_status e = rt_multi_each(s->multi, [&](rt_scene* c) { return rt_scene_set_material(c, index, m); });
+        if (e != RT_OK) return e;
+    }
     return RT_OK;
 }
 
@@ -3203,34 +3220,41 @@ rt_status rt_scene_update(rt_scene* s, const rt_scene_desc* d, int32_t* what) {
                           same(d->shapes, s->d_shapes.data(), d->n_shapes * sizeof(rt_shape)) &&
                           same(d->lights, s->d_lights.data(), d->n_lights * sizeof(rt_light)) &&
                           same(&d->ambient, &s->d_ambient, sizeof(rt_color));
+    std::vector<uint32_t> edits;
+    bool kinds = true;
     if (geometry) {
-        // material edits of the same kind (the GUI's sliders, gui.rs:221-236) in place
-        std::vector<uint32_t> edits;
-        bool kinds = true;
         for (uint32_t i = 0; i < d->n_materials; i++)
             if (!same(&d->materials[i], &s->d_mats[i], sizeof(rt_material))) {
                 edits.push_back(i);
                 kinds = kinds && d->materials[i].kind == s->d_mats[i].kind;
             }
         if (edits.empty()) return RT_OK;
-        if (kinds) {
-            for (uint32_t i : edits) {
-                rt_status st = rt_scene_set_material(s, i, &d->materials[i]);
-                if (st != RT_OK) return st;
-            }
-            if (what) *what = 1;
-            return RT_OK;
-        }
     }
-    // anything else: the scene is rebuilt (same device and tuning) and adopted in place, so the
-    // caller's handle, its stream, workspace and band shares stay valid.  A stream-ordered
-    // render's unreported status is returned first (the update is then not made).
+    // a stream-ordered render's unreported status is returned first (the update is then not
+    // made), on every path that changes the scene
     rt_status st = rt_scene_sync_status(s);
     if (st != RT_OK) return st;
     if (s->multi) {
         st = rt_multi_each(s->multi, [](rt_scene* c) { return rt_scene_sync_status(c); });
         if (st != RT_OK) return st;
     }
+    if (geometry && kinds) {
+        // material edits of the same kind (the GUI's sliders, gui.rs:221-236) in place; every
+        // edited material is validated before the first is applied (no partial update)
+        for (uint32_t i : edits) {
+            MatRec M;
+            st = mat_rec(d->materials[i], M, s->normal_max);
+            if (st != RT_OK) return st;
+        }
+        for (uint32_t i : edits) {
+            st = rt_scene_set_material(s, i, &d->materials[i]);
+            if (st != RT_OK) return st;
+        }
+        if (what) *what = 1;
+        return RT_OK;
+    }
+    // anything else: the scene is rebuilt (same device and tuning) and adopted in place, so the
+    // caller's handle, its stream, workspace and band shares stay valid
     rt_scene* fresh = nullptr;
     st = create_handle(d, s->device, s->tune, &fresh);
     if (st != RT_OK) return st;

@@ -141,3 +141,52 @@ def test_size_check_refused_inside_stream_capture():
     # outside the capture the same pass runs (and is checked)
     s.render_bands_ex_async([cam], depth + 4, 8, 0, 1, d_rgb.data_ptr(), 0, 0, stream.cuda_stream)
     s.sync_status()
+
+
+def test_multi_handle_material_edit_and_revert():
+    """A material edit in place on a multi-device handle, then reverted (a GUI slider A -> B ->
+    A): the handle records each edit, so the revert is applied too -- every frame equals a fresh
+    handle of the same description (the multi branch used to skip the record)."""
+    w, h, depth = 192, 108, 6
+    base = SceneDesc.synth_config(3).editable()
+    m = DeviceScene(base, devices=[0, 0])
+    a, _, _, _ = m.render(w, h, depth)
+    edited = SceneDesc.synth_config(3).editable()
+    k = next(s.material for s in edited.shapes if s.kind == 0)  # the first sphere's material
+    mat = edited.materials[k]
+    mat.diffuse.color.r = float(np.float32(mat.diffuse.color.r * 0.5))
+    mat.reflectivity = float(np.float32(0.7 if mat.reflectivity < 0.6 else 0.2))
+    assert m.update(edited) == "materials"
+    b, _, _, _ = m.render(w, h, depth)
+    want_b, _, _, _ = DeviceScene(edited, device=0).render(w, h, depth)
+    assert same_bits(b, want_b) and not same_bits(b, a)
+    assert m.update(base) == "materials"
+    c, _, _, _ = m.render(w, h, depth)
+    assert same_bits(c, a)
+
+
+def test_forest_refuses_to_shade_after_rebuild():
+    """A forest made before a rebuild keeps its trees (sizes, ids) but refuses to shade them
+    with the new scene (RT_ERR_INVALID_ARG); a material edit in place keeps it valid."""
+    from rust_tracer_amd import RtError
+    base = SceneDesc.my_scene().editable()
+    s = DeviceScene(base, device=0)
+    f = s.forest(64, 48, 4)
+    img = f.render()
+    sizes = f.tree_sizes()
+    d2 = base.editable()
+    d2.materials[0].reflectivity = float(np.float32(d2.materials[0].reflectivity + 0.25))
+    assert s.update(d2) == "materials"
+    f.render()  # in-place edits: the forest shades with them
+    d3 = _edited(d2)
+    assert s.update(d3) == "rebuilt"
+    with pytest.raises(RtError) as e:
+        f.render()
+    assert e.value.status == 1
+    with pytest.raises(RtError):
+        f.render_filter([0], img)
+    assert np.array_equal(f.tree_sizes(), sizes)
+    g = s.forest(64, 48, 4)  # a new forest of the rebuilt scene shades
+    assert g.render().shape == img.shape
+    g.close()
+    f.close()
