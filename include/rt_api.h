@@ -54,7 +54,9 @@ enum {
  * ray trees end where every branch missed, which the level-synchronous pipeline detects:
  * rt_render stops enqueuing levels once one is empty). */
 #define RT_MAX_DEPTH 1024
-#define RT_MAX_LIGHTS 256   /* lights per scene (a shadow entry holds its light index beside its node) */
+#define RT_MAX_LIGHTS 65536 /* lights per scene (the shadow-queue keys hold a 16-bit light index; above
+                               256 lights a shadow entry takes 8 B: node and light side by side).
+                               Each node keeps one bit per light: ceil(lights / 32) words */
 
 /* ---------------------------------------------------------------- scene description */
 

@@ -1292,6 +1292,7 @@ struct Workspace {
     float4* node_ec = nullptr;       // [2 x capacity] children's colours
     uint32_t capacity = 0;
     uint32_t* shadow = nullptr;      // shadow queue
+    uint32_t* shadow_light = nullptr;  // wide entries (> 256 lights): each entry's light
     uint32_t shadow_capacity = 0;
     uint32_t* levels = nullptr;      // RT_LEVEL_TABLE_WORDS words
     uint32_t* overflow = nullptr;    // [0] this pass's queue overflows, [1] sticky (rt_scene_sync_status)
@@ -1412,13 +1413,18 @@ rt_status select_device(int32_t device, int* resolved) {
     return RT_OK;
 }
 
-// Bits of the light index in a shadow entry ((node << bits) | light, rt_wavefront.hip).
-uint32_t light_bits(const rt_scene* s) {
+// Shadow entries: packed (node << bits) | light in 4 B for scenes of up to 256 lights (8 bits);
+// "wide" above that -- the node in shadow[], its light in shadow_light[] (rt_device.hpp), so that
+// a scene of many lights keeps the full node pool (RT_MAX_LIGHTS).
+constexpr uint32_t PACKED_LIGHT_BITS = 8;
+uint32_t light_index_bits(const rt_scene* s) {
     uint32_t b = 1;
     while ((1u << b) < (uint32_t)s->S.n_lights) b++;
     return b;
 }
-// Largest node pool: node indices must fit a shadow entry beside the light index (and
+bool wide_entries(const rt_scene* s) { return light_index_bits(s) > PACKED_LIGHT_BITS; }
+uint32_t light_bits(const rt_scene* s) { return wide_entries(s) ? 0u : light_index_bits(s); }
+// Largest node pool: node indices must fit a packed shadow entry beside the light index (and
 // (node << 1) | slot a parent reference).
 uint64_t pool_cap_limit(const rt_scene* s) { return std::min<uint64_t>(1ull << (32 - light_bits(s)), 1ull << 30); }
 
@@ -1478,6 +1484,7 @@ rt_status grow_node_pool(Workspace& w, uint32_t cap) {
 // Frees every device / pinned buffer of a workspace.
 void free_workspace(Workspace& w) {
     for (void* b : {(void*)w.out, (void*)w.out8, (void*)w.counters, (void*)w.work, (void*)w.tasks, (void*)w.shadow,
+                    (void*)w.shadow_light,
                     (void*)w.node_flags, (void*)w.levels, (void*)w.overflow, (void*)w.node_ps, (void*)w.node_n,
                     (void*)w.node_d, (void*)w.node_lit, (void*)w.node_lit_hi, (void*)w.node_ec, (void*)w.task_keys, (void*)w.perm,
                     (void*)w.shadow_keys, (void*)w.shadow_sorted, (void*)w.sort_tmp, (void*)w.node_dc,
@@ -1602,7 +1609,7 @@ rt_status prepare_scene(const rt_scene_desc* d, const Tune& tn, HostScene& H) {
                 return RT_ERR_INVALID_ARG;
         }
     }
-    if (d->n_lights > RT_MAX_LIGHTS) return RT_ERR_UNSUPPORTED;  // a shadow entry's light index beside its node
+    if (d->n_lights > RT_MAX_LIGHTS) return RT_ERR_UNSUPPORTED;  // the shadow keys' light index (16 bits)
     std::vector<LightRec>& lights = H.lights;
     lights.resize(d->n_lights);
     for (uint32_t i = 0; i < d->n_lights; i++) {
@@ -1958,7 +1965,7 @@ uint64_t rt_scene_workspace_bytes(const rt_scene* s) {
     b += (uint64_t)w.capacity * (sizeof(Task) + 4 + 3 * 16 + 4 * w.lit_words + 2 * 16);  // tasks, node arrays
     if (w.forest) b += (uint64_t)w.capacity * (2 * 16 + 4 + 4);
     b += (uint64_t)w.sort_capacity * 8;                                      // task keys, permutation
-    b += (uint64_t)w.shadow_capacity * 4 + (uint64_t)w.sort_shadow_capacity * 8;
+    b += (uint64_t)w.shadow_capacity * (w.shadow_light ? 8 : 4) + (uint64_t)w.sort_shadow_capacity * 8;
     b += (uint64_t)w.sort_tmp_words * 4;
     b += (uint64_t)w.spp_buf_floats * 4;
     if (w.levels) b += RT_LEVEL_TABLE_WORDS * 4 + 64;
@@ -2213,14 +2220,22 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     // shadow queue: at most one entry per point light per hit node; Tune::shadow_factor
     // (default 2) entries per node slot, at most the point lights (config 3 queues 2.0 per
     // traced node: the trace kernel decides the rest; overflow reported like the node pool's)
-    uint64_t want_sh = std::min<uint64_t>(
-        (uint64_t)((double)w.capacity * std::min<double>(tn.shadow_factor, (double)s->n_point_lights)), 0x7FFFFFFFu);
+    // Scenes of more than 32 point lights: lights 32 and up are never decided by the trace
+    // kernel, so a hit queues about one entry per point light -- the queue is sized for that
+    const double sh_per_node = s->n_point_lights > 32u ? (double)s->n_point_lights
+                                                        : std::min<double>(tn.shadow_factor, (double)s->n_point_lights);
+    uint64_t want_sh = std::min<uint64_t>((uint64_t)((double)w.capacity * sh_per_node), 0x7FFFFFFFu);
     if (want_sh == 0) want_sh = 1;
-    if (w.shadow_capacity < want_sh) {
-        if (w.shadow) (void)hipFree(w.shadow);
-        w.shadow = nullptr;
+    const bool wide = wide_entries(s);
+    if (w.shadow_capacity < want_sh || wide != (w.shadow_light != nullptr)) {
+        for (uint32_t** b : {&w.shadow, &w.shadow_light}) {
+            if (*b) (void)hipFree(*b);
+            *b = nullptr;
+        }
+        want_sh = std::max<uint64_t>(want_sh, w.shadow_capacity);
         w.shadow_capacity = 0;
         HIP_TRY(hipMalloc(&w.shadow, want_sh * sizeof(uint32_t)));
+        if (wide) HIP_TRY(hipMalloc(&w.shadow_light, want_sh * sizeof(uint32_t)));
         w.shadow_capacity = (uint32_t)want_sh;
     }
     const bool sort_tasks = s->S.use_bvh && tn.sort_tasks;
@@ -2368,7 +2383,9 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     p.task_keys = sort_tasks ? w.task_keys : nullptr;
     p.perm = nullptr;
     p.shadow_keys = sort_shadow ? w.shadow_keys : nullptr;
-    p.shadow_in = w.shadow;
+    // packed entries are read straight from the queue; wide ones by slot (null: slot t)
+    p.shadow_in = wide ? nullptr : w.shadow;
+    p.shadow_light = w.shadow_light;
     p.capacity = w.capacity;
     p.shadow_capacity = w.shadow_capacity;
     p.shadow = w.shadow;
@@ -2452,8 +2469,9 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
     }
     if (sort_shadow) {
         for (int r = 0; r < dup_sort; r++)
-            HIP_TRY(launch_sort(w.levels, -1, w.shadow_capacity, shadow_bits, w.shadow_keys, w.shadow, sort_scratch,
-                                w.shadow_sorted, tile_counts, digit_totals, 4 * s->num_cus, stream, sort_digit));
+            HIP_TRY(launch_sort(w.levels, -1, w.shadow_capacity, shadow_bits, w.shadow_keys, wide ? nullptr : w.shadow,
+                                sort_scratch, w.shadow_sorted, tile_counts, digit_totals, 4 * s->num_cus, stream,
+                                sort_digit));  // (wide entries: the values are the slots)
         p.shadow_in = w.shadow_sorted;
     }
     for (int r = 0; r < dup_shadow; r++) HIP_TRY(launch_wave_shadow(p, sb, stream));

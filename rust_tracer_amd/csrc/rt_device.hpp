@@ -210,8 +210,12 @@ struct WaveParams {
                                        // node n at (lit_words - 1) n + w - 1 (bit l % 32: light l)
     uint32_t lit_words;                // ceil(lights / 32), at least 1
     float4* node_ec;                   // [2 x capacity]: children's colours
-    uint32_t* shadow;                  // [shadow_capacity]: (node << light_bits) | light
-    uint32_t light_bits;               // bits of the light index in a shadow entry
+    uint32_t* shadow;                  // [shadow_capacity]: (node << light_bits) | light; wide: the node
+    uint32_t light_bits;               // bits of the light index in a shadow entry (wide: 0)
+    // scenes of more than 256 lights ("wide" entries, 8 B): the light index of slot s in
+    // shadow_light[s]; the shadow kernel then reads SLOTS through shadow_in (the sort's values
+    // are the slots; unsorted: shadow_in is null and entry t is slot t)
+    uint32_t* shadow_light;            // [shadow_capacity] or null (packed entries)
     uint32_t* levels;                  // [RT_LEVEL_TABLE_WORDS]: offset, count per level;
                                        // levels[2 * (RT_MAX_DEPTH + 1)] = shadow-queue count;
                                        // then the work counters (RT_WORK_WORD)

@@ -832,7 +832,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 group += (uint32_t)__builtin_popcountll(m);
                 if (want && !(RT_DIAG_ENTRIES == 1)) {  // (diagnostic 1: no entry stores)
                     if (slot < P.shadow_capacity) {
-                        P.shadow[slot] = (n << P.light_bits) | (uint32_t)li;
+                        if (P.shadow_light) {  // wide entries (> 256 lights)
+                            P.shadow[slot] = n;
+                            P.shadow_light[slot] = (uint32_t)li;
+                        } else {
+                            P.shadow[slot] = (n << P.light_bits) | (uint32_t)li;
+                        }
                         if (P.shadow_keys) {
                             uint32_t low = mort;
                             if (P.shadow_cell) {
@@ -959,6 +964,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
 #ifndef RT_SHADOW_WAVES
 #define RT_SHADOW_WAVES 5  // 96 VGPRs (round 4, light-buffer tiers: 5 / 6 / 8 waves 1236 / 1229 / 1196 Mpixels/s at K = 20, 3 runs each; round 3: 6 was +0.5 - 1% over 5)
 #endif
+// shadow entry t of the (sorted) queue -> its node and light.  Packed: (node << light_bits) |
+// light.  Wide (> 256 lights): shadow_in holds the entry's slot (or null: slot t), the node
+// and light sit in shadow[slot] and shadow_light[slot].
+__device__ __forceinline__ uint32_t shadow_raw(const WaveParams& P, uint32_t t) {
+    return P.shadow_in ? P.shadow_in[t] : t;
+}
+__device__ __forceinline__ void shadow_unpack(const WaveParams& P, uint32_t e, uint32_t& n, uint32_t& li) {
+    if (P.shadow_light) {
+        n = P.shadow[e];
+        li = P.shadow_light[e];
+    } else {
+        n = e >> P.light_bits;
+        li = e & ((1u << P.light_bits) - 1u);
+    }
+}
+__device__ __forceinline__ uint32_t shadow_node(const WaveParams& P, uint32_t e) {
+    return P.shadow_light ? P.shadow[e] : e >> P.light_bits;
+}
+
 template <bool LDS, bool COUNT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_WAVES, 8))) void shadow_kernel(WaveParams P) {
     if (RT_DIAG_ENTRIES) return;  // diagnostic builds whose shadow queue holds no valid entries
@@ -994,7 +1018,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
     typename std::conditional<COUNT, ScanCnt, NoCnt>::type cnt;
     if constexpr (COUNT) cnt_init(cnt);
     bc_init();
-    const uint32_t lmask = (1u << P.light_bits) - 1u;
     if (P.sched == 0) {
         // grid-stride, software-pipelined: the next iteration's entry is requested before this
         // iteration's scan and its origin before this iteration's lit-bit atomic, so the next
@@ -1003,13 +1026,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
         const uint32_t stride = gridDim.x * (blockDim.x >> 6) * 64u;
         uint32_t base = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64u;
         uint32_t t = base + lane;
-        uint32_t e = t < count ? P.shadow_in[t] : 0u;
-        float4 q = t < count ? P.node_ps[e >> P.light_bits] : make_float4(0.f, 0.f, 0.f, 0.f);
+        uint32_t e = t < count ? shadow_raw(P, t) : 0u;
+        float4 q = t < count ? P.node_ps[shadow_node(P, e)] : make_float4(0.f, 0.f, 0.f, 0.f);
         while (base < count) {
             const uint32_t tn = t + stride;
-            const uint32_t en = tn < count ? P.shadow_in[tn] : 0u;
+            const uint32_t en = tn < count ? shadow_raw(P, tn) : 0u;
             bool lit = false;
-            const uint32_t n = e >> P.light_bits, li = e & lmask;
+            uint32_t n = 0, li = 0;
+            if (t < count) shadow_unpack(P, e, n, li);
             if (t < count) {
                 V3 ps = v3(q.x, q.y, q.z);
                 float4 lq;
@@ -1024,7 +1048,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
                 n_shadow++;
                 lit = !shadow_scan<LDS, decltype(cnt), true>(S, ps, ldir, lpos, cnt, lnodes, __float_as_uint(lq.w));
             }
-            q = tn < count ? P.node_ps[en >> P.light_bits] : make_float4(0.f, 0.f, 0.f, 0.f);
+            q = tn < count ? P.node_ps[shadow_node(P, en)] : make_float4(0.f, 0.f, 0.f, 0.f);
             if (lit) atomicOr(lit_word(P, n, li), 1u << (li & 31u));
             base += stride;
             t = tn;
@@ -1039,8 +1063,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
             }
             const uint32_t t = base + lane;
             if (t < count) {
-                uint32_t e = P.shadow_in[t];
-                uint32_t n = e >> P.light_bits, li = e & lmask;
+                uint32_t n, li;
+                shadow_unpack(P, shadow_raw(P, t), n, li);
                 const float4 q = P.node_ps[n];
                 V3 ps = v3(q.x, q.y, q.z);
                 const LightRec L = light_at(S, li);

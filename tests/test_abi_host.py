@@ -202,10 +202,15 @@ def test_scene_build_is_deterministic_over_host_threads(which):
 
 
 def test_more_than_max_lights_are_refused_on_the_host():
-    """rt_api.h RT_MAX_LIGHTS (256): a shadow entry holds its light index beside its node.
-    256 lights build, 257 are refused with RT_ERR_UNSUPPORTED before any device work."""
+    """rt_api.h RT_MAX_LIGHTS (65536: the shadow keys' 16-bit light index).  300 lights build
+    (wide shadow entries past 256), 65537 are refused with RT_ERR_UNSUPPORTED before any device
+    work (and before any light buffer is built)."""
     from tests.test_gpu_many_lights import _scene
     assert _layout_digest(_scene(256), "lb_res=4")[1] > 0
+    assert _layout_digest(_scene(300), "lb_res=4")[1] > 0
+    d = rt.SceneDesc()
+    for k in range(65537):
+        d.point_light((0.0, 10.0 + k * 1e-3, 0.0), (0.0, 0.0, 0.0))
     dg, nb = C.c_uint64(), C.c_uint64()
-    st = abi.lib().rt_scene_layout_digest(_scene(257).ptr(), b"lb_res=4", C.byref(dg), C.byref(nb))
+    st = abi.lib().rt_scene_layout_digest(d.ptr(), b"lb_res=4", C.byref(dg), C.byref(nb))
     assert st == abi.RT_ERR_UNSUPPORTED

@@ -3,12 +3,14 @@ their shadow results in each node's node_lit word, lights 32 and up in node_lit_
 pass); the trace kernel's own-shape tests and inline scans decide lights 0-31 only, the rest
 always go to the shadow queue; the shadow kernel keeps up to 64 lights' positions in LDS
 (rt_wavefront.hip RT_LDS_LIGHTS) and reads the rest from the scene's records.  Frames and
-counters against the oracle at 32, 33, 64 and 70 lights; RT_MAX_LIGHTS + 1 lights are refused."""
+counters against the oracle at 32, 33, 64, 70 and 300 lights (above 256 lights a shadow entry
+is 8 B, node and light side by side: rt_device.hpp shadow_light); RT_MAX_LIGHTS + 1 (65537) are
+refused."""
 import numpy as np
 import pytest
 
 from oracle.oracle import OracleScene
-from rust_tracer_amd import DeviceScene, RtError, SceneDesc, abi
+from rust_tracer_amd import DeviceScene, SceneDesc
 
 from .test_gpu_parity import compare
 
@@ -27,7 +29,9 @@ def _scene(n_lights, seed=5):
 
 
 @pytest.mark.parametrize("n_lights,tuning", [(32, None), (33, None), (64, "lb_res=16"), (70, "lb_res=16"),
-                                             (70, "lb_res=16,inline_shadow=0,self_shadow=0")])
+                                             (70, "lb_res=16,inline_shadow=0,self_shadow=0"),
+                                             (256, "lb_res=8"), (257, "lb_res=8"), (300, "lb_res=8"),
+                                             (300, "lb_res=0,sort_shadow=0")])
 def test_many_lights_match_the_oracle(n_lights, tuning):
     desc = _scene(n_lights)
     w, h, depth = 96, 72, 4
@@ -43,7 +47,16 @@ def test_many_lights_match_the_oracle(n_lights, tuning):
     assert np.array_equal(img.view(np.uint32), img2.view(np.uint32)) and cnt2 == cnt
 
 
-def test_too_many_lights_are_refused():
-    with pytest.raises(RtError) as e:
-        DeviceScene(_scene(257))  # rt_api.h RT_MAX_LIGHTS + 1
-    assert e.value.status == abi.RT_ERR_UNSUPPORTED
+def test_wide_entries_larger_frame():
+    """300 lights (wide entries, every light past 32 queued) at 480x270, depth 3: every 30th
+    row against the oracle, counters of a second render equal (the pools are reused)."""
+    desc = _scene(300)
+    s = DeviceScene(desc, tuning="lb_res=0")
+    try:
+        a, ca, _, _ = s.render(480, 270, 3)
+        b, cb, _, _ = s.render(480, 270, 3)
+    finally:
+        s.close()
+    assert ca == cb and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    ref, _ = OracleScene(desc).render(480, 270, 3, rows=(0, 270, 30), threads=8)
+    compare(a[::30], ref[::30])
