@@ -105,6 +105,9 @@ def parse():
     p.add_argument("--seam-stats", type=int, default=1,
                    help="N = 1: also time one frame at a time, rt_render with its host copy, the scene "
                         "build, and the depth-9 reading of 'primary+8 bounces' (untimed extras)")
+    p.add_argument("--forest", type=int, default=1,
+                   help="N = 1, spp 1: also time the ray-forest path at the benchmark size (seam.forest: "
+                        "rt_forest_create, render_forest, render_forest_filter after a one-shape edit)")
     p.add_argument("--count-frame", type=int, default=1,
                    help="0: skip the instrumented (counting) frame; roofline test counts are then null "
                         "(used by the rocprofv3 counter passes so they see only the default kernels)")
@@ -310,6 +313,11 @@ def seam_stats(args, scene, pipe, tiler, dev):
                 out["render_call_updates"] = up
             except Exception as e:  # noqa: BLE001
                 out["render_call_error"] = repr(e)[:200]
+    if args.spp == 1 and args.forest:
+        try:  # an untimed extra
+            out["forest"] = forest_stats(args, scene)
+        except Exception as e:  # noqa: BLE001
+            out["forest_error"] = repr(e)[:200]
     t0 = time.perf_counter()
     c = scene.clone(dev.index)
     out["scene_clone_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
@@ -365,6 +373,125 @@ def seam_stats(args, scene, pipe, tiler, dev):
             t.depth = args.depth
         out["depth9_ms_per_frame"] = round(ms, 4)
         out["depth9_mpixels_per_s"] = round(args.width * args.height / (ms / 1e3) / 1e6, 3)
+    return out
+
+
+def forest_stats(args, scene, edit_shapes=(20, 725)):
+    """The ray-forest path at the benchmark size (render_tree.rs; the reference's bench -f mode,
+    main.rs:170-204): generate_ray_forest once (rt_forest_create), render_forest (the whole
+    forest shaded), and render_forest_filter after a one-shape material edit (the GUI's
+    re-shade, gui.rs:163-236) -- for a small sphere (shape 20) and for the floor plane (shape
+    725) -- wall clock of the C-ABI call (with its host copies of the float frame) and device
+    time of its kernels (rt_forest_timings), plus the share of the trees each edit re-shades.
+    Each edited material is restored afterwards."""
+    import numpy as np
+    w, h, depth = args.width, args.height, args.depth
+    out = {}
+    t0 = time.perf_counter()
+    f = scene.forest(w, h, depth)
+    out["forest_create_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+    out["forest_build_device_ms"] = round(f.timings()["build_ms"], 4)
+    img = f.render()
+    walls, dev = [], []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        img = f.render()
+        walls.append((time.perf_counter() - t0) * 1e3)
+        dev.append(f.timings()["shade_ms"])
+    out["forest_render_ms"] = round(min(walls), 3)
+    out["forest_render_device_ms"] = round(min(dev), 4)
+    edits = []
+    base = scene.desc.editable()
+    for shape in edit_shapes:
+        if shape >= len(base.shapes):
+            continue
+        k = int(base.shapes[shape].material)
+        old = base.materials[k]
+        m = type(old).from_buffer_copy(old)  # same kind (rt_scene_set_material keeps kinds)
+        m.reflectivity = float(np.float32(0.4 if old.reflectivity < 0.2 else 0.1))
+        m.power = float(np.float32(old.power * 1.5))
+        scene.set_material(k, m)
+        try:
+            walls, dev = [], []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                got = f.render_filter([shape], img)
+                walls.append((time.perf_counter() - t0) * 1e3)
+                dev.append(f.timings()["shade_ms"])
+            n = f.trees_with(shape)
+            edits.append({"shape": shape, "kind": ("sphere", "plane", "triangle", "cube")[base.shapes[shape].kind],
+                          "filter_ms": round(min(walls), 3), "filter_device_ms": round(min(dev), 4),
+                          "trees_reshaded": n, "tree_fraction": round(n / (w * h), 6),
+                          "pixels_changed": int(np.count_nonzero((got != img).any(axis=2)))})
+        finally:
+            scene.set_material(k, old)
+    out["filter"] = edits
+    st = f.stats()
+    out["forest_trees"] = st["num_trees"]
+    out["forest_intersections"] = st["num_intersections"]
+    f.close()
+    out["note"] = ("wall: the C-ABI call incl. its host copies of the float frame (render: one device-to-host "
+                   "copy; filter: the caller's frame up and back); device: HIP events around the forest_mark / "
+                   "forest_shade_level kernels (build: trace + shadow passes)")
+    return out
+
+
+def test_flops(ops):
+    """(reference tests at the reference's flop counts, as executed, hierarchy tests) of a
+    scan_ops dict."""
+    ref_f = sum(ops[k] * REF_TEST_FLOPS[k] for k in REF_TEST_FLOPS)
+    exec_f = sum(ops[k] * EXEC_TEST_FLOPS[k] for k in EXEC_TEST_FLOPS)
+    over_f = sum(ops[OVERHEAD_COUNTER.get(k, k)] * OVERHEAD_FLOPS[k] for k in OVERHEAD_FLOPS)
+    return ref_f, exec_f, over_f
+
+
+def kernel_roofline(args, pipe, reps=5):
+    """Per-kernel roofline at one frame at a time (the regime whose kernel times are exclusive):
+    one untimed pass of the whole frame counted twice (trace-kernel tests, shadow-kernel tests;
+    Tune::count), then `reps` uncounted passes with every launch group bracketed by HIP events on
+    the pass's stream (rt_scene_kernel_times).  achieved = the kernel's executed test flops per
+    frame / its summed launch time per frame, against the 157.3 TFLOP/s f32 peak.  The same
+    kernel's exclusive time in profiles/<tag>/kernel_trace_trace1.csv (rocprofv3, one frame at a
+    time) is the cross-check (`exclusive_kernel_ms_per_frame`)."""
+    whole = pipe.whole_tiler()
+    sc = whole.scene
+    sc.set_grid_share(100)
+    out = {"regime": "one frame at a time (one pipeline pass of the whole frame on one stream, full-chip grids)"}
+    try:
+        flops = {}
+        for kind in ("trace", "shadow"):
+            sc.set_tuning(f"count={kind}")
+            sc.set_scan_counting(True)
+            sc.scan_ops(reset=True)
+            whole.step()
+            torch.cuda.synchronize()
+            ops = sc.scan_ops(reset=True)
+            sc.set_scan_counting(False)
+            sc.set_tuning("count=all")
+            ref_f, exec_f, over_f = test_flops(ops)
+            flops[kind] = {"reference_tests_executed": exec_f, "hierarchy_tests": over_f,
+                           "reference_tests_at_reference_flops": ref_f}
+        whole.step()
+        torch.cuda.synchronize()
+        sc.set_kernel_timing(True)
+        sc.kernel_times(reset=True)
+        for _ in range(reps):
+            whole.step()
+        torch.cuda.synchronize()
+        kt = sc.kernel_times(reset=True)
+        sc.set_kernel_timing(False)
+    finally:
+        sc.set_grid_share(pipe.grid_share if pipe.inflight > 1 else 100)
+    ms = {k: kt[k] / reps for k in sc.KERNEL_KINDS}
+    for kind, name in (("trace", "trace_level_kernel"), ("shadow", "shadow_kernel")):
+        f = flops[kind]["reference_tests_executed"] + flops[kind]["hierarchy_tests"]
+        t = ms[kind]
+        out[name] = {"flops_per_frame": f, "flops_breakdown": flops[kind], "ms_per_frame": round(t, 4),
+                     "achieved_TFLOPs": round(f / (t / 1e3) / 1e12, 3) if t > 0 else None,
+                     "frac": round(f / (t / 1e3) / 1e12 / PEAK_F32_TFLOPS, 4) if t > 0 else None}
+    out["kernel_ms_per_frame"] = {k: round(v, 4) for k, v in ms.items()}
+    out["launch_groups_per_frame"] = kt["launch_groups"] / reps
+    out["frame_ms"] = round(sum(ms.values()), 4)
     return out
 
 
@@ -517,18 +644,31 @@ def main():
     # cameras (a batch's waves mix its frames' rays, so the tests a wave runs depend on the
     # pass), per frame; frames are deterministic, so the timed passes run these tests, uncounted
     ops = None
+    ops_by_kernel = None
     if args.count_frame:
+        # the same pass counted twice: the trace kernels' tests, then the shadow kernel's
+        # (Tune::count), so that the flops split by kernel; their sum is every test of the pass
         counted = [t.scene for t in pipe.group_tilers(0)]  # one pass of group 0 (all its shares)
-        for sc in counted:
-            sc.set_scan_counting(True)
-            sc.scan_ops(reset=True)
-        pipe.render_pass(0, [anim_cam(i) for i in range(batch)] if args.animate else [_abi.camera(args.width, args.height)] * batch)
-        torch.cuda.synchronize()
-        ops = {}
-        for sc in counted:
-            for k, v in sc.scan_ops().items():
-                ops[k] = ops.get(k, 0.0) + v / batch
-            sc.set_scan_counting(False)
+        ops, ops_by_kernel = {}, {}
+        for kind in ("trace", "shadow"):
+            for sc in counted:
+                sc.set_tuning(f"count={kind}")
+                sc.set_scan_counting(True)
+                sc.scan_ops(reset=True)
+            pipe.render_pass(0, [anim_cam(i) for i in range(batch)] if args.animate
+                             else [_abi.camera(args.width, args.height)] * batch)
+            torch.cuda.synchronize()
+            part = {}
+            for sc in counted:
+                for k, v in sc.scan_ops().items():
+                    part[k] = part.get(k, 0.0) + v / batch
+                sc.set_scan_counting(False)
+                sc.set_tuning("count=all")
+            ops_by_kernel[kind] = part
+            for k, v in part.items():
+                ops[k] = ops.get(k, 0.0) + v
+    # per-kernel rates at one frame at a time (exclusive kernel times, live HIP events)
+    per_kernel = kernel_roofline(args, pipe) if (args.count_frame and world == 1 and args.spp == 1) else None
     pipe.zero_counters()
 
     lat = []  # one (start, end) event pair per pass
@@ -607,11 +747,13 @@ def main():
         # reference's flop counts
         flops = None
         if ops:
-            ref_f = sum(ops[k] * REF_TEST_FLOPS[k] for k in REF_TEST_FLOPS)
-            exec_f = sum(ops[k] * EXEC_TEST_FLOPS[k] for k in EXEC_TEST_FLOPS)
-            over_f = sum(ops[OVERHEAD_COUNTER.get(k, k)] * OVERHEAD_FLOPS[k] for k in OVERHEAD_FLOPS)
+            ref_f, exec_f, over_f = test_flops(ops)
             flops = {"reference_tests_at_reference_flops": ref_f, "reference_tests_executed": exec_f,
-                     "hierarchy_tests": over_f}
+                     "hierarchy_tests": over_f,
+                     "by_kernel": {("trace_level_kernel" if k == "trace" else "shadow_kernel"):
+                                   dict(zip(("reference_tests_at_reference_flops", "reference_tests_executed",
+                                             "hierarchy_tests"), test_flops(v)))
+                                   for k, v in ops_by_kernel.items()}}
         per_launch_flops = flops["reference_tests_executed"] + flops["hierarchy_tests"] if flops else None
         achieved = per_launch_flops / (kernel_ms / 1e3) / 1e12 if ops else None
         # what the reference's linear scan would need for the same rays (F_alg per scan)
@@ -640,6 +782,10 @@ def main():
                                                 PEAK_F32_TFLOPS, 4) if flops else None),
             "tests_per_launch": {k: round(v) for k, v in ops.items() if not k.startswith("cycles")} if ops else None,
             "cycles_per_launch": {k: round(v) for k, v in ops.items() if k.startswith("cycles")} if ops else None,
+            # the dominant kernels' own rates, one frame at a time (live HIP events per launch
+            # group, bench.py kernel_roofline); the headline's frac above is the whole frame's
+            # executed tests over the frames-in-flight step time
+            "per_kernel": per_kernel,
             "culling": {"hierarchy": scene.uses_bvh,
                         "linear_scan_flops_per_launch": brute_flops,
                         "linear_scan_equivalent_TFLOPs": round(brute_flops / (kernel_ms / 1e3) / 1e12, 3)},
@@ -675,6 +821,13 @@ def main():
                 "peak_GBps": PEAK_HBM_GBPS,
                 "frac": round(traffic["bytes_per_launch"] / (kernel_ms / 1e3) / 1e9 / PEAK_HBM_GBPS, 6)
                 if traffic else None,
+                "frac_is": "the counters' HBM bytes (intermediate queue state included) over the step time",
+                # SURVEY.md §8(d)'s algorithmic bytes over the step time: the useful-work fraction
+                "frac_algorithmic": round(args.spp * (scene_soa_bytes + args.width * args.height * 12 / world)
+                                          / (elapsed / steps) / 1e9 / PEAK_HBM_GBPS, 6),
+                "traffic_over_algorithmic": (round(traffic["bytes_per_launch"] /
+                                                   (args.spp * (scene_soa_bytes + args.width * args.height * 12 / world)), 1)
+                                             if traffic else None),
             },
         }
         out = {

@@ -396,6 +396,18 @@ rt_status rt_scene_set_grid_share(rt_scene* scene, int32_t percent);
  * creation turns it off), 0 if they test every shape. */
 int32_t rt_scene_uses_bvh(const rt_scene* scene);
 
+/* Per-kernel device time of this handle's own render passes (not its band shares' or
+ * devices'): with timing on, every launch group of a pass -- a trace level, a task-queue sort,
+ * the shadow-queue sort, the shadow pass, a combine level -- is bracketed by HIP events on the
+ * pass's stream.  One pass at a time on one stream gives each kind's exclusive time
+ * (bench.py's per-kernel roofline).  rt_scene_kernel_times waits for the recorded events and
+ * writes ms[kind] summed over the passes since the last reset (RT_KT_* below; ms[RT_KT_LAUNCHES]
+ * = the number of spans); reset != 0 forgets them.  Measurement only: the events cost time. */
+enum { RT_KT_TRACE = 0, RT_KT_SORT_TASKS = 1, RT_KT_SORT_SHADOW = 2, RT_KT_SHADOW = 3, RT_KT_COMBINE = 4,
+       RT_KT_LAUNCHES = 5 };
+rt_status rt_scene_set_kernel_timing(rt_scene* scene, int32_t enable);
+rt_status rt_scene_kernel_times(rt_scene* scene, float* ms, uint32_t n, int32_t reset);
+
 /* ---- ray forest (src/render_tree.rs) -------------------------------------------------
  * generate_ray_forest(camera, scene, w, h, depth) -> RayForest (render_tree.rs:147-164):
  * traces every pixel's ray tree (the same rays, shadow tests and child rules as
@@ -427,6 +439,11 @@ rt_status rt_forest_trees_with(rt_forest* forest, int32_t shape_id, uint64_t* co
 
 /* Ray counts of the build (node rays, shadow rays, pixels). */
 rt_status rt_forest_counters(const rt_forest* forest, rt_counters* out);
+
+/* Device time (HIP events, ms) of the build's trace + shadow passes (its last attempt) and of
+ * the last rt_forest_render / _render_filter (the mark and shade kernels; host copies
+ * excluded; 0 before the first shade).  Either pointer may be NULL. */
+rt_status rt_forest_timings(const rt_forest* forest, float* build_ms, float* shade_ms);
 
 /* Replace material `index`'s parameters (same kind) -- the GUI's material edits
  * (gui.rs:221-236).  Affects later renders and forest shades. */

@@ -49,6 +49,8 @@ def lib():
     L.oracle_render_forest.argtypes = [vp, P(abi.rt_camera), C.c_uint32, fa, P(C.c_uint32)]
     L.oracle_forest_build.argtypes = [vp, P(abi.rt_camera), C.c_uint32, P(vp)]
     L.oracle_forest_render.argtypes = [vp, fa]
+    L.oracle_forest_build_mt.argtypes = [vp, P(abi.rt_camera), C.c_uint32, C.c_uint32, P(vp)]
+    L.oracle_forest_render_mt.argtypes = [vp, fa, C.c_uint32]
     L.oracle_forest_render_filter.argtypes = [vp, P(C.c_int32), C.c_uint32, fa]
     L.oracle_forest_tree_sizes.argtypes = [vp, P(C.c_uint32)]
     L.oracle_forest_trees_with.argtypes = [vp, C.c_int32]
@@ -131,8 +133,8 @@ class OracleScene:
         if st != 0:
             raise RuntimeError(f"oracle_scene_set_material failed: {st}")
 
-    def forest(self, x_res, y_res, depth):
-        return OracleForest(self, x_res, y_res, depth)
+    def forest(self, x_res, y_res, depth, threads=1):
+        return OracleForest(self, x_res, y_res, depth, threads)
 
     def render_forest(self, x_res, y_res, depth):
         from rust_tracer_amd import abi
@@ -150,13 +152,14 @@ class OracleScene:
 class OracleForest:
     """render_tree.rs RayForest on the CPU (test infrastructure)."""
 
-    def __init__(self, scene, x_res, y_res, depth):
+    def __init__(self, scene, x_res, y_res, depth, threads=1):
         from rust_tracer_amd import abi
         self.L, self.scene = scene.L, scene
         self.w, self.h_res = x_res, y_res
+        self.threads = threads
         self.h = C.c_void_p()
         cam = abi.camera(x_res, y_res)
-        st = self.L.oracle_forest_build(scene.h, C.byref(cam), depth, C.byref(self.h))
+        st = self.L.oracle_forest_build_mt(scene.h, C.byref(cam), depth, threads, C.byref(self.h))
         if st != 0:
             raise RuntimeError(f"oracle_forest_build failed: {st}")
 
@@ -167,7 +170,7 @@ class OracleForest:
 
     def render(self):
         rgb = np.zeros((self.h_res, self.w, 3), np.float32)
-        self.L.oracle_forest_render(self.h, rgb.ctypes.data_as(C.POINTER(C.c_float)))
+        self.L.oracle_forest_render_mt(self.h, rgb.ctypes.data_as(C.POINTER(C.c_float)), self.threads)
         return rgb
 
     def render_filter(self, mutated_ids, rgb):

@@ -1034,6 +1034,52 @@ rt_status oracle_forest_build(const oracle_scene* s, const rt_camera* cam, uint3
     return RT_OK;
 }
 
+// the same forest built over `threads` host threads (rows dealt in turn; the trees and their
+// shape sets are per pixel, the scene is read only -- the Rc<Material> copies are shared_ptr
+// copies, whose counts are atomic): test infrastructure for benchmark-size forests
+rt_status oracle_forest_build_mt(const oracle_scene* s, const rt_camera* cam, uint32_t depth, uint32_t threads,
+                                 oracle_forest** out) {
+    if (threads <= 1) return oracle_forest_build(s, cam, depth, out);
+    if (!s || !cam || !out) return RT_ERR_INVALID_ARG;
+    std::unique_ptr<oracle_forest> f(new oracle_forest());
+    Camera c = cam_of(cam);
+    f->s = s;
+    f->w = c.x_res;
+    f->h = c.y_res;
+    f->roots.resize((size_t)c.x_res * c.y_res);
+    f->shapes.resize((size_t)c.x_res * c.y_res);
+    std::vector<std::thread> pool;
+    oracle_forest* fp = f.get();
+    for (uint32_t k = 0; k < threads; k++)
+        pool.emplace_back([=]() {
+            Counters cnt;
+            for (uint32_t v = k; v < c.y_res; v += threads)
+                for (uint32_t u = 0; u < c.x_res; u++) {
+                    size_t i = (size_t)v * c.x_res + u;
+                    fp->roots[i] = build_ray_tree(s->scene, c.get_ray(u, v), depth, fp->shapes[i], cnt);
+                }
+        });
+    for (auto& t : pool) t.join();
+    *out = f.release();
+    return RT_OK;
+}
+
+rt_status oracle_forest_render_mt(const oracle_forest* f, float* rgb, uint32_t threads) {
+    if (!f || !rgb) return RT_ERR_INVALID_ARG;
+    if (threads <= 1) return oracle_forest_render(f, rgb);
+    std::vector<std::thread> pool;
+    const size_t n = f->roots.size();
+    for (uint32_t k = 0; k < threads; k++)
+        pool.emplace_back([=]() {
+            for (size_t i = k; i < n; i += threads) {
+                Color col = render_ray_tree(f->roots[i].get(), f->s->scene.ambient).first;
+                rgb[3 * i] = col.r; rgb[3 * i + 1] = col.g; rgb[3 * i + 2] = col.b;
+            }
+        });
+    for (auto& t : pool) t.join();
+    return RT_OK;
+}
+
 rt_status oracle_forest_render(const oracle_forest* f, float* rgb) {
     if (!f || !rgb) return RT_ERR_INVALID_ARG;
     for (size_t k = 0; k < f->roots.size(); k++) {

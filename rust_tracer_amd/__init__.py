@@ -375,6 +375,22 @@ class DeviceScene:
         self.last_wave_iterations = cnt.wave_iterations
         return rgb, counters, ms.value, rgb8
 
+    KERNEL_KINDS = ("trace", "sort_tasks", "sort_shadow", "shadow", "combine")
+
+    def set_kernel_timing(self, enable=True):
+        """rt_scene_set_kernel_timing: bracket every launch group of this handle's passes with
+        HIP events (measurement only)."""
+        check(self._L.rt_scene_set_kernel_timing(self.h, 1 if enable else 0), "rt_scene_set_kernel_timing")
+
+    def kernel_times(self, reset=False):
+        """rt_scene_kernel_times: ms per kernel kind summed over the timed passes, and the
+        number of launch groups timed."""
+        out = (C.c_float * (len(self.KERNEL_KINDS) + 1))()
+        check(self._L.rt_scene_kernel_times(self.h, out, len(out), 1 if reset else 0), "rt_scene_kernel_times")
+        d = dict(zip(self.KERNEL_KINDS, (float(v) for v in out)))
+        d["launch_groups"] = int(out[len(self.KERNEL_KINDS)])
+        return d
+
     def set_material(self, index, material):
         """rt_scene_set_material: replace material `index` (same kind), e.g. the GUI's edits."""
         check(self._L.rt_scene_set_material(self.h, index, C.byref(material)), "rt_scene_set_material")
@@ -492,6 +508,13 @@ class DeviceForest:
         c = abi.rt_counters()
         check(self._L.rt_forest_counters(self.h, C.byref(c)), "rt_forest_counters")
         return {"node_rays": c.node_rays, "shadow_rays": c.shadow_rays, "pixels": c.pixels}
+
+    def timings(self):
+        """rt_forest_timings: device ms of the build's trace + shadow passes and of the last
+        render / render_filter (mark + shade kernels, host copies excluded)."""
+        b, sh = C.c_float(0), C.c_float(0)
+        check(self._L.rt_forest_timings(self.h, C.byref(b), C.byref(sh)), "rt_forest_timings")
+        return {"build_ms": b.value, "shade_ms": sh.value}
 
     def stats(self):
         """RayForest::stats (render_tree.rs:73-93), including its f32 percentile indexing."""

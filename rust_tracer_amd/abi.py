@@ -171,6 +171,9 @@ def lib():
     L.rt_forest_tree_sizes.argtypes = [vp, P(C.c_uint32)]
     L.rt_forest_trees_with.argtypes = [vp, C.c_int32, P(C.c_uint64)]
     L.rt_forest_counters.argtypes = [vp, P(rt_counters)]
+    L.rt_forest_timings.argtypes = [vp, P(C.c_float), P(C.c_float)]
+    L.rt_scene_set_kernel_timing.argtypes = [vp, C.c_int32]
+    L.rt_scene_kernel_times.argtypes = [vp, P(C.c_float), C.c_uint32, C.c_int32]
     L.rt_scene_set_material.argtypes = [vp, C.c_uint32, P(rt_material)]
     L.rt_scene_update.argtypes = [vp, P(rt_scene_desc), P(C.c_int32)]
     L.rt_write_image.argtypes = [C.c_char_p, P(C.c_uint8), C.c_uint32, C.c_uint32]

@@ -1378,7 +1378,40 @@ struct rt_scene {
     // bumped by every rebuild rt_scene_update adopts: a forest made before it refuses to shade
     // (its trees hold the old scene's material indices and light count)
     uint64_t generation = 0;
+    // rt_scene_set_kernel_timing: HIP events around every launch of this handle's passes, by
+    // kernel kind (RT_KT_*), summed by rt_scene_kernel_times
+    bool ktime = false;
+    std::vector<hipEvent_t> kt_events;        // pool, reused
+    std::vector<std::pair<int, size_t>> kt_spans;  // (kind, index of the start event; end = +1)
+    size_t kt_used = 0;
 };
+
+namespace {
+// Brackets one launch of kind `kind` with a pair of events when the handle times its kernels.
+struct KSpan {
+    rt_scene* s;
+    hipStream_t st;
+    size_t at = 0;
+    bool on = false;
+    KSpan(rt_scene* sc, hipStream_t stream, int kind) : s(sc), st(stream) {
+        if (!s->ktime) return;
+        if (s->kt_used + 2 > s->kt_events.size()) {
+            for (int i = 0; i < 64; i++) {
+                hipEvent_t e = nullptr;
+                if (hipEventCreate(&e) != hipSuccess) return;
+                s->kt_events.push_back(e);
+            }
+        }
+        at = s->kt_used;
+        s->kt_used += 2;
+        on = hipEventRecord(s->kt_events[at], st) == hipSuccess;
+        if (on) s->kt_spans.emplace_back(kind, at);
+    }
+    ~KSpan() {
+        if (on) (void)hipEventRecord(s->kt_events[at + 1], st);
+    }
+};
+}  // namespace
 
 rt_multi_state*& rt_scene_multi(rt_scene* s) { return s->multi; }
 int rt_scene_device_of(const rt_scene* s) { return s->device; }
@@ -1936,6 +1969,7 @@ rt_status rt_scene_destroy(rt_scene* s) {
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     for (auto& se : s->ev_streams) (void)hipEventDestroy(se.second);
+    for (hipEvent_t e : s->kt_events) (void)hipEventDestroy(e);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
     return RT_OK;
@@ -2025,6 +2059,30 @@ rt_status rt_scene_set_scan_counting(rt_scene* s, int32_t enable) {
     return RT_OK;
 }
 
+rt_status rt_scene_set_kernel_timing(rt_scene* s, int32_t enable) {
+    if (!s) return RT_ERR_INVALID_ARG;
+    s->ktime = enable != 0;
+    return RT_OK;
+}
+
+rt_status rt_scene_kernel_times(rt_scene* s, float* ms, uint32_t n, int32_t reset) {
+    if (!s || (n && !ms)) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(s->device));
+    for (uint32_t k = 0; k < n; k++) ms[k] = 0.f;
+    for (const auto& sp : s->kt_spans) {
+        HIP_TRY(hipEventSynchronize(s->kt_events[sp.second + 1]));
+        float t = 0.f;
+        HIP_TRY(hipEventElapsedTime(&t, s->kt_events[sp.second], s->kt_events[sp.second + 1]));
+        if ((uint32_t)sp.first < n) ms[sp.first] += t;
+    }
+    if (n > RT_KT_LAUNCHES) ms[RT_KT_LAUNCHES] = (float)s->kt_spans.size();
+    if (reset) {
+        s->kt_spans.clear();
+        s->kt_used = 0;
+    }
+    return RT_OK;
+}
+
 #if RT_DIAG
 static uint32_t* g_task_clock = nullptr;  // RT_TASK_CLOCK records (diagnostic builds)
 #endif
@@ -2067,7 +2125,8 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
                                uint32_t rank, uint32_t world, const PassOut& o, hipStream_t stream,
                                WaveParams* forest_params, uint32_t* forest_levels, uint32_t spp = 1,
                                uint32_t sample = 0, uint32_t seed = 0, uint32_t frames = 1,
-                               const rt_camera* cams = nullptr, bool spp_batch = false);
+                               const rt_camera* cams = nullptr, bool spp_batch = false,
+                               hipEvent_t forest_done = nullptr);
 
 // Samples per pipeline pass for spp > 1: Tune::spp_batch, else as many (<= RT_MAX_FRAMES) as
 // keep a pass within Tune::spp_batch_items level-0 items (default 2^25: 4 x 3840x2160 or
@@ -2126,7 +2185,8 @@ static rt_status launch_bands_wave(rt_scene* s, const rt_camera* cam, uint32_t d
 static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, uint32_t depth, uint32_t band_rows,
                                uint32_t rank, uint32_t world, const PassOut& o, hipStream_t stream,
                                WaveParams* forest_params, uint32_t* forest_levels, uint32_t spp, uint32_t sample,
-                               uint32_t seed, uint32_t frames, const rt_camera* cams, bool spp_batch) {
+                               uint32_t seed, uint32_t frames, const rt_camera* cams, bool spp_batch,
+                               hipEvent_t forest_done) {
     if (frames == 0 || frames > RT_MAX_FRAMES || (frames > 1 && (!cams || forest_params))) return RT_ERR_INVALID_ARG;
     WaveParams p;
     std::memset(&p, 0, sizeof(p));
@@ -2443,7 +2503,10 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
                              stream));
     if (w.lit_words > 1)  // lights 32 and up: their bits start at 0 (the trace kernel stores word 0 only)
         HIP_TRY(hipMemsetAsync(w.node_lit_hi, 0, (size_t)(w.lit_words - 1) * w.capacity * sizeof(uint32_t), stream));
-    HIP_TRY(launch_wave_trace(p, 0, tb, stream, s->occ_trace_each, s->occ_trace));
+    {
+        KSpan k0(s, stream, RT_KT_TRACE);
+        HIP_TRY(launch_wave_trace(p, 0, tb, stream, s->occ_trace_each, s->occ_trace));
+    }
     // every level's queue is sorted (leaving any level unsorted lost: DESIGN.md)
     const uint64_t sort_levels = ~0ull;
     for (uint32_t k = 1; k < levels; k++) {
@@ -2460,22 +2523,29 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         }
         p.perm = nullptr;  // production order unless this level is sorted
         if (sort_tasks && ((sort_levels >> (k < 64 ? k : 63)) & 1ull)) {
+            KSpan ks(s, stream, RT_KT_SORT_TASKS);
             for (int r = 0; r < dup_sort; r++)
                 HIP_TRY(launch_sort(w.levels, (int32_t)k, w.capacity, task_bits, w.task_keys, nullptr, sort_scratch,
                                     w.perm, tile_counts, digit_totals, 4 * s->num_cus, stream, sort_digit));
             p.perm = w.perm;
         }
+        KSpan kt(s, stream, RT_KT_TRACE);
         HIP_TRY(launch_wave_trace(p, k, tb, stream, s->occ_trace_each, s->occ_trace));
     }
     if (sort_shadow) {
+        KSpan ks(s, stream, RT_KT_SORT_SHADOW);
         for (int r = 0; r < dup_sort; r++)
             HIP_TRY(launch_sort(w.levels, -1, w.shadow_capacity, shadow_bits, w.shadow_keys, wide ? nullptr : w.shadow,
                                 sort_scratch, w.shadow_sorted, tile_counts, digit_totals, 4 * s->num_cus, stream,
                                 sort_digit));  // (wide entries: the values are the slots)
         p.shadow_in = w.shadow_sorted;
     }
-    for (int r = 0; r < dup_shadow; r++) HIP_TRY(launch_wave_shadow(p, sb, stream));
+    {
+        KSpan ksh(s, stream, RT_KT_SHADOW);
+        for (int r = 0; r < dup_shadow; r++) HIP_TRY(launch_wave_shadow(p, sb, stream));
+    }
     if (w.forest) {  // no combine: the forest is shaded later, any number of times
+        if (forest_done) HIP_TRY(hipEventRecord(forest_done, stream));
         HIP_TRY(hipMemcpyAsync(forest_levels, w.levels, 2 * (RT_MAX_DEPTH + 1) * sizeof(uint32_t),
                                hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
@@ -2490,8 +2560,10 @@ static rt_status wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam, 
         forest_levels[2 * (RT_MAX_DEPTH + 1)] = used;
         return RT_OK;
     }
-    for (uint32_t k = levels; k-- > 0;)
+    for (uint32_t k = levels; k-- > 0;) {
+        KSpan kc(s, stream, RT_KT_COMBINE);
         for (int r = 0; r < dup_comb; r++) HIP_TRY(launch_wave_combine(p, k, cb, stream));
+    }
     return RT_OK;
 }
 
@@ -3030,6 +3102,9 @@ struct rt_forest {
     uint32_t n_keys = 0;
     uint32_t* sizes = nullptr;  // [pixels]
     unsigned long long* counters = nullptr;  // node, shadow, pixels of the build
+    // device time of the build's last pass and of the last shade (rt_forest_timings)
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool shaded = false;
 };
 
 namespace {
@@ -3037,20 +3112,22 @@ namespace {
 size_t forest_pixels(const rt_forest* f) { return (size_t)f->cam.x_res * f->cam.y_res; }
 
 rt_status forest_shade(rt_forest* f, const uint8_t* dirty) {
-    // a rebuild since the forest was made: its nodes' material indices and lit words describe
-    // the old scene, which the handle no longer holds (rt_api.h rt_scene_update)
-    if (f->generation != f->s->generation) return RT_ERR_INVALID_ARG;
     WaveParams p = f->p;
     p.S = f->s->S;  // current material table
     p.dirty = dirty;
     int cb = f->s->num_cus * (f->s->occ_combine > 0 ? f->s->occ_combine : 1);
     uint32_t used = f->levels[2 * (RT_MAX_DEPTH + 1)];
     for (uint32_t k = used; k-- > 0;) HIP_TRY(launch_forest_shade(p, k, cb, f->frame, f->s->stream));
+    HIP_TRY(hipEventRecord(f->ev[3], f->s->stream));
+    f->shaded = true;
     return RT_OK;
 }
+// a rebuild since the forest was made: its nodes' material indices and lit words describe
+// the old scene, which the handle no longer holds (rt_api.h rt_scene_update)
+bool forest_stale(const rt_forest* f) { return f->generation != f->s->generation; }
 
 // mark[pixel] = tree holds one of `ids` (or sizes per pixel when ids == nullptr)
-rt_status forest_mark(rt_forest* f, const int32_t* ids, uint32_t n_ids, bool sizes) {
+rt_status forest_mark(rt_forest* f, const int32_t* ids, uint32_t n_ids, bool sizes, hipEvent_t start = nullptr) {
     hipStream_t st = f->s->stream;
     size_t px = forest_pixels(f);
     const uint8_t* mask = nullptr;
@@ -3064,6 +3141,7 @@ rt_status forest_mark(rt_forest* f, const int32_t* ids, uint32_t n_ids, bool siz
         mask = f->key_mask;
     }
     if (sizes) HIP_TRY(hipMemsetAsync(f->sizes, 0, px * sizeof(uint32_t), st));
+    if (start) HIP_TRY(hipEventRecord(start, st));
     HIP_TRY(launch_forest_mark(f->ws.node_key, f->ws.node_pixel, f->ws.node_flags, f->n_nodes, mask, f->n_keys, f->mark,
                                sizes ? f->sizes : nullptr, st));
     return RT_OK;
@@ -3095,8 +3173,11 @@ rt_status rt_forest_create(rt_scene* s, const rt_camera* cam, uint32_t depth, rt
             free_workspace(f->ws);
             for (void* b : {(void*)f->frame, (void*)f->mark, (void*)f->key_mask, (void*)f->sizes, (void*)f->counters})
                 if (b) (void)hipFree(b);
+            for (hipEvent_t e : f->ev)
+                if (e) (void)hipEventDestroy(e);
         }
     } guard{f.get()};
+    for (hipEvent_t& e : f->ev) HIP_TRY(hipEventCreate(&e));
     HIP_TRY(hipMalloc(&f->frame, px * 3 * sizeof(float)));
     HIP_TRY(hipMalloc(&f->mark, px));
     HIP_TRY(hipMalloc(&f->key_mask, f->n_keys));
@@ -3107,7 +3188,9 @@ rt_status rt_forest_create(rt_scene* s, const rt_camera* cam, uint32_t depth, rt
     for (int attempt = 0;; attempt++) {
         HIP_TRY(hipMemsetAsync(f->counters, 0, 4 * sizeof(unsigned long long), st));
         const PassOut o{nullptr, nullptr, f->counters, false, true};
-        rt_status r = wave_pipeline(s, f->ws, cam, depth, band_rows, 0, 1, o, st, &f->p, f->levels);
+        HIP_TRY(hipEventRecord(f->ev[0], st));
+        rt_status r = wave_pipeline(s, f->ws, cam, depth, band_rows, 0, 1, o, st, &f->p, f->levels, 1, 0, 0, 1,
+                                    nullptr, false, f->ev[1]);
         if (r != RT_OK) return r;
         uint32_t ovf = 0;
         HIP_TRY(hipMemcpyAsync(&ovf, f->ws.overflow, sizeof(ovf), hipMemcpyDeviceToHost, st));
@@ -3132,13 +3215,28 @@ rt_status rt_forest_destroy(rt_forest* f) {
     free_workspace(f->ws);
     for (void* b : {(void*)f->frame, (void*)f->mark, (void*)f->key_mask, (void*)f->sizes, (void*)f->counters})
         if (b) (void)hipFree(b);
+    for (hipEvent_t e : f->ev)
+        if (e) (void)hipEventDestroy(e);
     delete f;
+    return RT_OK;
+}
+
+rt_status rt_forest_timings(const rt_forest* f, float* build_ms, float* shade_ms) {
+    if (!f) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(f->s->device));
+    if (build_ms) HIP_TRY(hipEventElapsedTime(build_ms, f->ev[0], f->ev[1]));
+    if (shade_ms) {
+        *shade_ms = 0.f;
+        if (f->shaded) HIP_TRY(hipEventElapsedTime(shade_ms, f->ev[2], f->ev[3]));
+    }
     return RT_OK;
 }
 
 rt_status rt_forest_render(rt_forest* f, float* rgb) {
     if (!f || !rgb) return RT_ERR_INVALID_ARG;
+    if (forest_stale(f)) return RT_ERR_INVALID_ARG;
     HIP_TRY(hipSetDevice(f->s->device));
+    HIP_TRY(hipEventRecord(f->ev[2], f->s->stream));
     rt_status r = forest_shade(f, nullptr);
     if (r != RT_OK) return r;
     HIP_TRY(hipMemcpyAsync(rgb, f->frame, forest_pixels(f) * 3 * sizeof(float), hipMemcpyDeviceToHost,
@@ -3149,11 +3247,12 @@ rt_status rt_forest_render(rt_forest* f, float* rgb) {
 
 rt_status rt_forest_render_filter(rt_forest* f, const int32_t* mutated_ids, uint32_t n_ids, float* rgb) {
     if (!f || !rgb || (n_ids && !mutated_ids)) return RT_ERR_INVALID_ARG;
+    if (forest_stale(f)) return RT_ERR_INVALID_ARG;
     HIP_TRY(hipSetDevice(f->s->device));
     hipStream_t st = f->s->stream;
     size_t bytes = forest_pixels(f) * 3 * sizeof(float);
     HIP_TRY(hipMemcpyAsync(f->frame, rgb, bytes, hipMemcpyHostToDevice, st));  // untouched pixels keep these
-    rt_status r = forest_mark(f, mutated_ids, n_ids, false);
+    rt_status r = forest_mark(f, mutated_ids, n_ids, false, f->ev[2]);
     if (r != RT_OK) return r;
     r = forest_shade(f, f->mark);
     if (r != RT_OK) return r;

@@ -134,3 +134,43 @@ def test_set_material_rejects_kind_change():
     s = DeviceScene(SceneDesc.my_scene())
     with pytest.raises(RtError):  # material 3 of my_scene is a TexturePhong
         s.set_material(3, phong_material((0, 0, 0), (1, 1, 1), (1, 1, 1), 10.0, 0.0, 0.0))
+
+
+def _threads():
+    from .test_gpu_fullframe import host_threads
+    return host_threads()
+
+
+def test_forest_config3_benchmark_frame():
+    """The benchmark frame (config 3: 1920x1080, depth 8, 1k primitives) as a ray forest:
+    generate_ray_forest + render_forest (render_tree.rs:121-164) against the oracle's forest on
+    EVERY pixel (bits equal, or NaN in both), tree sizes and RayForest::trees_with exact; then a
+    material edit and render_forest_filter (render_tree.rs:129-145, the GUI's re-shade) on every
+    pixel too.  The oracle forest is built over the host threads (~10-20 s on the box)."""
+    from .test_gpu_fullframe import report
+    desc = SceneDesc.synth_config(3)
+    w, h, depth = 1920, 1080, 8
+    s = DeviceScene(desc, device=0)
+    o = OracleScene(desc)
+    f = s.forest(w, h, depth)
+    fo = o.forest(w, h, depth, threads=_threads())
+    img, ref = f.render(), fo.render()
+    worst, bad, nan_eq, msg = report(img, ref)
+    assert bad == 0 and nan_eq, msg
+    assert np.array_equal(f.tree_sizes(), fo.tree_sizes())
+    # the forest's trees are render.rs's trees: the same ray counts as rt_render's frame
+    _, rcnt, _, _ = s.render(w, h, depth)
+    assert f.counters() == rcnt
+    for k in (0, 5, 11, 20, 350, 610, 700, 725, 726):  # spheres (0..11 collide with cube ids), a cube's, triangles, planes
+        assert f.trees_with(k) == fo.trees_with(k), k
+    # a GUI edit of sphere 20's material, re-shaded through the filter
+    k = int(desc.editable().shapes[20].material)
+    m = phong_material((0.02, 0.0, 0.05), (0.3, 0.8, 0.2), (0.6, 0.6, 0.6), 90.0, 0.4, 0.0)
+    s.set_material(k, m)
+    o.set_material(k, m)
+    got = f.render_filter([20], img)
+    want = fo.render_filter([20], ref)
+    worst, bad, nan_eq, msg = report(got, want)
+    assert bad == 0 and nan_eq, msg
+    assert (got != img).any()
+    f.close()
