@@ -14,15 +14,8 @@
 #include "rt_device.hpp"
 #include "rt_libmf.hpp"
 #include "rt_powf.hpp"
-// the specular power (material.rs:211): glibc's powf, bit for bit; RT_POWF_OCML=1 builds
-// ocml's powf instead (timing A/B only -- not the reference's values)
-#ifndef RT_POWF_LDS
-#define RT_POWF_LDS 1  // tables in LDS: +1% over constant-memory reads (951 / 950 vs 943 / 937 Mpixels/s)
-#endif
-#if RT_POWF_OCML
-#define RT_POW(x, y) powf((x), (y))
-#elif RT_POWF_LDS
-// the tables in LDS: every kernel that shades calls rt_pow_stage() first
+// the specular power (material.rs:211): glibc's powf, bit for bit (rt_powf.hpp); its tables in
+// LDS (+1% over constant-memory reads): every kernel that shades calls rt_pow_stage() first
 __shared__ rtpow::Log2Entry rt_pow_log2[16];
 __shared__ uint64_t rt_pow_exp2[32];
 struct LdsTabs {
@@ -35,12 +28,6 @@ __device__ __forceinline__ void rt_pow_stage() {
     __syncthreads();
 }
 #define RT_POW(x, y) rtpow::powf_glibc<true, LdsTabs>((x), (y))
-#else
-#define RT_POW(x, y) rtpow::powf_glibc((x), (y))
-#endif
-#if !RT_POWF_LDS
-__device__ __forceinline__ void rt_pow_stage() {}
-#endif
 
 namespace rtdev {
 

@@ -1,4 +1,4 @@
-// rt_device.hpp -- device-side scene layout shared by the host builder (rt_api.cpp) and
+// rt_device.hpp -- device-side scene layout shared by the host builder (rt_build.cpp) and
 // the HIP kernels (rt_wavefront.hip, rt_order.hip, rt_frame.hip).
 //
 // The scene lives in ONE device allocation, cut into per-type runs so the hot
@@ -32,7 +32,7 @@ namespace rtdev {
 struct ShapeRec {
     int32_t kind, mat;
     uint32_t center_key;  // sphere / cube: 15-bit Morton code of its centre (rt_wavefront.hip task_key)
-    int32_t pad1;         // sphere: its shape buffer's leaf + 1 (0: none; rt_api.cpp build_shape_buffers)
+    int32_t pad1;         // sphere: its shape buffer's leaf + 1 (0: none; rt_build.cpp build_shape_buffers)
     float inv[12];   // rows 0..2 of the inverse transform (row 3 is never read)
     float a[16];     // plane: n(3) origin(3) Tn(3) u(3) v(3); triangle: v0 e1 e2 normal;
                      // sphere with a shape buffer: its bounding ball's centre (3) and radius
@@ -45,7 +45,7 @@ struct TexRec {
 
 struct MatRec {
     int32_t kind;
-    int32_t dark_zero;   // 1: an unlit point light's term is exactly +-0 for this material (rt_api.cpp mat_rec)
+    int32_t dark_zero;   // 1: an unlit point light's term is exactly +-0 for this material (rt_build.cpp mat_rec)
     float power, reflectivity;
     float refraction_index, pad1, pad2, pad3;
     TexRec ambient, diffuse, specular;
@@ -93,7 +93,7 @@ struct DevScene {
     uint32_t graze_res, graze_words;  // 0: the cone path (rt_scan.hpp graze_pass)
     uint32_t graze_lane;       // 1: each lane tests its own cell's pairs first (per-lane grazing sets)
     unsigned long long* scan_ops;  // RT_OPS_* lane-weighted test counts
-    // light buffers (shadow rays; rt_api.cpp build_light_buffers): per point light
+    // light buffers (shadow rays; rt_build.cpp build_light_buffers): per point light
     // 6 x lb_res x lb_res cells, each a leaf of bvh_leaves (LightRec::lb_base + cell)
     uint32_t lb_res;           // 0: no light buffers
     float lb_dmax;             // tier t of a light's buffer holds origins with D <= lb_dmax 2^t
@@ -246,7 +246,7 @@ struct WaveParams {
     // supersampling (rt_render_spp): this pipeline run traces sample `sample` of `spp`;
     // level 0 jitters the primary ray (spp > 1) and the level-0 combine accumulates
     uint32_t spp, sample, seed;
-    // sample batches (rt_api.cpp launch_bands_wave): this pass's `frames` are samples
+    // sample batches (rt_render.cpp launch_bands_wave): this pass's `frames` are samples
     // sample + f of one camera; the level-0 combine writes each sample's raw colour to its
     // own buffer (out + f x frame_floats) and spp_accumulate_kernel sums them in sample order
     uint32_t spp_batch;
@@ -254,10 +254,7 @@ struct WaveParams {
     uint32_t l0_interleave;            // frames > 1: level-0 tiles dealt to the frames in turn (default; RT_L0_INTERLEAVE=0 off)
     uint32_t self_shadow;              // trace decides shadow rays its own shape settles (A/B: RT_SELF_SHADOW=0)
     uint32_t inline_levels;            // trace levels < this trace their own shadow rays (RT_INLINE_SHADOW)
-    uint32_t sched;                    // work distribution of trace / shadow launches (rt_wavefront.hip sched_base)
-    uint32_t* task_clock;              // debug (RT_TASK_CLOCK): [0] count, then {level, base, ticks, lanes} per wave iteration
-    uint32_t task_clock_cap;
-    uint32_t reverse_levels;           // bit k: level k's queue is traced from its end (A/B, RT_REVERSE)
+    uint32_t sched;                    // trace kernels' work distribution (Tune::sched, rt_wavefront.hip sched_base)
     uint32_t task_w_min;               // narrowest trace task (rays per wave iteration; 64 = never narrowed)
     float task_w_fill;                 // trace tasks are narrowed while a level has fewer than fill x wave slots of them
     // host-side launch choices (Tune, rt_wavefront.hip's launchers): walk records staged in LDS

@@ -96,7 +96,7 @@ hipError_t launch_quantize(const float* in, size_t n, uint8_t* out, hipStream_t 
 }
 
 
-// ---- sample batches (rt_api.cpp launch_bands_wave): the batch's samples first .. first + n - 1
+// ---- sample batches (rt_render.cpp launch_bands_wave): the batch's samples first .. first + n - 1
 // were rendered into n buffers of frame_floats floats; fold them into `out` in sample order
 // -- sample 0 starts the sum, each later sample is added to it (the f32 sample-order sum of
 // rt_render_spp, include/rt_api.h) -- and the batch holding the last sample divides by spp

@@ -1,5 +1,5 @@
 // rt_internal.hpp -- what rt_multi.cpp (the multi-device render behind rt_scene_create_multi)
-// needs from rt_api.cpp's scene handle.  Not part of the C ABI.
+// needs from rt_scene.cpp's scene handle.  Not part of the C ABI.
 #pragma once
 #include <functional>
 

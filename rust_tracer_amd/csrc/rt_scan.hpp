@@ -19,12 +19,12 @@
 #pragma once
 // (included inside namespace rtdev, after the V3 helpers of rt_kernels.hip)
 
-// RT_STATS builds (tools only) count, per wave, how often each divergent hit path of the
+// RT_DIAG builds (tools only) count, per wave, how often each divergent hit path of the
 // scan is entered; the counts go to rt_scan_stats (see tools/scan_stats.py).
-#ifndef RT_STATS
-#define RT_STATS 0
+#ifndef RT_DIAG
+#define RT_DIAG 0
 #endif
-#if RT_STATS
+#if RT_DIAG
 __device__ unsigned long long rt_scan_stats[40];
 #define RT_STAT(i) do { if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == \
     (uint32_t)__builtin_ctzll(__ballot(1))) atomicAdd(&rt_scan_stats[i], 1ull); } while (0)
@@ -315,24 +315,13 @@ __device__ __forceinline__ unsigned long long* ops_slot(const DevScene& S) {
     return S.scan_ops + (blockIdx.x % RT_OPS_SLOTS) * RT_OPS_STRIDE;
 }
 
-// Leaf loops load record i + 1 while testing record i (RT_LEAF_PREFETCH=1, default) or
-// load each record at the top of its iteration (0: half the SGPRs, A/B)
-#ifndef RT_LEAF_PREFETCH
-#define RT_LEAF_PREFETCH 1
-#endif
-#if RT_LEAF_PREFETCH
+// Leaf loops load record i + 1 while testing record i (loading each record at the top of its
+// iteration instead: 4.65 vs 4.62 ms, round 1)
 #define RT_PF_INIT(T, ld, p) T cur = ld(p);
 #define RT_PF_NEXT(T, ld, p, K) \
     p += K;                     \
     T nxt = ld(p);
 #define RT_PF_ADV cur = nxt;
-#else
-#define RT_PF_INIT(T, ld, p)
-#define RT_PF_NEXT(T, ld, p, K) \
-    T cur = ld(p);              \
-    p += K;
-#define RT_PF_ADV
-#endif
 
 // ------------------------------------------------------------------ linear runs
 // Group loops prefetch record i+1 before testing record i; every section is padded by
@@ -413,7 +402,7 @@ __device__ __forceinline__ void run_cube(const DevScene& S, int b, int e, V3 o, 
 // satisfies: the point o + t*d lies within h(D) = (g2 D + g1) D + g0 of the primitive for
 // some t* with |t' - t*| <= m(D)/|d|.  Every primitive's bound is on the reported point
 // itself (t* = t', m = 0 today); triangles for rays meeting their plane at
-// sin(phi) >= sin(phi_T), the triangle's own grazing threshold (rt_api.cpp graze_sin).
+// sin(phi) >= sin(phi_T), the triangle's own grazing threshold (rt_build.cpp graze_sin).
 // h also covers the rounding of this slab test.  A child box is skipped for a lane only
 // when its box grown by h misses the ray on [-m, t_max + m] (t_max = the lane's best t,
 // or the shadow limit); the wave skips it only when every lane does.  Spheres,
@@ -554,7 +543,7 @@ template <bool SHADOW, bool LDS, class C>
 __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, float tlim,
                                          float l2, C& c, lfloat4* lnodes, bool novote = false) {
     const BvhRay R = bvh_ray(S, o, d);
-#if RT_STATS
+#if RT_DIAG
     if (!SHADOW) {  // slots 23-28: trace walks' lanes by D / R in (0,3] (3,6] (6,12] (12,25] (25,50] (50,inf);
                     // 29-31: leaf visits of waves whose farthest lane is within 3 R / 12 R / beyond
         const float dx = o.x - S.bvh_cx, dy = o.y - S.bvh_cy, dz = o.z - S.bvh_cz;
@@ -574,7 +563,7 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
         rt_far_class = __ballot(q > 12.f) ? 2u : (__ballot(q > 3.f) ? 1u : 0u);
     }
 #endif
-#if RT_STATS
+#if RT_DIAG
     // leaf-major planning (DESIGN.md "Leaf-major trace pass"): the leaves a trace ray's own
     // box tests admit with no nearest-hit bound during the walk (its bound at the start:
     // infinite, or the enclosing sphere's exit) -- slot 32, rays in slot 33 -- and, after the
@@ -614,7 +603,7 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
     uint32_t sp = 0;
     uint32_t cur = S.bvh_root;
     bool done = SHADOW ? (novote || shadow_decided(o, d, bt, l2)) : false;
-#if RT_STATS
+#if RT_DIAG
     // lanes whose own box test admitted the current node (stats build only)
     __shared__ uint64_t rt_need_stack[4 * 32];
     uint64_t* nstk = rt_need_stack + ((threadIdx.x >> 6) << 5);
@@ -630,7 +619,7 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
         float tnode = (tmax < 0.f) ? -__builtin_huge_valf() : tmax + R.m;
         RT_T0(C, t_it);
         if (cur & BVH_LEAF) {
-#if RT_STATS
+#if RT_DIAG
             {
                 uint64_t act = __ballot(SHADOW ? !done : true);
                 if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == (uint32_t)__builtin_ctzll(__ballot(1))) {
@@ -693,13 +682,13 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
         RT_NEED(need = nstk[sp - 1];)
         cur = rfl(stk[--sp]);
     }
-#if RT_STATS
+#if RT_DIAG
     if (!SHADOW && !novote) atomicAdd(&rt_scan_stats[34], (unsigned long long)lane_leaves(bt));
 #endif
 }
 
 // cube-map cell of a direction (face = largest |component|, ties x > y > z); the host
-// builds light buffers and grazing masks over the same cells (rt_api.cpp lb_face_dir)
+// builds light buffers and grazing masks over the same cells (rt_build.cpp lb_face_dir)
 __device__ __forceinline__ uint32_t lb_cell(uint32_t res, V3 v) {
     const float ax = fabsf(v.x), ay = fabsf(v.y), az = fabsf(v.z);
     uint32_t f;
@@ -728,7 +717,7 @@ __device__ __forceinline__ uint32_t lb_cell(uint32_t res, V3 v) {
 
 // The light-buffer tier a shadow ray's origin falls in -- the first tier t with D <=
 // lb_dmax 2^t and a light within RT_LB_LMAX 2^t (the buffers built for that reach and that
-// direction error, rt_api.cpp build_light_buffers) -- or -1: no buffer (the light has none,
+// direction error, rt_build.cpp build_light_buffers) -- or -1: no buffer (the light has none,
 // or the origin lies beyond its tiers) -- walk.  LightRec::lb_base: the light's first cell in
 // bits 0-27, its tier count in bits 28-30 (~0: no buffer).
 // ... for the origin's D = |o - c| + R given (the trace kernel's queue keys: D once per hit)
@@ -755,12 +744,9 @@ __device__ __forceinline__ int lb_tier(const DevScene& S, uint32_t lb_base, V3 o
 struct GrazePre {
     uint32_t m0, m1;
 };
-#ifndef RT_GRAZE_PRE
-#define RT_GRAZE_PRE 0  // 1: prefetch the mask words at scan start (trace kernel scratch 100 -> 204 B; -1.2%)
-#endif
 __device__ __forceinline__ GrazePre graze_prefetch(const DevScene& S, V3 d) {
     GrazePre g{0u, 0u};
-    if (RT_GRAZE_PRE && S.graze_res && S.n_graze_blk) {
+    if (false && S.graze_res && S.n_graze_blk) {
         const uint32_t* mp = S.graze_mask + (size_t)lb_cell(S.graze_res, d) * S.graze_words;
         g.m0 = mp[0];
         if (S.graze_words > 1) g.m1 = mp[1];
@@ -788,12 +774,12 @@ __device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float&
             lfloat4* lpn = lnodes + 4 * S.n_bvh_nodes;
             // the first two words requested together (one memory round trip where a scene has
             // at most 64 grazing pairs, config 3: 50)
-            const uint32_t w0 = (RT_GRAZE_PRE || novote) ? 0u : mp[0];
-            const uint32_t w1 = (RT_GRAZE_PRE || novote || S.graze_words < 2) ? 0u : mp[1];
+            const uint32_t w0 = (false || novote) ? 0u : mp[0];
+            const uint32_t w1 = (false || novote || S.graze_words < 2) ? 0u : mp[1];
             for (uint32_t w = 0; w < S.graze_words; ++w) {
                 uint32_t own = novote ? 0u
-                                      : (w == 0 ? (RT_GRAZE_PRE ? pre.m0 : w0)
-                                                : (w == 1 ? (RT_GRAZE_PRE ? pre.m1 : w1) : mp[w]));
+                                      : (w == 0 ? (false ? pre.m0 : w0)
+                                                : (w == 1 ? (false ? pre.m1 : w1) : mp[w]));
                 RT_OPS(c, graze);
                 uint32_t real = 0u;  // the pairs of word w this lane grazes
                 while (own) {        // divergent: as many rounds as the longest list
@@ -832,7 +818,7 @@ __device__ __forceinline__ void graze_pass(const DevScene& S, V3 o, V3 d, float&
         cfloat4* pn = cptr(S.graze_pn);
         for (uint32_t w = 0; w < S.graze_words; ++w) {
             // the pairs this lane's direction cell lists: a superset of the pairs it grazes
-            const uint32_t own = (RT_GRAZE_PRE && w == 0) ? pre.m0 : ((RT_GRAZE_PRE && w == 1) ? pre.m1 : mp[w]);
+            const uint32_t own = (false && w == 0) ? pre.m0 : ((false && w == 1) ? pre.m1 : mp[w]);
             RT_OPS(c, graze);
             // Every pair some active lane lists, each once: take the first lane that still
             // lists an untested pair, test all of its untested pairs, repeat.  Ballots and
@@ -934,7 +920,7 @@ __device__ __forceinline__ void scan_from(const DevScene& S, V3 o, V3 d, float& 
     linear_rest(S, o, d, bt, bk, c);
     RT_T1(C, c, cyc_scan, t_s);
 }
-// scan_from for lanes that may hold a shape buffer (rt_api.cpp build_shape_buffers): a lane
+// scan_from for lanes that may hold a shape buffer (rt_build.cpp build_shape_buffers): a lane
 // with buf_ok (its segment to the enclosing sphere's exit lies in the sphere's ball, bt = that
 // exit) tests the buffer's records instead of walking the hierarchy; the wave takes its
 // lanes' buffers one after the other, each tested like a leaf by every lane (a record tested
@@ -976,7 +962,7 @@ __device__ __forceinline__ void scan(const DevScene& S, V3 o, V3 d, float& bt, u
 }
 
 // ------------------------------------------------------------------ light buffers
-// (rt_api.cpp build_light_buffers, DESIGN.md "Light buffers")
+// (rt_build.cpp build_light_buffers, DESIGN.md "Light buffers")
 
 // max of x over the active lanes (NaN lanes ignored unless the first lane's is NaN, which
 // only makes the caller's reach unbounded), wave-uniform: each round jumps to a lane above
@@ -1129,7 +1115,7 @@ __device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lp
             if (SPLIT) RT_T1(C, c, cyc_post, t_lb);
         }
         RT_T0(C, t_w);
-#if RT_STATS
+#if RT_DIAG
         {  // slot 15: lanes a hierarchy walk serves (no light buffer, undecided); slots 16-21:
            // those lanes by D / R in (0,3] (3,6] (6,12] (12,25] (25,50] (50,inf); 22: light
            // farther than RT_LB_LMAX

@@ -78,6 +78,7 @@ bool apply_one(Tune& t, const std::string& k, const std::string& v, bool build) 
     if (k == "task_key") return set_int(v, 0, 7, t.task_key);
     if (k == "self_shadow") return set_int(v, 0, 1, t.self_shadow);
     if (k == "inline_shadow") return set_int(v, 0, 1024, t.inline_shadow);
+    if (k == "sched") return set_int(v, 0, 2, t.sched);
     if (k == "task_w") {
         if (!set_int(v, 16, 64, t.task_w)) return false;
         return t.task_w == 16 || t.task_w == 32 || t.task_w == 64;

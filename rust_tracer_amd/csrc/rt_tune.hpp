@@ -44,6 +44,7 @@ struct Tune {
     int self_shadow = 1;      // own-shape shadow pre-test in the trace kernel
     int inline_shadow = 1;    // levels whose shadow rays the trace kernel scans inline
     int task_w = 64;          // narrowest trace task (64 / 32 / 16 rays)
+    int sched = 0;            // trace kernels' work distribution: 0 grid-stride, 1 dynamic, 2 block-contiguous
     double task_fill = 1.0;   // tasks per wave slot below which a level's tasks are narrowed
     int shadow_key = 2;       // shadow queue key: 2 cell2, 1 cell, 16 / 18 / 21 light | Morton bits
     int task_fine = 1;        // frame batches: 21-bit task keys

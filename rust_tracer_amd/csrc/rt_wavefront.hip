@@ -29,15 +29,6 @@
 
 #include "rt_common.hpp"
 
-#ifndef RT_HIT_BULK
-#define RT_HIT_BULK 1  // the trace kernel reads the hit shape's and material's records whole
-#endif
-#ifndef RT_MAT_BULK
-#define RT_MAT_BULK 1  // the combine reads a node's material whole (rt_common.hpp load_mat)
-#endif
-#ifndef RT_EC_LAZY
-#define RT_EC_LAZY 1   // the combine reads a child's colour only where the child was queued
-#endif
 
 
 namespace rtdev {
@@ -104,12 +95,10 @@ __device__ __forceinline__ uint32_t spread5(uint32_t v) {  // abcde -> a..b..c..
 }
 // Queue keys order the queues and nothing else (a key never reaches a result), so their
 // arithmetic takes the hardware's approximate reciprocal and square root instead of the
-// correctly rounded sequences the render's own arithmetic needs (RT_FAST_KEYS=0: exact forms)
-#ifndef RT_FAST_KEYS
-#define RT_FAST_KEYS 1
-#endif
-__device__ __forceinline__ float key_rcp(float x) { return RT_FAST_KEYS ? __builtin_amdgcn_rcpf(x) : 1.f / x; }
-__device__ __forceinline__ float key_sqrt(float x) { return RT_FAST_KEYS ? __builtin_amdgcn_sqrtf(x) : sqrtf(x); }
+// correctly rounded sequences the render's own arithmetic needs (measured flat against the
+// exact forms, round 5)
+__device__ __forceinline__ float key_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float key_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ uint32_t morton15(const DevScene& S, V3 p) {
     float sc = 16.f * key_rcp(S.bvh_r);
     int x = (int)fminf(fmaxf((p.x - S.bvh_cx) * sc + 16.f, 0.f), 31.f);
@@ -156,10 +145,7 @@ __device__ __forceinline__ uint32_t morton21(const DevScene& S, V3 p) {
 // the shape's centre (15-bit Morton) [| direction cell, frame batches]
 // a batch's inside keys hold the ray's direction cell (cube face x 2x2) in their low 5 bits:
 // rays leaving one shape the same way share a wave (943 / 950 / 945 vs 937 / 942 / 938
-// Mpixels/s with the bits left zero, RT_INSIDE_DIR=0)
-#ifndef RT_INSIDE_DIR
-#define RT_INSIDE_DIR 1
-#endif
+// Mpixels/s with the bits left zero)
 // cube-map face of d x 4x4 cells of the face (< 96: 7 bits)
 __device__ __forceinline__ uint32_t dir_cell16(V3 d) {
     float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z), u, v, m;
@@ -175,7 +161,7 @@ __device__ __forceinline__ uint32_t dir_cell16(V3 d) {
 __device__ __forceinline__ uint32_t inside_key(const WaveParams& P, uint32_t center_key, V3 d) {
     if (P.task_fine == 3u) return (1u << 23) | (center_key << 8) | (dir_cell16(d) << 1);  // 24-bit, 4x4 cells
     uint32_t low = 0;
-    if (RT_INSIDE_DIR && P.task_fine) {
+    if (P.task_fine) {
         float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z), u, v;
         uint32_t face;
         if (ax >= ay && ax >= az) { face = d.x < 0.f; u = d.y; v = d.z; }
@@ -279,16 +265,18 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
-// Work distribution of the trace / shadow launches (P.sched, A/B):
+// Work distribution of the trace launches (Tune::sched, A/B; the shadow kernel is always
+// grid-stride):
 //   0  grid-stride: wave w of the grid takes chunks w, w + W, w + 2W, ... (W waves)
-//   1  dynamic: every wave takes its next 64-task chunk from a work counter
+//   1  dynamic: every wave takes its next chunk from a work counter
 //   2  block-contiguous: the blocks of one XCD cover one contiguous range of the queue,
 //      each block a contiguous sub-range, its 4 waves adjacent chunks
-// Measured (config 3, 1080p): 0 -> 4.94 ms, 1 -> 6.68, 2 -> 11.2; remapping the
-// grid-stride block order by XCD or by co-resident blocks: 5.2 - 5.6.  Grid-stride keeps
-// the whole chip on one narrow front of the sorted queue, so the hierarchy nodes and
-// records every CU reads at a time are few (scalar caches and L2 stay warm); every
-// scheme that spreads concurrent waves over the queue loses that.
+// Measured (config 3, 1080p; round 1): 0 -> 4.94 ms, 1 -> 6.68, 2 -> 11.2; the grid-stride
+// block order remapped by XCD or by co-resident blocks: 5.2 - 5.6.  Grid-stride keeps the whole
+// chip on one narrow front of the sorted queue, so the hierarchy nodes and records every CU
+// reads at a time are few (scalar caches and L2 stay warm).  (Round 6: the kernels compiled
+// without modes 1 / 2 allocate registers differently -- 16 B more scratch in the deep-level
+// instantiation, -1.1% -- so the modes stay.)
 // Returns the base of the wave's iteration `it`, or >= count when done.
 __device__ __forceinline__ uint32_t sched_base(const WaveParams& P, uint32_t* counter, uint32_t count, uint32_t it,
                                                   uint32_t W = 64u) {
@@ -309,29 +297,11 @@ __device__ __forceinline__ uint32_t sched_base(const WaveParams& P, uint32_t* co
     return ((blockIdx.x * waves_per_block + wave) + it * gridDim.x * waves_per_block) * W;
 }
 
-// debug (RT_TASK_CLOCK, librt_hip_clk.so from tools/task_clock.sh): one record per finished wave iteration -- level, base task,
-// start tick, ticks (wall clock), active lanes
-__device__ __forceinline__ void task_clock_mark(const WaveParams& P, uint32_t level, uint32_t it, uint32_t base,
-                                             uint64_t& clk0, uint32_t count) {
-    const uint64_t now = wall_clock64();
-    if (it > 0 && lane_id() == 0) {
-        const uint32_t i = atomicAdd(P.task_clock, 1u);
-        if (i < P.task_clock_cap) {
-            uint32_t* r = P.task_clock + 4 + 4 * (size_t)i;
-            r[0] = level;
-            r[1] = (uint32_t)clk0;  // start (low word)
-            r[2] = (uint32_t)(now - clk0);
-            r[3] = count > base ? min(count - base, 64u) : 0u;
-        }
-    }
-    clk0 = now;
-}
-
 // wave-aggregated append of `n` (< 64) consecutive slots per lane to a device counter:
 // one atomic per wave, slots in lane order
 // ... split in two: the atomic is issued by wave_append_begin and its value read by
 // wave_append_end, so that work in between overlaps its round trip (a returning append
-// costs ~1.8% of the frame when waited for at once: RT_EXTRA_ATOMIC)
+// costs ~1.8% of the frame when waited for at once: DESIGN.md, round 5)
 struct AppendTicket {
     uint32_t mine, base, first, total;
 };
@@ -392,50 +362,16 @@ __device__ __forceinline__ void own_shape_test(const DevScene& S, uint32_t key, 
     }
 }
 
-#ifndef RT_TRACE_WAVES
-#define RT_TRACE_WAVES 5  // 96 VGPRs, 20 B scratch (measured: 4 -> 8.02 ms, 5 -> 7.89, 6 -> 7.85 with 84 B)
-#endif
+// Waves per SIMD of the walk kernels: 5 at 96 VGPRs (re-measured every round: 4 and 6 waves
+// lose 1 - 3% for every instantiation; DESIGN.md "Kernels and occupancy")
+constexpr int TRACE_WAVES = 5, SHADOW_WAVES = 5, COMBINE_WAVES = 5;
 extern __shared__ float4 rt_dyn_lds[];
 
 // DEEP: a level past the pixels and the inline shadow scans (level >= max(1, inline_levels)):
 // the instantiation without their code (fewer live registers across the walk).  FIRST:
 // level 0 only (its rays start at the camera: no task loads, no ray inside a shape).
-#ifndef RT_DEEP_WAVES
-#define RT_DEEP_WAVES RT_TRACE_WAVES
-#endif
-#ifndef RT_FIRST_WAVES
-#define RT_FIRST_WAVES RT_TRACE_WAVES  // level 0's instantiation (A/B builds: -DRT_FIRST_WAVES=4)
-#endif
-#ifndef RT_POST_CLOCK
-#define RT_POST_CLOCK 0  // diagnostic builds: wall-clock of the trace iteration's phases (tools/post_clock.py)
-#endif
-#if RT_POST_CLOCK
-// [level 0 / levels >= 1][load, scan, attributes + node record, children, self, shadow entries, iterations]
-__device__ unsigned long long rt_post_clock[2 * 8];
-#define RT_PC(v) v = __builtin_amdgcn_s_memtime()
-#else
-#define RT_PC(v)
-#endif
-#ifndef RT_DIAG_ENTRIES
-#define RT_DIAG_ENTRIES 0  // diagnostic builds (wrong frames): 1 no shadow-entry stores, 2 no shadow append
-#endif
-#ifndef RT_EXTRA_ATOMIC
-#define RT_EXTRA_ATOMIC 0  // measurement builds only: one more returning atomic per trace wave iteration
-#endif
-#if RT_EXTRA_ATOMIC
-__device__ uint32_t rt_extra_words[8 * 32];
-#endif
-#ifndef RT_LATE_TASKS
-#define RT_LATE_TASKS 0    // deep levels: the children's append read after the own-shape shadow tests
-#endif
-#ifndef RT_DEFER_STORES
-// deep levels: both appends issued and read before the wave iteration's first store.  Stores
-// count in vmcnt on gfx9 and the compiler waits with vmcnt(0) once loads and stores are both
-// outstanding, so an append read after a store waits for that store's acknowledgement
-#define RT_DEFER_STORES 1
-#endif
 template <bool COUNT, bool LDS, bool DEEP = false, bool FIRST = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_DEEP_WAVES : (FIRST ? RT_FIRST_WAVES : RT_TRACE_WAVES), 8))) void trace_level_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TRACE_WAVES, 8))) void trace_level_kernel(
     WaveParams P, uint32_t level) {
     const DevScene& S = P.S;
     if (LDS) {  // stage the hierarchy's node records in LDS
@@ -472,33 +408,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         while (W > P.task_w_min && (float)count < P.task_w_fill * slots * (float)W) W >>= 1;
     }
     // whole waves iterate together (the wave-aggregated appends see every lane)
-#if RT_TASK_CLOCK_BUILD
-    uint64_t clk0 = 0;
-    uint32_t clk_base = 0;
-#endif
     // key mode 7 (not for ray forests, whose tasks carry the pixel itself): a task of a ray
     // inside a sphere / cube carries that shape + 1 in the pixel word's low bits
     const bool inside_keys = P.key_mode == 7 && !P.node_pixel;
     // sorted levels, grid-stride: this lane's next permutation entry is requested one
     // iteration ahead, so a task costs one dependent load (the task), not two
     const bool pf_on = level > 0 && P.perm && P.sched == 0;
-    const bool rev = level > 0 && ((P.reverse_levels >> min(level, 31u)) & 1u);
     const uint32_t pf_stride = gridDim.x * (blockDim.x >> 6) * W;
     uint32_t pf_slot = 0;
     bool pf_have = false;
-#if RT_POST_CLOCK
-    uint64_t pc_acc[7] = {0, 0, 0, 0, 0, 0, 0};
-#endif
     for (uint32_t it = 0;; ++it) {
-#if RT_POST_CLOCK
-        uint64_t pc0, pc1, pc2 = 0, pc3, pc4, pc5, pc6;
-#endif
-        RT_PC(pc0);
         const uint32_t base = sched_base(P, &P.levels[RT_WORK_WORD(level)], count, it, W);
-#if RT_TASK_CLOCK_BUILD
-        if (P.task_clock) task_clock_mark(P, level, it, clk_base, clk0, count);
-        clk_base = base;
-#endif
         if (base >= count) {
             if (P.sched == 2 && base != 0xFFFFFFFFu) continue;  // a block's tail past the queue end
             break;
@@ -508,14 +428,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         uint32_t pf_next = 0;
         if (pf_on) {
             const uint32_t tn = t + pf_stride;
-            pf_next = (lane < W && tn < count) ? P.perm[off + (rev ? count - 1u - tn : tn)] : 0u;
+            pf_next = (lane < W && tn < count) ? P.perm[off + tn] : 0u;
         }
         typedef decltype(cnt) CntT;
         RT_T0(CntT, t_load);
         V3 ro = v3(0, 0, 0), rd = v3(0, 0, 0);
         uint32_t parent = 0, pix = 0, in_shape = 0;
-        // rev: the sorted queue is taken from its end (the keys' high end first)
-        const uint32_t n = off + ((rev && active) ? count - 1u - t : t);
+        const uint32_t n = off + t;
         if (active) {
             if (FIRST || (!DEEP && level == 0)) {
                 uint32_t local;
@@ -569,7 +488,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         V3 sh_ps = v3(0, 0, 0), sh_n = v3(0, 0, 0);  // the hit's shadow-ray origin and normal
         bool sh_entering = false;
         uint32_t sh_key = 0;
-        constexpr bool DEFER = DEEP && RT_DEFER_STORES;  // (level 0 too: -4%, its inline scans spill the stores' data)
+        // deep levels: both appends issued and read before the wave iteration's first store.
+        // Stores count in vmcnt on gfx9 and the compiler waits with vmcnt(0) once loads and
+        // stores are both outstanding, so an append read after a store waits for that store's
+        // acknowledgement (level 0 too: -4%, its inline scans spill the stores' data)
+        constexpr bool DEFER = DEEP;
         int32_t sh_kind = 0;             // the hit shape's kind,
         uint32_t own_ck = 0;             // ... its centre key (inside keys),
         float sh_tu = 0.f, sh_tv = 0.f;  // DEFER: the hit's texture coordinates (node record)
@@ -582,7 +505,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
             it_scan0 = cnt.cyc_scan;
             it_self0 = cnt.cyc_self;
         }
-        RT_PC(pc1);
         if (active) {
             n_node++;
             float bt = __builtin_huge_valf();
@@ -611,7 +533,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 scan_from<LDS>(S, ro, rd, bt, bk, cnt, lnodes);
             else
                 scan_buffered<LDS>(S, ro, rd, bt, bk, cnt, lnodes, buf_ok, buf_leaf);
-            RT_PC(pc2);
             if (bk == 0xFFFFFFFFu) {
                 // trace_ray -> BLACK: the parent's child slot gets BLACK (forest: direction 0)
                 if constexpr (DEFER) {
@@ -625,22 +546,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 }
             } else {
                 hit = true;
-#if RT_HIT_BULK
                 // the hit shape's record whole, then its material whole: two round trips
                 const ShapeW SR = load_shape(S.shapes, bk >> 4);
                 const MatRec M = load_mat(S.mats, (uint32_t)SR.mat());
                 Hit h = hit_attrs_w(S, SR, bk, ro, rd, M.kind == RT_MAT_TEXTURE_PHONG);
-#else
-                const MatRec& M = S.mats[S.shapes[bk >> 4].mat];
-                Hit h = hit_attrs(S, bk, ro, rd, M.kind == RT_MAT_TEXTURE_PHONG);
-#endif
                 float ri = M.refraction_index;
                 float n1 = h.entering ? 1.f : ri;
                 float n2 = h.entering ? ri : 1.f;
                 V3 ps = add(h.p, mul(h.n, 0.0002f));  // render.rs:147
                 if (P.shadow_keys)
                     mort = P.shadow_fine == 21u ? morton21(S, ps) : (P.shadow_fine ? morton18(S, ps) : morton15(S, ps));
-#if RT_STATS
+#if RT_DIAG
                 {  // hit points outside the Morton cube (clamped to its faces)
                     const float dx = fabsf(ps.x - S.bvh_cx), dy = fabsf(ps.y - S.bvh_cy), dz = fabsf(ps.z - S.bvh_cz);
                     const bool out = fmaxf(dx, fmaxf(dy, dz)) > S.bvh_r;
@@ -657,13 +573,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 sh_key = bk;
                 // the shape's kind and centre key from its record now: no load after the
                 // iteration's first store (it would wait for that store's acknowledgement)
-#if RT_HIT_BULK
                 sh_kind = SR.kind();
                 own_ck = __float_as_uint(SR.w[0].z);
-#else
-                sh_kind = S.shapes[bk >> 4].kind;
-                own_ck = S.shapes[bk >> 4].center_key;
-#endif
                 if constexpr (DEFER) {
                     sh_tu = h.tu;
                     sh_tv = h.tv;
@@ -698,12 +609,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 }
             }
         }
-        RT_PC(pc3);
         // ---- children -> level k+1 queue
         const uint32_t nc = (want_refl ? 1u : 0u) + (want_refr ? 1u : 0u);
-        // LATE (deep levels, whose own-shape shadow tests issue no vector-memory loads): the
-        // children's slots are read after those tests, which overlap the append's round trip
-        constexpr bool LATE = RT_LATE_TASKS && DEEP && !DEFER;
         // my: the lane's first child slot past next_off (wave_append_end)
         auto write_children = [&](uint32_t my) {
         const uint32_t fkey = (P.frames > 1 && P.frame_keys) ? ((pix >> RT_FRAME_SHIFT) << P.task_frame_shift) : 0u;
@@ -806,15 +713,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                     if (light_at(S, li).kind == RT_LIGHT_POINT)
                         total += (uint32_t)__builtin_popcountll(__ballot(hit && undecided(li)));
                 s_first = (uint32_t)__builtin_ctzll(hits);
-#if RT_DIAG_ENTRIES == 2  // diagnostic: no append (slots overlap; the frame is wrong, the trace's timing is not)
-                s_raw = (n - lane) * 3u % (P.shadow_capacity - 256u);
-#else
                 if (lane == s_first && total) s_raw = atomicAdd(&RT_SHADOW_COUNT(P), total);
-#endif
             }
         };
         auto shadow_base = [&]() -> uint32_t {
-            if (!hits || RT_DIAG_ENTRIES == 2) return s_raw;
+            if (!hits) return s_raw;
             return (uint32_t)__builtin_amdgcn_readlane((int)s_raw, (int)s_first);
         };
         auto shadow_entries = [&](uint32_t sbase) {
@@ -830,7 +733,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                 const uint64_t m = __ballot(want);
                 const uint32_t slot = sbase + group + (uint32_t)__builtin_popcountll(m & lanemask_lt());
                 group += (uint32_t)__builtin_popcountll(m);
-                if (want && !(RT_DIAG_ENTRIES == 1)) {  // (diagnostic 1: no entry stores)
+                if (want) {
                     if (slot < P.shadow_capacity) {
                         if (P.shadow_light) {  // wide entries (> 256 lights)
                             P.shadow[slot] = n;
@@ -848,9 +751,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                                 const LightRec L = light_at(S, li);
                                 const V3 raw = sub(v3(L.px, L.py, L.pz), sh_ps);
                                 const float l2 = len2(raw);
-                                const V3 dir = RT_FAST_KEYS ? neg(raw) : neg(norm(raw));
-                                const bool lb = RT_FAST_KEYS ? lb_tier_at(S, L.lb_base, key_d, l2) >= 0
-                                                             : lb_tier(S, L.lb_base, sh_ps, l2) >= 0;
+                                const V3 dir = neg(raw);
+                                const bool lb = lb_tier_at(S, L.lb_base, key_d, l2) >= 0;
                                 if (!lb) {
                                     low = (1u << (P.shadow_fine - 1u)) |
                                           (P.shadow_fine >= 19u ? mort << (P.shadow_fine - 19u) : mort >> (19u - P.shadow_fine));
@@ -880,7 +782,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
         if constexpr (DEFER) {
             // every load and both appends' values first, then the stores
             self_tests();
-            RT_PC(pc4);
             const AppendTicket child_ticket = wave_append_begin(&P.levels[2 * (level + 1) + 1], nc, lane);
             shadow_begin();
             const uint32_t my = wave_append_end(child_ticket);
@@ -898,49 +799,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
                     if (P.node_dc) P.node_dc[parent] = make_float4(0.f, 0.f, 0.f, 0.f);
                 }
             }
-            RT_PC(pc5);
             shadow_entries(sbase);
         } else {
             const AppendTicket child_ticket = wave_append_begin(&P.levels[2 * (level + 1) + 1], nc, lane);
-            if constexpr (!LATE) write_children(wave_append_end(child_ticket));
-            RT_PC(pc4);
+            write_children(wave_append_end(child_ticket));
             self_tests();
-            RT_PC(pc5);
-            if constexpr (LATE) write_children(wave_append_end(child_ticket));
             shadow_begin();
             shadow_entries(shadow_base());
         }
-#if RT_POST_CLOCK
-        RT_PC(pc6);
-        if (!pc2) pc2 = pc1;  // no lane traced
-        pc_acc[0] += pc1 - pc0;
-        pc_acc[1] += pc2 - pc1;
-        pc_acc[2] += pc3 - pc2;
-        pc_acc[3] += pc4 - pc3;
-        pc_acc[4] += pc5 - pc4;
-        pc_acc[5] += pc6 - pc5;
-        pc_acc[6] += 1;
-#endif
-#if RT_EXTRA_ATOMIC
-        {  // measurement only (tools: A/B of a build with -DRT_EXTRA_ATOMIC=1): one more returning
-           // append-style atomic per wave iteration, its value waited for -- what an append costs
-            uint32_t z = 0;
-            // 1: one word for the whole device; 2: one word per XCD (blockIdx % 8, 128 B apart)
-            if (lane == 0) z = atomicAdd(&rt_extra_words[RT_EXTRA_ATOMIC == 2 ? (blockIdx.x & 7u) * 32u : 0u], 1u);
-            z = (uint32_t)__builtin_amdgcn_readlane((int)z, 0);
-            if (z == 0xFFFFFFFFu) P.node_flags[n] = 0u;
-        }
-#endif
         if constexpr (CntT::kCount)  // the rest of the iteration: attributes, records, children, entries
             cnt.cyc_post += (rt_clock() - t_load) - it_load - (cnt.cyc_scan - it_scan0 - it_scan_self) -
                             (cnt.cyc_self - it_self0);
         pf_slot = pf_next;
         pf_have = pf_on;
     }
-#if RT_POST_CLOCK
-    if (lane == 0)
-        for (int k = 0; k < 7; k++) atomicAdd(&rt_post_clock[(level == 0 ? 0 : 8) + k], (unsigned long long)pc_acc[k]);
-#endif
     for (int o = 32; o > 0; o >>= 1) {
         n_node += __shfl_xor(n_node, o);
         n_pix += __shfl_xor(n_pix, o);
@@ -958,12 +830,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? RT_D
 // Every shadow ray of the frame: PointLight::get_energy's scan + distance test, result as
 // a bit in the node record.
 
-#ifndef RT_LDS_LIGHTS
-#define RT_LDS_LIGHTS 64  // the shadow kernel stages up to this many lights in LDS (0: never)
-#endif
-#ifndef RT_SHADOW_WAVES
-#define RT_SHADOW_WAVES 5  // 96 VGPRs (round 4, light-buffer tiers: 5 / 6 / 8 waves 1236 / 1229 / 1196 Mpixels/s at K = 20, 3 runs each; round 3: 6 was +0.5 - 1% over 5)
-#endif
+// the shadow kernel stages up to this many lights in LDS
+constexpr int LDS_LIGHTS = 64;
 // shadow entry t of the (sorted) queue -> its node and light.  Packed: (node << light_bits) |
 // light.  Wide (> 256 lights): shadow_in holds the entry's slot (or null: slot t), the node
 // and light sit in shadow[slot] and shadow_light[slot].
@@ -984,8 +852,7 @@ __device__ __forceinline__ uint32_t shadow_node(const WaveParams& P, uint32_t e)
 }
 
 template <bool LDS, bool COUNT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_WAVES, 8))) void shadow_kernel(WaveParams P) {
-    if (RT_DIAG_ENTRIES) return;  // diagnostic builds whose shadow queue holds no valid entries
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SHADOW_WAVES, 8))) void shadow_kernel(WaveParams P) {
     const DevScene& S = P.S;
     if (LDS) {  // stage the hierarchy's node records in LDS
         for (int i = threadIdx.x; i < 4 * S.n_bvh_nodes; i += blockDim.x) rt_dyn_lds[i] = S.bvh_nodes[i];
@@ -1002,8 +869,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
     }
     // the lights' positions and light-buffer bases in LDS (an entry's light is per lane): read
     // with an LDS load, not a vector load that would wait for the previous lit-bit atomic
-    __shared__ float4 lds_lights[RT_LDS_LIGHTS > 0 ? RT_LDS_LIGHTS : 1];
-    const bool lights_lds = RT_LDS_LIGHTS > 0 && S.n_lights <= RT_LDS_LIGHTS;
+    __shared__ float4 lds_lights[LDS_LIGHTS];
+    const bool lights_lds = S.n_lights <= LDS_LIGHTS;
     if (lights_lds) {
         for (int i = threadIdx.x; i < S.n_lights; i += blockDim.x) {
             const LightRec L = light_at(S, i);
@@ -1018,7 +885,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
     typename std::conditional<COUNT, ScanCnt, NoCnt>::type cnt;
     if constexpr (COUNT) cnt_init(cnt);
     bc_init();
-    if (P.sched == 0) {
+    {
         // grid-stride, software-pipelined: the next iteration's entry is requested before this
         // iteration's scan and its origin before this iteration's lit-bit atomic, so the next
         // iteration waits neither for an HBM round trip nor for the atomic (vmcnt counts loads,
@@ -1053,27 +920,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_SHADOW_W
             base += stride;
             t = tn;
             e = en;
-        }
-    } else {
-        for (uint32_t it = 0;; ++it) {
-            const uint32_t base = sched_base(P, &P.levels[RT_WORK_WORD(RT_MAX_DEPTH + 1)], count, it);
-            if (base >= count) {
-                if (P.sched == 2 && base != 0xFFFFFFFFu) continue;  // a block's tail past the queue end
-                break;
-            }
-            const uint32_t t = base + lane;
-            if (t < count) {
-                uint32_t n, li;
-                shadow_unpack(P, shadow_raw(P, t), n, li);
-                const float4 q = P.node_ps[n];
-                V3 ps = v3(q.x, q.y, q.z);
-                const LightRec L = light_at(S, li);
-                V3 lpos = v3(L.px, L.py, L.pz);
-                V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
-                n_shadow++;
-                if (!shadow_scan<LDS, decltype(cnt), true>(S, ps, ldir, lpos, cnt, lnodes, L.lb_base))
-                    atomicOr(lit_word(P, n, li), 1u << (li & 31u));
-            }
         }
     }
     for (int o = 32; o > 0; o >>= 1) n_shadow += __shfl_xor(n_shadow, o);
@@ -1149,10 +995,7 @@ __device__ __forceinline__ V3 light_sum(const DevScene& S, const MatRec& M, cons
 }
 
 // render.rs:57-68 + :100 for every node of `level`; children (level + 1) already reported.
-#ifndef RT_COMBINE_WAVES
-#define RT_COMBINE_WAVES 5
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_COMBINE_WAVES, 8))) void combine_level_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMBINE_WAVES, 8))) void combine_level_kernel(
     WaveParams P, uint32_t level) {
     rt_pow_stage();
     const DevScene& S = P.S;
@@ -1168,14 +1011,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_COMBINE_
         const uint32_t flags = P.node_flags[n];
         // every input of the node requested at once (one memory round trip, not three: flags,
         // then the record, then the children's colours); the slots of a miss, of padding or of
-        // an absent child hold stale values that are never used.  RT_EC_LAZY: the children's
+        // an absent child hold stale values that are never used.  The children's
         // colours are read only where a child was queued, together with the material record
         // that needs the flags anyway (no extra round trip; 64% of config 3's nodes have none)
         const float4 qa = P.node_ps[n], qb = P.node_n[n], qc = P.node_d[n];
         const uint32_t litmask = P.node_lit[n];
-#if !RT_EC_LAZY
-        const float4 er = P.node_ec[2u * n], et = P.node_ec[2u * n + 1u];
-#endif
         // frame batches: level-0 node t belongs to frame t / frame_items
         uint32_t local = t;
         const uint32_t fr = level == 0 ? item_frame(P, t, local) : 0u;
@@ -1199,16 +1039,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_COMBINE_
         V3 c = v3(0.f, 0.f, 0.f);
         uint32_t parent = 0;
         if (flags & NODE_HIT) {
-#if RT_MAT_BULK
             const MatRec M = load_mat(S.mats, flags >> F_MAT_SHIFT);
-#else
-            const MatRec& M = S.mats[flags >> F_MAT_SHIFT];
-#endif
-#if RT_EC_LAZY
             const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
             const float4 er = (flags & F_HAS_R) ? P.node_ec[2u * n] : z4;
             const float4 et = (flags & F_HAS_T) ? P.node_ec[2u * n + 1u] : z4;
-#endif
             const NodeIn q = node_in(qa, qb, qc, flags, M);
             parent = q.parent;
             const V3 ka = tex_eval(M.ambient, q.h.tu, q.h.tv);
@@ -1422,7 +1256,7 @@ hipError_t launch_wave_trace(const WaveParams& p, uint32_t level, int blocks, hi
     // the deep instantiation past level 0 and the inline shadow levels (deep_kernel=0: never, A/B)
     const bool deep_ok = p.deep_kernel != 0;
     const bool deep = deep_ok && level > 0 && level >= p.inline_levels && !(p.count_mask & 1u);
-    // occ_each=1 (A/B builds whose instantiations differ in occupancy, e.g. RT_FIRST_WAVES)
+    // occ_each=1 (builds whose instantiations differ in occupancy)
     const bool occ_each_on = p.occ_each != 0;
     if (occ_each_on && occ_each && occ_min > 0 && !(p.count_mask & 1u)) {
         const int v = (level == 0 && deep_ok) ? 1 : (deep ? 2 : 0);
@@ -1489,19 +1323,7 @@ hipError_t launch_wave_combine(const WaveParams& p, uint32_t level, int blocks, 
 
 }  // namespace rtdev
 
-#if RT_POST_CLOCK
-// tools/post_clock.py: read (and optionally reset) the trace iteration's phase clocks
-extern "C" int rt_debug_post_clock(unsigned long long* out16, int reset) {
-    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(rtdev::rt_post_clock), 16 * sizeof(unsigned long long)) != hipSuccess)
-        return 1;
-    if (reset) {
-        unsigned long long z[16] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(rtdev::rt_post_clock), z, sizeof(z)) != hipSuccess) return 1;
-    }
-    return 0;
-}
-#endif
-#if RT_STATS
+#if RT_DIAG
 // tools/scan_stats.py: read (and optionally reset) the wavefront pipeline's scan counters
 extern "C" int rt_debug_scan_stats(unsigned long long* out40, int reset) {
     if (hipMemcpyFromSymbol(out40, HIP_SYMBOL(rtdev::rt_scan_stats), 40 * sizeof(unsigned long long)) != hipSuccess)

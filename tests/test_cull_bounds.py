@@ -1,8 +1,8 @@
 """The culling hierarchy's error bounds (DESIGN.md "Exact culling") against the
 reference arithmetic, replayed in numpy float32 on adversarial rays
-(tools/cull_bounds_check.py).  rt_api.cpp multiplies each basis by a safety factor
+(tools/cull_bounds_check.py).  rt_build.cpp multiplies each basis by a safety factor
 (sphere 4, cube 32; triangles 4 on rho for sin(phi) < 0.1 and 4 x 10 on rho / sin(phi)
-above, rt_api.cpp SAFETY_TRI / TRI_STEEP); the largest ratio measured here must stay a
+above, rt_build.cpp SAFETY_TRI / TRI_STEEP); the largest ratio measured here must stay a
 factor 4 below it, or the product would cull hits the reference reports."""
 import pytest
 

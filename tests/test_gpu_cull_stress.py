@@ -146,7 +146,7 @@ def test_stress_scenes_match_oracle(seed, scale, cam_mode, near, slivers):
 
 @pytest.mark.parametrize("case", [None] + CASES[:3] + CASES[4:5])
 def test_shape_buffers_change_nothing(case, monkeypatch):
-    """Rays inside a sphere test its shape buffer instead of walking the hierarchy (rt_api.cpp
+    """Rays inside a sphere test its shape buffer instead of walking the hierarchy (rt_build.cpp
     build_shape_buffers): frames and counters identical to the walk (RT_SHAPE_BUF=0) and to
     the key mode without inside rays (task_key=6)."""
     if case is None:
@@ -166,7 +166,7 @@ def test_shape_buffers_change_nothing(case, monkeypatch):
 
 @pytest.mark.parametrize("case", [None] + CASES)
 def test_light_buffer_tiers_change_nothing(case):
-    """Light-buffer tiers (rt_api.cpp build_light_buffers: tier t serves shadow-ray origins
+    """Light-buffer tiers (rt_build.cpp build_light_buffers: tier t serves shadow-ray origins
     with D <= 3 R 2^t and a light within 45 * 2^t, its records' balls grown by their bound at
     that reach): frames and counters identical with one tier, the default, seven, no light
     buffers at all (every shadow ray walks the hierarchy), and six tiers for every light with

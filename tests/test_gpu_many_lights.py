@@ -2,7 +2,7 @@
 their shadow results in each node's node_lit word, lights 32 and up in node_lit_hi (zeroed per
 pass); the trace kernel's own-shape tests and inline scans decide lights 0-31 only, the rest
 always go to the shadow queue; the shadow kernel keeps up to 64 lights' positions in LDS
-(rt_wavefront.hip RT_LDS_LIGHTS) and reads the rest from the scene's records.  Frames and
+(rt_wavefront.hip LDS_LIGHTS) and reads the rest from the scene's records.  Frames and
 counters against the oracle at 32, 33, 64, 70 and 300 lights (above 256 lights a shadow entry
 is 8 B, node and light side by side: rt_device.hpp shadow_light); RT_MAX_LIGHTS + 1 (65537) are
 refused."""

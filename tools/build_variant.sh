@@ -3,7 +3,8 @@
 #   tools/build_variant.sh NAME "-DRT_SWITCH=0 ..."  -> rust_tracer_amd/librt_hip_NAME.so
 # (load it with RT_LIB=rust_tracer_amd/librt_hip_NAME.so; tools/ab_env.sh takes RT_LIB=...)
 # "-DRT_DIAG=1" builds the diagnostic knobs (result-changing measurement switches, debug
-# prints, RT_TASK_CLOCK records) that the product library does not contain.
+# prints, the scan hit-path and leaf-occupancy counters of tools/scan_stats.py) that the
+# product library does not contain.
 set -e
 NAME=$1; FLAGS=$2
 R=$(cd "$(dirname "$0")/.." && pwd)

@@ -17,10 +17,10 @@ primitive, and prints the largest ratio  distance / bound-basis  per primitive t
 with l = o' (the object-space origin), lam = |L|_F |o| + |s| (the magnitudes the
 rounding of L o + s scales with), phi the angle between the ray and the triangle plane.
 
-rt_api.cpp multiplies each basis by a safety factor that must exceed the ratios printed
+rt_build.cpp multiplies each basis by a safety factor that must exceed the ratios printed
 here by a wide margin.  Triangles report two numbers: rho = distance / basis over rays
 with sin(phi) < 0.1 (the grazing range, where 1/sin(phi) is large), and for steeper rays
-distance * sin(alpha) / (eps (...)), i.e. rho / sin(phi) (the box growth rt_api.cpp
+distance * sin(alpha) / (eps (...)), i.e. rho / sin(phi) (the box growth rt_build.cpp
 caps at TRI_STEEP).  The line distance of the ray from the triangle is printed for
 reference only: the hierarchy bounds the reported POINT, which lies on the ray.
 

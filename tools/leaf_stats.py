@@ -1,4 +1,4 @@
-"""Leaf occupancy of the wave-uniform walk (RT_STATS build, tools/scan_stats.sh):
+"""Leaf occupancy of the wave-uniform walk (RT_DIAG build, tools/scan_stats.sh):
 of the lanes active at each leaf visit, how many had their own box test admit the leaf.
 usage: RT_LIB=rust_tracer_amd/librt_hip_stats.so python tools/leaf_stats.py [config]"""
 import ctypes as C

@@ -1,4 +1,4 @@
-"""Per-level frequency of the scan's divergent hit paths (RT_STATS build).
+"""Per-level frequency of the scan's divergent hit paths (RT_DIAG build).
 Level k statistics = stats(depth k+1) - stats(depth k).
 usage: RT_LIB=rust_tracer_amd/librt_hip_stats.so python tools/scan_stats.py [config] [max_depth]"""
 import ctypes as C
