@@ -99,6 +99,10 @@ def parse():
                    help="at N = 1 under torchrun: assemble every pass through the process group's gather "
                         "and the un-permute kernel anyway (a one-rank RCCL communicator; tests the N > 1 "
                         "exchange on one GPU)")
+    p.add_argument("--emulate-rank", type=int, default=None,
+                   help="one process on one GPU standing in for rank R of a --gpus N run: the same pass "
+                        "plan and slots, no process group and no gather (tools/scale_projection.py projects "
+                        "the N-GPU step from every rank's time); no checks, no extras")
     p.add_argument("--output", choices=("f32", "rgb8"), default="f32",
                    help="f32 frames (the parity contract), or Color::as_u8 bytes only: fused into the "
                         "render and gathered at 3 B per pixel (N > 1)")
@@ -527,7 +531,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    use_pg = world > 1 or bool(args.force_gather)
+    emulate = args.emulate_rank is not None
+    if emulate:  # rank R of an N-GPU run, alone on this GPU: no process group, no exchange
+        assert world == 1 and 0 <= args.emulate_rank < args.gpus
+        world, rank = args.gpus, args.emulate_rank
+        args.check = args.seam_stats = args.cpu_baseline = args.count_frame = 0
+    use_pg = (world > 1 and not emulate) or bool(args.force_gather)
     if use_pg:
         # one process per GPU; ranks share a device only in a --backend gloo rehearsal
         torch.cuda.set_device(local_rank % torch.cuda.device_count())
@@ -610,7 +619,8 @@ def main():
         args.batch = max(1, b)
     pipe = FramePipeline(scene, desc, args.width, args.height, args.depth, args.band_rows, rank, world, dev,
                          spp=args.spp, seed=args.seed, inflight=inflight, batch=args.batch,
-                         rgb8=args.output == "rgb8", force_gather=bool(args.force_gather), sub_bands=sub)
+                         rgb8=args.output == "rgb8", force_gather=bool(args.force_gather), sub_bands=sub,
+                         emulate=emulate)
     batch = pipe.batch
     tilers = pipe.tilers
     tiler = tilers[0]
@@ -739,6 +749,17 @@ def main():
     elapsed, kernel_ms_max = stats.tolist()
     node_rays, shadow_rays, pixels = cnt.tolist()
 
+    if emulate:
+        # one rank's share of the timed region (tools/scale_projection.py takes the max over ranks)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps({"emulated": {"world": world, "rank": rank}, "steps": args.steps,
+                                       "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                                       "kernel_ms_per_step": round(kernel_ms, 4), "frames_per_pass": batch,
+                                       "passes_in_flight": inflight, "sub_bands": sub,
+                                       "pass_latency_ms": round(latency_ms, 4),
+                                       "rows_per_rank": band_rows_per_rank(args.height, args.band_rows, world),
+                                       "node_rays_per_step": node_rays / args.steps}) + "\n").encode())
+        return
     if rank == 0:
         steps = args.steps
         mpix = args.width * args.height * steps / elapsed / 1e6

@@ -39,7 +39,7 @@ class FrameTiler:
 
     def __init__(self, scene: DeviceScene, width, height, depth, band_rows=8, rank=0, world=1,
                  device=None, spp=1, seed=0, batch=1, rgb8=False, force_gather=False, split=False,
-                 frames_out=None, band_out=None):
+                 frames_out=None, band_out=None, no_gather=False):
         """rgb8: render and gather only Color::as_u8 bytes (3 B per pixel instead of 12; the
         level-0 combine writes them, rt_render_bands_ex_async with no float buffer).
         force_gather: at world 1 too, assemble through the process group's gather and the
@@ -52,7 +52,9 @@ class FrameTiler:
         other shares fill the rest of the same frames, and nothing is gathered.
         band_out: a [batch, rows_per_rank, W, 3] tensor (a slice of a caller's buffer) that
         receives this rank's band buffers; the caller assembles them (FramePipeline's gathered
-        band-share groups), this tiler never gathers."""
+        band-share groups), this tiler never gathers.
+        no_gather: render this rank's bands of a world > 1 frame without any exchange (one
+        GPU standing in for one rank of an N-GPU run: tools/scale_projection.py)."""
         self.scene = scene
         self.rgb8 = bool(rgb8) and spp == 1
         self.spp, self.seed = spp, seed
@@ -62,7 +64,7 @@ class FrameTiler:
         if self.direct and (spp != 1 or force_gather or split):
             raise ValueError("frames_out: spp 1, no gather, no split")
         self.external = band_out is not None
-        self.gather = not self.direct and not self.external and (world > 1 or bool(force_gather))
+        self.gather = not no_gather and not self.direct and not self.external and (world > 1 or bool(force_gather))
         self.split = bool(split) and not self.gather and spp == 1 and not self.rgb8 and int(batch) == 1
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.rpr = band_rows_per_rank(height, band_rows, world)
@@ -174,11 +176,14 @@ class FramePipeline:
     share j is band rank r*S + j of a world of W*S: its band buffer is slice j of the group's
     [S, B, rows, W, 3] buffer, which is the rank's contribution to ONE gather per group pass
     (rank-major, so the gathered buffer is virtual-rank-major) and rank 0 un-permutes it with
-    W*S ranks."""
+    W*S ranks.
+
+    emulate: rank `rank` of a `world`-rank run on this one GPU with no process group: the same
+    slots, groups and passes, every exchange skipped (tools/scale_projection.py)."""
 
     def __init__(self, scene: DeviceScene, desc, width, height, depth, band_rows=8, rank=0, world=1,
                  device=None, spp=1, seed=0, inflight=4, batch=1, rgb8=False, grid_share=None,
-                 force_gather=False, sub_bands=1):
+                 force_gather=False, sub_bands=1, emulate=False):
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.inflight = max(1, int(inflight))
         self.world = world
@@ -190,13 +195,14 @@ class FramePipeline:
         self.rank = rank
         self.band_rows = band_rows
         self.w, self.h = width, height
-        self.group_gather = S > 1 and (world > 1 or bool(force_gather))
+        band_groups = S > 1 and (world > 1 or bool(force_gather))
+        self.group_gather = band_groups and not emulate
         scenes = [scene if i == 0 else scene.clone(self.device.index) for i in range(self.inflight)]
         if S == 1:
             self.tilers = [FrameTiler(scenes[i], width, height, depth, band_rows, rank, world, self.device, spp=spp,
-                                      seed=seed, batch=batch, rgb8=rgb8, force_gather=force_gather)
+                                      seed=seed, batch=batch, rgb8=rgb8, force_gather=force_gather, no_gather=emulate)
                            for i in range(self.inflight)]
-        elif not self.group_gather:
+        elif not band_groups:
             nb = max(1, min(int(batch), int(abi.lib().rt_max_frames())))
             dt = torch.uint8 if rgb8 else torch.float32
             self.group_frames = [torch.zeros((nb, height, width, 3), dtype=dt, device=self.device)
@@ -215,7 +221,7 @@ class FramePipeline:
                                       self.device, batch=nb, rgb8=rgb8, band_out=self.group_local[i // S][i % S])
                            for i in range(self.inflight)]
             self.group_gathered = self.group_frames = None
-            if rank == 0:
+            if rank == 0 and self.group_gather:
                 self.group_gathered = [torch.zeros((world, S, nb, rpr, width, 3), dtype=dt, device=self.device)
                                        for _ in range(self.groups)]
                 self.group_frames = [torch.zeros((nb, height, width, 3), dtype=dt, device=self.device)
