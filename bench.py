@@ -73,15 +73,16 @@ def parse():
                         "passes of up to 32 frames (rt_max_frames()) (a divisor of q where one is close) within 16 x 1080p of pixels "
                         "per pass and rank; 1 for spp > 1, whose samples are batched inside each pass)")
     p.add_argument("--sub-bands", type=int, default=None,
-                   help="N = 1: slots as groups of S band shares of one device, each rendering its rows of "
-                        "every frame of its group's passes in place (rt_render_bands_direct_async): S times "
-                        "the frames per pass at the same rays in flight.  Default (N <= 2, spp 1): the largest S "
-                        "of 4, 2 that divides the slots and whose groups still take the timed frames in one pass "
-                        "each (ceil(K / (F / S)) <= rt_max_frames()): K = 20 gives 1 group x 4 shares x 20 "
-                        "frames, K = 64 2 groups x 2 shares x 32 frames; otherwise 1")
+                   help="slots as groups of S band shares of the rank's rows, each rendering its rows of "
+                        "every frame of its group's passes (N = 1: in place, rt_render_bands_direct_async; "
+                        "N > 1: one gather per group pass): S times the frames per pass at the same rays in "
+                        "flight.  Default (spp 1): the first S of (4, 2) -- (2, 4) at N = 4 -- that divides "
+                        "the slots and whose groups still take the timed frames in one pass each "
+                        "(ceil(K / (F / S)) <= rt_max_frames()): K = 20 gives 1 group x 4 shares x 20 frames "
+                        "(N = 4: 2 groups x 2 shares x 10), K = 64 2 groups x 2 shares x 32 frames; otherwise 1")
     p.add_argument("--inflight", type=int, default=None,
                    help="frames in flight (F scene handles / HIP streams; default 4 = the box's hardware "
-                        "queues per process, 3 from 4 ranks up); 1 = one at a time")
+                        "queues per process; 3 from 4 ranks up when no band-share plan applies); 1 = one at a time")
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU oracle timing")
     p.add_argument("--cpu-threads", type=int, default=None,
                    help="threads of the multi-core CPU baseline (default: every core in the affinity mask)")
@@ -560,31 +561,29 @@ def main():
     t_sc = time.perf_counter()
     scene = DeviceScene(desc, device=dev.index)   # host build (hierarchy, light buffers) + upload
     scene_create_ms = (time.perf_counter() - t_sc) * 1e3
-    # 4 passes in flight.  A short burst at N >= 4 (fewer than 8 frames per slot) takes 3, so
-    # that each pass is bigger: a rank's share of a frame is small there and bigger passes
-    # amortise each level's fixed latency (one rank's share on one MI355X, K = 20,
-    # round-3 A/B run r3_share2, profiles/r3ab/: N = 8: 3 x 7 0.310 vs 4 x 5 0.326 ms per share-frame, N = 4: 0.543 vs
-    # 0.554).  With 16 frames per slot 4 x 16 wins at every N (K = 64, round-3 A/B run r3_share5, profiles/r3ab/:
-    # N = 8: 0.251 vs 0.270 for 3 x 11, N = 4: 0.487 vs 0.508)
-    inflight = max(1, args.inflight or (3 if world >= 4 and -(-args.steps // 4) < 8 else 4))
+    # 4 passes in flight, as band-share groups where a group still takes its frames in one pass
+    # per slot.  Round 4 (config 3, tools/subband_time.py, profiles/r4m/subband.txt): at K = 20,
+    # 4 x 5 whole frames 1.977 ms per frame, 2 groups x 2 shares x 10 frames 1.929, 1 group x 4
+    # shares x 20 frames 1.886; with the light-buffer tiers (profiles/r4k64/): K = 64: 1 / 2 / 4
+    # shares 1237 - 1253 / 1264 - 1269 / 1259 - 1263 Mpixels/s.  At N > 1 one rank's share played
+    # alone on one MI355X (tools/emulate_ab.py, round 6, K = 20, profiles/r6ab/r6k_plans.log, ms
+    # per frame of the slowest rank): N = 8: 4 shares x 20 frames 0.272, 2 x 2 x 10 0.278, 3 x 7
+    # whole shares 0.281 (round 5's default), 4 x 5 0.292; N = 4: 2 x 2 x 10 0.457, 3 x 7 0.465,
+    # 4 x 5 0.472, 4 shares 0.478.  A short burst that no group plan holds in one pass per slot
+    # takes 3 whole-share passes from N = 4 up (bigger passes amortise each level's fixed
+    # latency; round 3, profiles/r3ab/r3_share2.txt)
+    inflight = max(1, args.inflight or 4)
     if args.sub_bands is None:
-        # Round 4 (config 3, tools/subband_time.py, profiles/r4m/subband.txt): at K = 20, 4 x 5
-        # whole frames 1.977 ms per frame, 2 groups x 2 shares x 10 frames 1.929, 1 group x 4
-        # shares x 20 frames 1.886.  With the light-buffer tiers and 50% trace grids
-        # (profiles/r4k64/): K = 64: 1 / 2 / 4 shares 1237 - 1253 / 1264 - 1269 / 1259 - 1263
-        # Mpixels/s; K = 40: 1220 - 1225 / 1245 / 1233 - 1236 -- the most shares whose group
-        # still takes its frames in one pass per slot.  At N = 2 too (rank 0's share on one
-        # MI355X, K = 20, profiles/r4l/subband.txt: 4 x 5 1.026, 3 x 7 1.019, 2 x 2 x 10 1.008,
-        # 1 x 4 x 20 0.997 ms per share-frame); from N = 4 the 3 x 7 whole-share passes stay
-        # ahead (N = 4: 0.547 vs 0.556 / 0.567; N = 8: 0.309 vs 0.330 / 0.370)
         sub = 1
-        if world <= 2 and args.spp == 1:
+        if args.spp == 1:
             from rust_tracer_amd import abi as _abi0
             mf = int(_abi0.lib().rt_max_frames())
-            for cand in (4, 2):
+            for cand in ((2, 4) if world == 4 else (4, 2)):
                 if inflight % cand == 0 and -(-args.steps // (inflight // cand)) <= mf:
                     sub = cand
                     break
+        if sub == 1 and args.inflight is None and world >= 4 and -(-args.steps // 4) < 8:
+            inflight = 3
     else:
         sub = max(1, args.sub_bands)
     groups = max(1, inflight // sub)

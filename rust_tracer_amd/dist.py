@@ -227,7 +227,7 @@ class FramePipeline:
                 self.group_frames = [torch.zeros((nb, height, width, 3), dtype=dt, device=self.device)
                                      for _ in range(self.groups)]
             for i, t in enumerate(self.tilers):
-                t.frames = self.group_frames[i // S] if rank == 0 else None
+                t.frames = self.group_frames[i // S] if (rank == 0 and self.group_gather) else None
                 t.frame = t.frames[0] if t.frames is not None else None
         self.rgb8 = bool(rgb8)
         self.gather = self.tilers[0].gather
