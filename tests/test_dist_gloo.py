@@ -99,7 +99,7 @@ def _worker_sub(rank, world, sub, port, h, w, band, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,sub,h", [(2, 2, 1080), (2, 4, 117), (3, 2, 90)])
+@pytest.mark.parametrize("world,sub,h", [(2, 2, 1080), (2, 4, 117), (3, 2, 90), (4, 2, 1080), (8, 4, 1080)])
 def test_gather_band_share_groups(world, sub, h):
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
