@@ -689,7 +689,25 @@ __device__ __forceinline__ void bvh_walk(const DevScene& S, V3 o, V3 d, float& b
 
 // cube-map cell of a direction (face = largest |component|, ties x > y > z); the host
 // builds light buffers and grazing masks over the same cells (rt_build.cpp lb_face_dir)
+// A wave-uniform scene constant read where it is used: the compiler may not hoist what is
+// derived from it out of the loops.  Hoisted, such values (0.5 res, res - 1, 16 / r ...) were
+// computed once into VGPRs, spilled to scratch, and every reload inside the trace iteration
+// waited (vmcnt counts stores on gfx9) for the iteration's outstanding stores.
+__device__ __forceinline__ uint32_t opaque_u(uint32_t x) {
+    __asm__ volatile("" : "+s"(x));
+    return x;
+}
+__device__ __forceinline__ float opaque_f(float x) {
+    __asm__ volatile("" : "+s"(x));
+    return x;
+}
+// ... and a per-lane value (loop-invariant values derived from it are recomputed per use)
+__device__ __forceinline__ V3 opaque_v3(V3 v) {
+    __asm__ volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z));
+    return v;
+}
 __device__ __forceinline__ uint32_t lb_cell(uint32_t res, V3 v) {
+    res = opaque_u(res);
     const float ax = fabsf(v.x), ay = fabsf(v.y), az = fabsf(v.z);
     uint32_t f;
     float a, b, m;

@@ -41,14 +41,19 @@ struct PixelRef {
     uint32_t u, v, lr;
 };
 
-// level-0 item -> pixel of this rank's band buffer (8x8 tiles, block-cyclic row bands)
+// level-0 item -> pixel of this rank's band buffer (8x8 tiles, block-cyclic row bands).  A
+// wave's active items lie in one 64-item tile (waves take 64- or 32-aligned chunks), so the
+// tile index is wave-uniform and its division by tiles_x runs on the scalar unit; the band
+// divisor is read where it is used (opaque_u: its hoisted reciprocal would be spilled)
 __device__ __forceinline__ PixelRef pixel_of(const WaveParams& P, uint32_t item) {
     PixelRef r;
-    uint32_t tile = item >> 6, w = item & 63u;
-    r.u = (tile % P.tiles_x) * 8u + (w & 7u);
-    r.lr = (tile / P.tiles_x) * 8u + (w >> 3);
-    uint32_t band = r.lr / P.band_rows;
-    r.v = (band * P.world + P.rank) * P.band_rows + (r.lr - band * P.band_rows);
+    const uint32_t tile = (uint32_t)__builtin_amdgcn_readfirstlane((int)(item >> 6)), w = item & 63u;
+    const uint32_t tx = opaque_u(P.tiles_x), ty = tile / tx;
+    r.u = (tile - ty * tx) * 8u + (w & 7u);
+    r.lr = ty * 8u + (w >> 3);
+    const uint32_t br = opaque_u(P.band_rows);
+    uint32_t band = r.lr / br;
+    r.v = (band * P.world + P.rank) * br + (r.lr - band * br);
     r.valid = r.u < P.width && r.lr < P.rows_local && r.v < P.height;
     return r;
 }
@@ -61,13 +66,15 @@ __device__ __forceinline__ uint32_t item_frame(const WaveParams& P, uint32_t t, 
         local = t;
         return 0u;
     }
-    if (P.l0_interleave) {
-        const uint32_t tile = t >> 6, fr = tile % P.frames;
-        local = ((tile / P.frames) << 6) | (t & 63u);
+    if (P.l0_interleave) {  // (the tile is wave-uniform: pixel_of)
+        const uint32_t tile = (uint32_t)__builtin_amdgcn_readfirstlane((int)(t >> 6)), nf = opaque_u(P.frames);
+        const uint32_t q = tile / nf, fr = tile - q * nf;
+        local = (q << 6) | (t & 63u);
         return fr;
     }
-    const uint32_t fr = t / P.frame_items;
-    local = t - fr * P.frame_items;
+    const uint32_t fi = opaque_u(P.frame_items);
+    const uint32_t fr = t / fi;
+    local = t - fr * fi;
     return fr;
 }
 
@@ -100,7 +107,7 @@ __device__ __forceinline__ uint32_t spread5(uint32_t v) {  // abcde -> a..b..c..
 __device__ __forceinline__ float key_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float key_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ uint32_t morton15(const DevScene& S, V3 p) {
-    float sc = 16.f * key_rcp(S.bvh_r);
+    float sc = 16.f * key_rcp(opaque_f(S.bvh_r));
     int x = (int)fminf(fmaxf((p.x - S.bvh_cx) * sc + 16.f, 0.f), 31.f);
     int y = (int)fminf(fmaxf((p.y - S.bvh_cy) * sc + 16.f, 0.f), 31.f);
     int z = (int)fminf(fmaxf((p.z - S.bvh_cz) * sc + 16.f, 0.f), 31.f);
@@ -117,7 +124,7 @@ __device__ __forceinline__ uint32_t spread6(uint32_t v) {  // abcdef -> a..b..c.
 }
 // 18-bit Morton code over the 64^3 grid of the same cube
 __device__ __forceinline__ uint32_t morton18(const DevScene& S, V3 p) {
-    float sc = 32.f * key_rcp(S.bvh_r);
+    float sc = 32.f * key_rcp(opaque_f(S.bvh_r));
     int x = (int)fminf(fmaxf((p.x - S.bvh_cx) * sc + 32.f, 0.f), 63.f);
     int y = (int)fminf(fmaxf((p.y - S.bvh_cy) * sc + 32.f, 0.f), 63.f);
     int z = (int)fminf(fmaxf((p.z - S.bvh_cz) * sc + 32.f, 0.f), 63.f);
@@ -133,7 +140,7 @@ __device__ __forceinline__ uint32_t spread7(uint32_t v) {  // 7 bits -> every th
 }
 // 21-bit Morton code over the 128^3 grid of the same cube
 __device__ __forceinline__ uint32_t morton21(const DevScene& S, V3 p) {
-    float sc = 64.f * key_rcp(S.bvh_r);
+    float sc = 64.f * key_rcp(opaque_f(S.bvh_r));
     int x = (int)fminf(fmaxf((p.x - S.bvh_cx) * sc + 64.f, 0.f), 127.f);
     int y = (int)fminf(fmaxf((p.y - S.bvh_cy) * sc + 64.f, 0.f), 127.f);
     int z = (int)fminf(fmaxf((p.z - S.bvh_cz) * sc + 64.f, 0.f), 127.f);
@@ -182,7 +189,7 @@ __device__ __forceinline__ uint32_t task_key(const WaveParams& P, V3 o, V3 d) {
     else if (ay >= az) { face = 2u + (d.y < 0.f); u = d.x; v = d.z; m = ay; }
     else { face = 4u + (d.z < 0.f); u = d.x; v = d.y; m = az; }
     if (P.key_mode >= 5 && P.key_mode <= 7) {  // Morton of a point ahead on the ray
-        const float ahead = P.key_ahead * P.S.bvh_r;
+        const float ahead = opaque_f(P.key_ahead) * P.S.bvh_r;
         const V3 q = add(o, mul(d, ahead));
         uint32_t cu = u > 0.f ? 1u : 0u, cv = v > 0.f ? 1u : 0u;
         uint32_t dir = (face << 2) | (cu << 1) | cv;
@@ -686,9 +693,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TRACE_WAVES
                 for (int li = 0; li < lights32; ++li) {
                     const LightRec L = light_at(S, li);
                     if (L.kind != RT_LIGHT_POINT || ((decided >> li) & 1u)) continue;
+                    // the origin re-read per light: what the scan derives from it alone (o +- h,
+                    // |o|) is recomputed instead of hoisted out of this loop and spilled
+                    const V3 ps = opaque_v3(sh_ps);
                     const V3 lpos = v3(L.px, L.py, L.pz);
-                    const V3 ldir = norm(sub(lpos, sh_ps));  // mod.rs:191
-                    if (!shadow_scan<LDS>(S, sh_ps, ldir, lpos, cnt, lnodes, L.lb_base)) lit_pre |= 1u << li;
+                    const V3 ldir = norm(sub(lpos, ps));  // mod.rs:191
+                    if (!shadow_scan<LDS>(S, ps, ldir, lpos, cnt, lnodes, L.lb_base)) lit_pre |= 1u << li;
                     decided |= 1u << li;
                     n_pre++;
                 }

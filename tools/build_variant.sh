@@ -16,11 +16,11 @@ CF="-O3 -std=c++17 -fPIC -ffp-contract=off -Wall $FLAGS"
 WFFLAGS=${WFFLAGS--mllvm -amdgpu-atomic-optimizer-strategy=None}  # as the Makefile (WFFLAGS= : the compiler's default)
 /opt/rocm/bin/hipcc $HF $WFFLAGS -c -o $B/rt_wavefront.o $C/rt_wavefront.hip &
 for f in rt_frame rt_order; do /opt/rocm/bin/hipcc $HF -c -o $B/$f.o $C/$f.hip & done
-for f in rt_api rt_multi; do /opt/rocm/bin/hipcc $HF -c -o $B/$f.o $C/$f.cpp & done
+for f in rt_build rt_scene rt_render rt_forest rt_multi; do /opt/rocm/bin/hipcc $HF -c -o $B/$f.o $C/$f.cpp & done
 /opt/rocm/bin/hipcc $CF -x c++ -c -o $B/rt_bvh.o $C/rt_bvh.cpp &
 /opt/rocm/bin/hipcc $CF -x c++ -c -o $B/rt_tune.o $C/rt_tune.cpp &
 /opt/rocm/bin/hipcc $CF -x c++ -c -o $B/image_io.o $C/host/image_io.cpp &
 /opt/rocm/bin/hipcc $CF -x c++ -c -o $B/scene.o $C/host/scene.cpp &
-wait
+for j in $(jobs -p); do wait $j || { echo "compile failed" >&2; exit 1; }; done
 /opt/rocm/bin/hipcc $HF -shared -o $R/rust_tracer_amd/librt_hip_$NAME.so $B/*.o -ldl
 echo built rust_tracer_amd/librt_hip_$NAME.so
