@@ -22,9 +22,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace1 -o run -- \
     python bench.py --steps 6 --warmup 1 --inflight 1 --batch 1 $B --count-frame 0 > $OUT/trace1.log 2>&1 || exit 4
 echo traces
+SIZES=${SIZES:-1 5 16 20/4 32/2}  # (commas or spaces)
 # a size N/S: passes of N frames over S band shares of the device (bench.py --sub-bands S; the
 # driver's K = 20 runs 20/4), one group of S slots
-for spec in ${SIZES:-1 5 16 20/4 32/2}; do
+for spec in ${SIZES//,/ }; do
   n=${spec%/*}; s=1; [ "$spec" != "$n" ] && s=${spec#*/}
   args="--steps $n --warmup 0 --inflight $s --sub-bands $s --batch $n $B --count-frame 0"
   [ "$s" = 1 ] && suf=$n || suf=${n}s$s
