@@ -76,8 +76,8 @@ def parse():
                    help="slots as groups of S band shares of the rank's rows, each rendering its rows of "
                         "every frame of its group's passes (N = 1: in place, rt_render_bands_direct_async; "
                         "N > 1: one gather per group pass): S times the frames per pass at the same rays in "
-                        "flight.  Default (spp 1): the first S of (4, 2) -- (2, 4) at N = 4 -- that divides "
-                        "the slots and whose groups still take the timed frames in one pass each "
+                        "flight.  Default (spp 1, N <= 4): the first S of (4, 2) -- (2, 4) at N = 4 -- that "
+                        "divides the slots and whose groups still take the timed frames in one pass each "
                         "(ceil(K / (F / S)) <= rt_max_frames()): K = 20 gives 1 group x 4 shares x 20 frames "
                         "(N = 4: 2 groups x 2 shares x 10), K = 64 2 groups x 2 shares x 32 frames; otherwise 1")
     p.add_argument("--inflight", type=int, default=None,
@@ -565,17 +565,20 @@ def main():
     # per slot.  Round 4 (config 3, tools/subband_time.py, profiles/r4m/subband.txt): at K = 20,
     # 4 x 5 whole frames 1.977 ms per frame, 2 groups x 2 shares x 10 frames 1.929, 1 group x 4
     # shares x 20 frames 1.886; with the light-buffer tiers (profiles/r4k64/): K = 64: 1 / 2 / 4
-    # shares 1237 - 1253 / 1264 - 1269 / 1259 - 1263 Mpixels/s.  At N > 1 one rank's share played
-    # alone on one MI355X (tools/emulate_ab.py, round 6, K = 20, profiles/r6ab/r6k_plans.log, ms
-    # per frame of the slowest rank): N = 8: 4 shares x 20 frames 0.272, 2 x 2 x 10 0.278, 3 x 7
-    # whole shares 0.281 (round 5's default), 4 x 5 0.292; N = 4: 2 x 2 x 10 0.457, 3 x 7 0.465,
-    # 4 x 5 0.472, 4 shares 0.478.  A short burst that no group plan holds in one pass per slot
-    # takes 3 whole-share passes from N = 4 up (bigger passes amortise each level's fixed
-    # latency; round 3, profiles/r3ab/r3_share2.txt)
+    # shares 1237 - 1253 / 1264 - 1269 / 1259 - 1263 Mpixels/s.  At N > 1 every rank played
+    # alone on one MI355X (tools/emulate_ab.py / tools/scale_projection.py, round 6, K = 20,
+    # profiles/r6ab/r6k_plans.log, profiles/r6share/): N = 4: 2 groups x 2 shares x 10 frames,
+    # slowest rank 0.453 ms per frame, against 0.470 for 3 x 7 whole shares (the same 34 bands
+    # on rank 0).  N = 8: 3 x 7 whole shares -- a rank's share then holds 16 - 17 of the 135
+    # 8-row bands; as 4 band shares (32 virtual ranks, rank-major) the 7 leftover bands all land
+    # on ranks 0 - 1 (20 / 19 bands against 16): 0.334 ms on rank 0 against 0.280, and per band
+    # the shares are no faster (0.0170 vs 0.0165 ms).  A short burst that no group plan holds in
+    # one pass per slot takes 3 whole-share passes from N = 4 up (bigger passes amortise each
+    # level's fixed latency; round 3, profiles/r3ab/r3_share2.txt)
     inflight = max(1, args.inflight or 4)
     if args.sub_bands is None:
         sub = 1
-        if args.spp == 1:
+        if args.spp == 1 and world <= 4:
             from rust_tracer_amd import abi as _abi0
             mf = int(_abi0.lib().rt_max_frames())
             for cand in ((2, 4) if world == 4 else (4, 2)):
