@@ -87,6 +87,8 @@ struct DevScene {
     // per ray, D = |o - c| + r: box inflation h(D) = (g2 D + g1) D + g0 and t-margin
     // m(D) = m1 D + m0 (distance units), see rt_scan.hpp
     float bvh_cx, bvh_cy, bvh_cz, bvh_r, bvh_g2, bvh_g1, bvh_g0, bvh_m1, bvh_m0;
+    float walk_lin_h;          // shadow walks: a wave whose nearest walking origin has h(D) >= this
+                               // tests every hierarchy primitive in order (rt_scan.hpp hier_linear)
     float graze_s2;            // 1.0201: (d.n')^2 < graze_s2 |d|^2 with n' = n / sin(phi_T): the ray grazes
     const float4* graze_pn;    // per graze pair: {nAx nBx nAy nBy} {nAz nBz - -} (n / sin(phi_T))
     const uint32_t* graze_mask;  // per direction cell: graze_words words of pair bits
@@ -236,6 +238,10 @@ struct WaveParams {
     uint32_t shadow_fine;              // 18 / 19 / 21: bits below the light index (3 sort passes); 0: 16-bit key
     uint32_t shadow_cell;              // light | light-buffer cell (1), x 3-bit (2) / 4-bit (3, shadow_fine 19)
                                        // distance from the light; rays that walk: light | flag | Morton
+    // cell keys: key = light << shadow_li_shift | low, low = shadow_walk_flag | Morton for rays that
+    // walk, shadow_lb_flag | cell... for the others (Tune::walk_first: the flag above the light
+    // bits on the buffered rays -- walking rays first; else on the walking rays, below the light)
+    uint32_t shadow_li_shift, shadow_walk_flag, shadow_lb_flag;
     uint32_t light_shift;              // shadow key = (light << light_shift) | (Morton >> (15 - light_shift))
     uint32_t count_mask;               // bit 0: trace kernels add to scan_ops, bit 1: shadow kernel
     // ray forest (render_tree.rs; set only when building an rt_forest): per node

@@ -185,6 +185,9 @@ rt_status rthost::wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam,
     p.sample = sample;
     p.seed = seed;
     p.S = s->S;
+    // shadow waves whose walk cannot cull (its box growth h(D) at least walk_linear scene radii:
+    // origins on the far floor) scan the hierarchy's primitives linearly (exact either way)
+    p.S.walk_lin_h = tn.walk_linear > 0.0 ? (float)tn.walk_linear * s->S.bvh_r : __builtin_huge_valf();
     p.width = cam->x_res;
     p.height = cam->y_res;
     p.depth = depth;
@@ -354,6 +357,19 @@ rt_status rthost::wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam,
         shadow_bits += fbits;
         if (shadow_bits > 32u) return RT_ERR_UNSUPPORTED;
     }
+    // Cell keys put the shadow rays that walk the hierarchy (origins beyond every light-buffer
+    // tier: the far floor) first instead of after each light's cells: such a task takes ~20x
+    // a buffered one (300 - 430 us against ~12, tools/shadow_tail.py), and at the end of the
+    // queue it started last and set the shadow kernel's end.  Same key bits, ordering only.
+    // World-8 share 0.469 -> 0.337 ms of shadow kernel, the seam's one frame 3.35 - 3.40 ->
+    // 3.16 - 3.20 ms (profiles/r6ab/r6z_shadow_tail.log).  Measured without gain: the buffered
+    // rays after them in tier order, farthest first (2 more key bits: world 1 better, world 8
+    // 0.48 ms -- the far tiers' records crowd the walkers' out of the caches); consecutive
+    // tasks on the waves of consecutive blocks (other CUs) instead of one block's 4 waves: flat.
+    const bool walk_first = tn.walk_first && p.shadow_cell && p.shadow_fine;
+    p.shadow_li_shift = walk_first ? p.shadow_fine - 1u : p.shadow_fine;
+    p.shadow_walk_flag = walk_first ? 0u : (p.shadow_fine ? 1u << (p.shadow_fine - 1u) : 0u);
+    p.shadow_lb_flag = walk_first ? 1u << (p.shadow_fine - 1u + lbits) : 0u;
     if (sort_tasks && w.sort_capacity < w.capacity) {
         for (uint32_t** b : {&w.task_keys, &w.perm}) {
             if (*b) (void)hipFree(*b);

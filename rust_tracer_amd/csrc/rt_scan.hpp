@@ -31,6 +31,13 @@ __device__ unsigned long long rt_scan_stats[40];
 #else
 #define RT_STAT(i) do { } while (0)
 #endif
+#ifndef RT_SHADOW_CLOCK
+#define RT_SHADOW_CLOCK 0
+#endif
+#if RT_SHADOW_CLOCK
+#define RT_SHADOW_CLOCK_WORDS (2u + 4u * (1u << 20))
+__device__ uint32_t rt_shadow_clock[RT_SHADOW_CLOCK_WORDS];
+#endif
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1087,6 +1094,35 @@ __device__ __forceinline__ void lb_pass(const DevScene& S, uint32_t base, uint32
     }
 }
 
+// Every hierarchy primitive for every lane, in leaf order: the shadow walk of a wave none of
+// whose boxes can be culled (far origins: the box growth h(D) spans the scene ball), without
+// the walk's node tests, stack and per-leaf dependent loads -- the records stream through the
+// prefetching run loops.  Exact: a superset of what the walk tests (the nearest (t, key) does
+// not depend on order or on extra records; a decided lane stays decided; a buffered lane's
+// hierarchy primitives are settled, so extra records change nothing for it).  The grazing pass
+// after it tests nothing new.  Stops when every lane is decided.  (Raising the wave's issue
+// priority meanwhile -- such a task is the shadow pass's critical path -- measured flat.)
+template <bool LDS, class C>
+__device__ __forceinline__ void hier_linear(const DevScene& S, V3 o, V3 d, float& bt, uint32_t& bk, float tlim,
+                                            float l2, C& c, lfloat4* lnodes) {
+    constexpr int CH = 32;
+    for (int b = 0; b < S.n_dsph_bvh; b += CH) {
+        const int e = min(b + CH, S.n_dsph_bvh);
+        if (LDS) run_dsph_lds(b, e, o, d, bt, bk, c, lds_dsph(S, lnodes));
+        else run_dsph(S, b, e, o, d, bt, bk, c);
+        if (__ballot(!shadow_decided(o, d, bt, l2)) == 0) return;
+    }
+    run_gsph(S, 0, S.n_gsph_bvh, o, d, bt, bk, c);
+    run_tri(S, 0, S.n_tri_bvh, o, d, bt, bk, c);
+    if (__ballot(!shadow_decided(o, d, bt, l2)) == 0) return;
+    const float on = sqrtf(len2(o));
+    cfloat4* p = cptr(S.cube);
+    for (int i = 0; i < S.n_cube_bvh; ++i, p += 4) {
+        const bool dec = shadow_decided(o, d, bt, l2);
+        cube_culled(ld_rec(p), o, d, on, dec ? -1.f : fminf(bt, tlim), bt, bk, c);
+    }
+}
+
 // ------------------------------------------------------------------ shadow scan
 // PointLight::get_energy (scene/mod.rs:189-206): a FULL nearest-hit scan, then
 // "shadowed iff |hit.point - p|^2 < |pos - p|^2".  Exact early exit:
@@ -1155,12 +1191,23 @@ __device__ __forceinline__ bool shadow_scan(const DevScene& S, V3 o, V3 d, V3 lp
             }
         }
 #endif
-        if (__ballot(!lb && !shadow_decided(o, d, bt, l2)))
-            bvh_walk<true, LDS>(S, o, d, bt, bk, tlim, l2, c, lnodes, lb);
+        bool linear = false;
+        {
+            const bool walker = !lb && !shadow_decided(o, d, bt, l2);
+            if (__ballot(walker)) {
+                // the nearest walking origin's box growth (D = |o - c| + R as bvh_ray)
+                const float dx = o.x - S.bvh_cx, dy = o.y - S.bvh_cy, dz = o.z - S.bvh_cz;
+                const float D = sqrtf(dx * dx + dy * dy + dz * dz) + S.bvh_r;
+                const float dmin = -wave_max(walker ? -D : -__builtin_huge_valf());
+                linear = fmaf(fmaf(S.bvh_g2, dmin, S.bvh_g1), dmin, S.bvh_g0) >= S.walk_lin_h;
+                if (linear) hier_linear<LDS>(S, o, d, bt, bk, tlim, l2, c, lnodes);
+                else bvh_walk<true, LDS>(S, o, d, bt, bk, tlim, l2, c, lnodes, lb);
+            }
+        }
         if (SPLIT) RT_T1(C, c, cyc_self, t_w);
         done = shadow_decided(o, d, bt, l2);
         if (__ballot(!done) == 0) goto finish;
-        graze_pass<LDS>(S, o, d, bt, bk, c, gp, lnodes, done);
+        if (!linear) graze_pass<LDS>(S, o, d, bt, bk, c, gp, lnodes, done);
         done = shadow_decided(o, d, bt, l2);
         if (__ballot(!done) == 0) goto finish;
     }

@@ -91,6 +91,8 @@ bool apply_one(Tune& t, const std::string& k, const std::string& v, bool build) 
         return t.shadow_key == 1 || t.shadow_key == 2 || t.shadow_key == 16 || t.shadow_key == 18 ||
                t.shadow_key == 21;
     }
+    if (k == "walk_linear") return parse_real(v, 0.0, 1e6, &t.walk_linear);
+    if (k == "walk_first") return set_int(v, 0, 1, t.walk_first);
     if (k == "task_fine") return set_int(v, 0, 1, t.task_fine);
     if (k == "shadow_fine") return set_int(v, 0, 1, t.shadow_fine);
     if (k == "key24") return set_int(v, 0, 1, t.key24);

@@ -47,6 +47,8 @@ struct Tune {
     int sched = 0;            // trace kernels' work distribution: 0 grid-stride, 1 dynamic, 2 block-contiguous
     double task_fill = 1.0;   // tasks per wave slot below which a level's tasks are narrowed
     int shadow_key = 2;       // shadow queue key: 2 cell2, 1 cell, 16 / 18 / 21 light | Morton bits
+    double walk_linear = 1.0; // shadow walks: linear hierarchy scan from h(D) >= this x scene radius (0: off)
+    int walk_first = 1;       // cell keys: the shadow rays that walk the hierarchy sort first (0: last)
     int task_fine = 1;        // frame batches: 21-bit task keys
     int shadow_fine = 1;      // frame batches: a 4th shadow-distance bit
     int key24 = 1;            // frame batches without frame bits: 24-bit keys

@@ -764,7 +764,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TRACE_WAVES
                                 const V3 dir = neg(raw);
                                 const bool lb = lb_tier_at(S, L.lb_base, key_d, l2) >= 0;
                                 if (!lb) {
-                                    low = (1u << (P.shadow_fine - 1u)) |
+                                    low = P.shadow_walk_flag |
                                           (P.shadow_fine >= 19u ? mort << (P.shadow_fine - 19u) : mort >> (19u - P.shadow_fine));
                                 } else if (P.shadow_cell == 2u) {  // cell | 3-bit distance from the light
                                     const float dl = key_sqrt(l2) * (8.f / RT_LB_LMAX);
@@ -778,8 +778,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TRACE_WAVES
                                 } else {
                                     low = lb_cell(S.lb_res, dir);
                                 }
+                                if (lb) low |= P.shadow_lb_flag;
                             }
-                            P.shadow_keys[slot] = (P.shadow_fine ? (((uint32_t)li << P.shadow_fine) | low)
+                            P.shadow_keys[slot] = (P.shadow_fine ? (((uint32_t)li << P.shadow_li_shift) | low)
                                                                    : ((uint32_t)li << P.light_shift) | (mort >> (15u - P.light_shift)))
                                                   | ((P.frames > 1 && P.frame_keys) ? ((pix >> RT_FRAME_SHIFT) << P.shadow_frame_shift) : 0u);
                         }
@@ -905,12 +906,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SHADOW_WAVE
         uint32_t t = base + lane;
         uint32_t e = t < count ? shadow_raw(P, t) : 0u;
         float4 q = t < count ? P.node_ps[shadow_node(P, e)] : make_float4(0.f, 0.f, 0.f, 0.f);
+#if RT_SHADOW_CLOCK
+        // tools/shadow_tail.py: wall clock (100 MHz) of every 64-entry task of the queue, and the
+        // distance of its origins from the scene ball's centre in scene radii (mean, max)
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            rt_shadow_clock[0] = count;
+            rt_shadow_clock[1] = stride / 64u;
+        }
+        uint64_t tc0 = wall_clock64();
+#endif
         while (base < count) {
             const uint32_t tn = t + stride;
             const uint32_t en = tn < count ? shadow_raw(P, tn) : 0u;
             bool lit = false;
             uint32_t n = 0, li = 0;
             if (t < count) shadow_unpack(P, e, n, li);
+#if RT_SHADOW_CLOCK
+            const float q0x = q.x, q0y = q.y, q0z = q.z;
+#endif
             if (t < count) {
                 V3 ps = v3(q.x, q.y, q.z);
                 float4 lq;
@@ -927,6 +940,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SHADOW_WAVE
             }
             q = tn < count ? P.node_ps[shadow_node(P, en)] : make_float4(0.f, 0.f, 0.f, 0.f);
             if (lit) atomicOr(lit_word(P, n, li), 1u << (li & 31u));
+#if RT_SHADOW_CLOCK
+            {
+                const uint64_t tc1 = wall_clock64();
+                const uint32_t task = base / 64u;
+                float dd = 0.f;
+                if (t < count) {
+                    const float dx = q0x - S.bvh_cx, dy = q0y - S.bvh_cy, dz = q0z - S.bvh_cz;
+                    dd = sqrtf(dx * dx + dy * dy + dz * dz) / S.bvh_r;
+                }
+                float dsum = dd, dmax = dd;
+                for (int o = 32; o > 0; o >>= 1) {
+                    dsum += __shfl_xor(dsum, o);
+                    dmax = fmaxf(dmax, __shfl_xor(dmax, o));
+                }
+                const uint32_t nl = (uint32_t)__builtin_popcountll(__ballot(t < count));
+                if (lane == 0 && 2u + 4u * task + 3u < RT_SHADOW_CLOCK_WORDS) {
+                    uint32_t* rec = rt_shadow_clock + 2u + 4u * task;
+                    rec[0] = (uint32_t)(tc1 - tc0);
+                    rec[1] = __float_as_uint(dsum / (float)max(nl, 1u));
+                    rec[2] = __float_as_uint(dmax);
+                    rec[3] = nl | (li << 8);
+                }
+                tc0 = tc1;
+            }
+#endif
             base += stride;
             t = tn;
             e = en;
@@ -1333,6 +1371,15 @@ hipError_t launch_wave_combine(const WaveParams& p, uint32_t level, int blocks, 
 
 }  // namespace rtdev
 
+#if RT_SHADOW_CLOCK
+// tools/shadow_tail.py (build: tools/build_variant.sh clock -DRT_SHADOW_CLOCK=1): the shadow kernel's task clock of the last pass (entries, waves of the
+// grid, then per 64-entry task: 10-ns ticks, mean and max origin distance / scene radius,
+// lanes | light << 8)
+extern "C" int rt_debug_shadow_clock(uint32_t* out, uint32_t words) {
+    if (words > RT_SHADOW_CLOCK_WORDS) words = RT_SHADOW_CLOCK_WORDS;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(rtdev::rt_shadow_clock), words * sizeof(uint32_t)) != hipSuccess;
+}
+#endif
 #if RT_DIAG
 // tools/scan_stats.py: read (and optionally reset) the wavefront pipeline's scan counters
 extern "C" int rt_debug_scan_stats(unsigned long long* out40, int reset) {

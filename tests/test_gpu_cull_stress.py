@@ -186,6 +186,30 @@ def test_light_buffer_tiers_change_nothing(case):
         assert same_bits(img, out[0][0]) and cnt == out[0][1]
 
 
+@pytest.mark.parametrize("case", [None] + CASES)
+def test_far_shadow_walks_change_nothing(case):
+    """Shadow waves whose walk cannot cull (the box growth h(D) of their nearest walking origin
+    spans walk_linear scene radii: the far floor) test every hierarchy primitive linearly
+    (rt_scan.hpp hier_linear), and the walking rays sort first in the shadow queue
+    (walk_first): frames and counters identical to the walk for every wave, to the old key
+    order, and to the linear scan taken from any distance (walk_linear=1e-6), with no light
+    buffers too (every shadow ray walks)."""
+    if case is None:
+        desc, w, h, depth, cam = SceneDesc.synth_config(3), 480, 270, 8, None
+    else:
+        seed, scale, cam_mode, near, slivers = case
+        desc, w, h, depth = stress_scene(seed, scale, near, slivers), 160, 120, 8
+        cam = stress_camera(w, h, scale, cam_mode)
+    out = []
+    for tune in (None, "walk_linear=0", "walk_first=0,walk_linear=0", "walk_linear=0.000001",
+                 "lb_res=0,walk_linear=0.000001"):
+        s = DeviceScene(desc, device=0, tuning=tune)
+        out.append(s.render(w, h, depth, cam=cam)[:2])
+        s.close()
+    for img, cnt in out[1:]:
+        assert same_bits(img, out[0][0]) and cnt == out[0][1]
+
+
 @pytest.mark.parametrize("key", ["18", "cell", "16"])
 def test_shadow_queue_order_changes_nothing(key, monkeypatch):
     """The shadow queue's sort key (default: light | light-buffer cell | distance) only

@@ -1,6 +1,8 @@
 """Time one rank's share of a frame (rt_render_bands_async, block-cyclic bands) on one GPU,
 for world sizes 1..8: the strong-scaling ceiling of the multi-GPU path before the gather.
-usage: python tools/band_share_time.py [config=3] [width height]"""
+usage: python tools/band_share_time.py [config=3] [width height]
+   (env WORLDS=1,2,4,8; KT=1 adds the per-kind kernel times of the timed renders,
+   rt_scene_kernel_times: trace / sorts / shadow / combine launch groups, ms per share)"""
 import os
 import sys
 
@@ -16,6 +18,9 @@ def main():
     h = int(sys.argv[3]) if len(sys.argv) > 3 else 1080
     depth = 4 if config == 2 else 8
     s = DeviceScene(SceneDesc.synth_config(config))
+    kt = os.environ.get("KT", "0") == "1"
+    if kt:
+        s.set_kernel_timing(True)
     cam = abi.camera(w, h)
     stream = torch.cuda.current_stream().cuda_stream
     base = None
@@ -33,9 +38,15 @@ def main():
             torch.cuda.synchronize()
             if it >= 2:
                 times.append(a.elapsed_time(b))
+            elif kt:
+                s.kernel_times(reset=True)
         t = sorted(times)[len(times) // 2]
         base = base or t
         print(f"{w}x{h} world {world}: rank-0 share {t:.3f} ms  -> ideal speedup {base / t:.2f} (x{world})", flush=True)
+        if kt:
+            d = s.kernel_times(reset=True)
+            n = len(times)
+            print("   kernel ms per share: " + "  ".join(f"{k} {d[k] / n:.3f}" for k in DeviceScene.KERNEL_KINDS), flush=True)
     s.close()
 
 

@@ -10,6 +10,7 @@
 #   "ab [VAR=v ...] -- SPEC ..." tools/ab_env.sh with the given environment (e.g. REPS=4 K=64)
 #   "profile PTAG"               tools/profile.sh PTAG (rocprofv3 kernel trace + PMC passes)
 #   "py SCRIPT [args]"           python SCRIPT args (the tools/*.py timers and statistics)
+#   "sh SCRIPT [args]"           bash SCRIPT args (e.g. tools/seam_ab.sh default walk_first=0)
 #   "env VAR=v ... -- STEP"      the same STEP with extra environment (e.g. RT_TUNE=..., RT_LIB=...)
 # Logs: gpurun_out/TAG/NN_<kind>.log (bench: .json + .err).  Replaces round 4's one-off
 # tools/r4*_check.sh launchers.
@@ -56,6 +57,9 @@ run_step() {
         py)
             timeout -k 10 400 python "$@" > "$O/${id}_py.log" 2>&1 || { tail -20 "$O/${id}_py.log"; return 1; }
             tail -15 "$O/${id}_py.log" ;;
+        sh)
+            timeout -k 10 900 bash "$@" > "$O/${id}_sh.log" 2>&1 || { tail -20 "$O/${id}_sh.log"; return 1; }
+            tail -15 "$O/${id}_sh.log" ;;
         env)
             local envs=()
             while [ $# -gt 0 ] && [ "$1" != "--" ]; do envs+=("$1"); shift; done
