@@ -287,7 +287,12 @@ rt_status rthost::wave_pipeline(rt_scene* s, Workspace& w, const rt_camera* cam,
     // through the sorted shadow queue (inlining levels 0-1: +20%, all: x2.4)
     p.inline_levels = (uint32_t)tn.inline_shadow;
     // narrowest trace task width (64: fixed 64-ray tasks) and the tasks per wave slot below
-    // which a level's tasks are narrowed
+    // which a level's tasks are narrowed.  A level with fewer 64-ray tasks than half the wave
+    // slots (a world-8 share's deep levels: 1.3 - 1.8 K tasks for 5120 waves) runs one task per
+    // wave and lasts as long as its slowest task (p50 25 us, max 140 us: tools/trace_tail.py);
+    // 32-ray tasks there: world-8 share 1.764 -> 1.584 ms (16: 1.594; 32 from a full level
+    // down, task_fill 1: 1.630, and the seam's half frames lose), frames in flight and the
+    // seam unchanged (profiles/r6ab/r6ah_task_width.log)
     p.task_w_min = (uint32_t)tn.task_w;
     p.task_w_fill = (float)tn.task_fill;
     // instrumented kernels (counting frames): Tune::count selects the kernels that count

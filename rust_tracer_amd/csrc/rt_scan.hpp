@@ -31,12 +31,17 @@ __device__ unsigned long long rt_scan_stats[40];
 #else
 #define RT_STAT(i) do { } while (0)
 #endif
-#ifndef RT_SHADOW_CLOCK
-#define RT_SHADOW_CLOCK 0
+#ifndef RT_TASK_CLOCK
+#define RT_TASK_CLOCK 0
 #endif
-#if RT_SHADOW_CLOCK
+#if RT_TASK_CLOCK
 #define RT_SHADOW_CLOCK_WORDS (2u + 4u * (1u << 20))
 __device__ uint32_t rt_shadow_clock[RT_SHADOW_CLOCK_WORDS];
+// trace kernels: per level (< 16) a header of 4 words (tasks' entries, grid waves, task width)
+// and 2^16 task records of 4 words
+#define RT_TRACE_CLOCK_TASKS (1u << 16)
+#define RT_TRACE_CLOCK_WORDS (16u * (4u + 4u * RT_TRACE_CLOCK_TASKS))
+__device__ uint32_t rt_trace_clock[RT_TRACE_CLOCK_WORDS];
 #endif
 
 typedef float f2 __attribute__((ext_vector_type(2)));

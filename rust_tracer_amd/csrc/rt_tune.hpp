@@ -43,9 +43,9 @@ struct Tune {
     int task_key = 7;         // task key mode (rt_wavefront.hip task_key / inside_key)
     int self_shadow = 1;      // own-shape shadow pre-test in the trace kernel
     int inline_shadow = 1;    // levels whose shadow rays the trace kernel scans inline
-    int task_w = 64;          // narrowest trace task (64 / 32 / 16 rays)
+    int task_w = 32;          // narrowest trace task (64 / 32 / 16 rays)
     int sched = 0;            // trace kernels' work distribution: 0 grid-stride, 1 dynamic, 2 block-contiguous
-    double task_fill = 1.0;   // tasks per wave slot below which a level's tasks are narrowed
+    double task_fill = 0.5;   // tasks per wave slot below which a level's tasks are narrowed
     int shadow_key = 2;       // shadow queue key: 2 cell2, 1 cell, 16 / 18 / 21 light | Morton bits
     double walk_linear = 1.0; // shadow walks: linear hierarchy scan from h(D) >= this x scene radius (0: off)
     int walk_first = 1;       // cell keys: the shadow rays that walk the hierarchy sort first (0: last)

@@ -424,8 +424,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TRACE_WAVES
     const uint32_t pf_stride = gridDim.x * (blockDim.x >> 6) * W;
     uint32_t pf_slot = 0;
     bool pf_have = false;
+#if RT_TASK_CLOCK
+    // tools/trace_tail.py: each task's wall time (from this iteration's start to the next's),
+    // the mean distance of its origins from the scene ball's centre (scene radii), its lanes
+    uint32_t* tclk = level < 16u ? rt_trace_clock + level * (4u + 4u * RT_TRACE_CLOCK_TASKS) : nullptr;
+    if (tclk && blockIdx.x == 0 && threadIdx.x == 0) {
+        tclk[0] = count;
+        tclk[1] = gridDim.x * (blockDim.x >> 6);
+        tclk[2] = W;
+    }
+    uint64_t tc_prev = wall_clock64();
+    uint32_t tc_task = 0xFFFFFFFFu, tc_lanes = 0;
+    float tc_dmean = 0.f;
+#endif
     for (uint32_t it = 0;; ++it) {
         const uint32_t base = sched_base(P, &P.levels[RT_WORK_WORD(level)], count, it, W);
+#if RT_TASK_CLOCK
+        {
+            const uint64_t now = wall_clock64();
+            if (tclk && tc_task < RT_TRACE_CLOCK_TASKS && lane == 0) {
+                uint32_t* rec = tclk + 4u + 4u * tc_task;
+                rec[0] = (uint32_t)(now - tc_prev);
+                rec[1] = __float_as_uint(tc_dmean);
+                rec[2] = tc_lanes;
+                rec[3] = it;
+            }
+            tc_prev = now;
+            tc_task = base < count ? base / W : 0xFFFFFFFFu;
+        }
+#endif
         if (base >= count) {
             if (P.sched == 2 && base != 0xFFFFFFFFu) continue;  // a block's tail past the queue end
             break;
@@ -486,6 +513,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TRACE_WAVES
                 }
             }
         }
+#if RT_TASK_CLOCK
+        {
+            const float dx = ro.x - S.bvh_cx, dy = ro.y - S.bvh_cy, dz = ro.z - S.bvh_cz;
+            float dd = active ? sqrtf(dx * dx + dy * dy + dz * dz) / S.bvh_r : 0.f;
+            for (int o = 32; o > 0; o >>= 1) dd += __shfl_xor(dd, o);
+            tc_lanes = (uint32_t)__builtin_popcountll(__ballot(active)) | ((in_shape ? 1u : 0u) << 16);
+            tc_dmean = dd / (float)max(tc_lanes & 0xFFFFu, 1u);
+        }
+#endif
         bool want_refl = false, want_refr = false, hit = false;
         bool refl_in = false, refr_in = false;  // the child starts inside the hit sphere / cube
         uint32_t hit_flags = 0;  // node_flags of a hit, F_HAS_R / F_HAS_T added once queued
@@ -906,7 +942,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SHADOW_WAVE
         uint32_t t = base + lane;
         uint32_t e = t < count ? shadow_raw(P, t) : 0u;
         float4 q = t < count ? P.node_ps[shadow_node(P, e)] : make_float4(0.f, 0.f, 0.f, 0.f);
-#if RT_SHADOW_CLOCK
+#if RT_TASK_CLOCK
         // tools/shadow_tail.py: wall clock (100 MHz) of every 64-entry task of the queue, and the
         // distance of its origins from the scene ball's centre in scene radii (mean, max)
         if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -921,7 +957,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SHADOW_WAVE
             bool lit = false;
             uint32_t n = 0, li = 0;
             if (t < count) shadow_unpack(P, e, n, li);
-#if RT_SHADOW_CLOCK
+#if RT_TASK_CLOCK
             const float q0x = q.x, q0y = q.y, q0z = q.z;
 #endif
             if (t < count) {
@@ -940,7 +976,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SHADOW_WAVE
             }
             q = tn < count ? P.node_ps[shadow_node(P, en)] : make_float4(0.f, 0.f, 0.f, 0.f);
             if (lit) atomicOr(lit_word(P, n, li), 1u << (li & 31u));
-#if RT_SHADOW_CLOCK
+#if RT_TASK_CLOCK
             {
                 const uint64_t tc1 = wall_clock64();
                 const uint32_t task = base / 64u;
@@ -1371,13 +1407,18 @@ hipError_t launch_wave_combine(const WaveParams& p, uint32_t level, int blocks, 
 
 }  // namespace rtdev
 
-#if RT_SHADOW_CLOCK
-// tools/shadow_tail.py (build: tools/build_variant.sh clock -DRT_SHADOW_CLOCK=1): the shadow kernel's task clock of the last pass (entries, waves of the
+#if RT_TASK_CLOCK
+// tools/shadow_tail.py (build: tools/build_variant.sh clock -DRT_TASK_CLOCK=1): the shadow kernel's task clock of the last pass (entries, waves of the
 // grid, then per 64-entry task: 10-ns ticks, mean and max origin distance / scene radius,
 // lanes | light << 8)
 extern "C" int rt_debug_shadow_clock(uint32_t* out, uint32_t words) {
     if (words > RT_SHADOW_CLOCK_WORDS) words = RT_SHADOW_CLOCK_WORDS;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(rtdev::rt_shadow_clock), words * sizeof(uint32_t)) != hipSuccess;
+}
+// tools/trace_tail.py: the trace kernels' task clocks of the last pass, per level (rt_scan.hpp)
+extern "C" int rt_debug_trace_clock(uint32_t* out, uint32_t words) {
+    if (words > RT_TRACE_CLOCK_WORDS) words = RT_TRACE_CLOCK_WORDS;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(rtdev::rt_trace_clock), words * sizeof(uint32_t)) != hipSuccess;
 }
 #endif
 #if RT_DIAG

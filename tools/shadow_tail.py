@@ -1,4 +1,4 @@
-"""Where the shadow kernel's time goes, per 64-entry task (a task-clock build, RT_SHADOW_CLOCK).
+"""Where the shadow kernel's time goes, per 64-entry task (a task-clock build, RT_TASK_CLOCK).
 
 Renders one rank's share of config 3 (rt_render_bands_async, block-cyclic 8-row bands) and
 reads the shadow kernel's task clock of that pass: per task its wall time, the mean and
@@ -6,7 +6,7 @@ largest distance of its origins from the scene ball's centre (in scene radii) an
 first lane's light.  A wave of the persistent grid takes tasks w, w + G, w + 2G, ..., so the
 kernel lasts at least as long as its slowest wave's tasks together.
 usage: RT_LIB=rust_tracer_amd/librt_hip_clock.so python tools/shadow_tail.py [world ...]
-       (default worlds 1 8; build: tools/build_variant.sh clock -DRT_SHADOW_CLOCK=1)"""
+       (default worlds 1 8; build: tools/build_variant.sh clock -DRT_TASK_CLOCK=1)"""
 import ctypes as C
 import os
 import sys
