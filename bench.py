@@ -698,6 +698,8 @@ def main():
     # render pipeline's time per frame at steady state; one frame's own span beside it
     kernel_ms = ev[0].elapsed_time(ev[1]) / args.steps
     latency_ms = sum(a.elapsed_time(b) for a, b in lat) / max(1, len(lat))  # one pass of `batch` frames
+    # each pass's (start, end) in ms from the timed region's start: how the passes overlap
+    pass_spans = [[round(ev[0].elapsed_time(a), 3), round(ev[0].elapsed_time(b), 3)] for a, b in lat]
     cnt = pipe.counters.double()
     local_scans = float(cnt[0] + cnt[1]) / args.steps   # this rank's launch (for the roofline)
     red_dev = dev if args.backend == "nccl" else torch.device("cpu")
@@ -875,6 +877,7 @@ def main():
                            else "K renders of Camera::new (the reference's bench -n loop, main.rs:137-140)"),
                 "frames_in_flight": groups * batch, "passes_in_flight": inflight,
                 "frames_per_pass": batch, "sub_bands": sub, "pass_latency_ms": round(latency_ms, 4),
+                "pass_spans_ms": pass_spans,
                 "output": args.output,
                 "msamples_per_s": round(args.width * args.height * args.spp * steps / elapsed / 1e6, 3),
                 "parallelism": f"row-bands x{world}" + (f" (x{sub} band shares per device)" if sub > 1 else "") + ((" + RCCL gather" if args.backend == "nccl"
