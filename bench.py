@@ -110,6 +110,9 @@ def parse():
     p.add_argument("--seam-stats", type=int, default=1,
                    help="N = 1: also time one frame at a time, rt_render with its host copy, the scene "
                         "build, and the depth-9 reading of 'primary+8 bounces' (untimed extras)")
+    p.add_argument("--grid-share", type=int, default=None,
+                   help="%% of the chip each pass's persistent trace grids take with passes in flight "
+                        "(FramePipeline grid_share; default 50 for band-share groups, 75 otherwise)")
     p.add_argument("--forest", type=int, default=1,
                    help="N = 1, spp 1: also time the ray-forest path at the benchmark size (seam.forest: "
                         "rt_forest_create, render_forest, render_forest_filter after a one-shape edit)")
@@ -622,7 +625,7 @@ def main():
     pipe = FramePipeline(scene, desc, args.width, args.height, args.depth, args.band_rows, rank, world, dev,
                          spp=args.spp, seed=args.seed, inflight=inflight, batch=args.batch,
                          rgb8=args.output == "rgb8", force_gather=bool(args.force_gather), sub_bands=sub,
-                         emulate=emulate)
+                         emulate=emulate, grid_share=args.grid_share)
     batch = pipe.batch
     tilers = pipe.tilers
     tiler = tilers[0]
