@@ -72,6 +72,7 @@ def stress_scene(seed, scale, near_lights, slivers):
     else:
         d.point_light((0.5 * s, 4.0 * s, -1.0 * s), (0.5, 0.5, 0.5))
     d.set_ambient((0.1, 0.1, 0.1))
+    d.stress_spheres = spheres  # (centre, radius) of the axis-aligned ones' balls
     return d
 
 
@@ -222,3 +223,43 @@ def test_shadow_queue_order_changes_nothing(key, monkeypatch):
     img, cnt, _, _ = s.render(320, 180, 8)
     s.close()
     assert same_bits(img, ref) and cnt == rcnt
+
+
+def _lights_at_the_edges(seed, scale):
+    """A stress scene plus point lights placed around the light buffers' absolute constants
+    (DESIGN.md §4.3): at 0.5 - 3 x rho = 0.05 from a sphere's surface (no buffer below rho,
+    the nearest records in the all-cell leaves above it), and at 0.8 - 1.3 x the tiers' reach
+    Lambda = 45 * 2^t from the scene (the tier boundaries)."""
+    d = stress_scene(seed, scale, False, seed % 2 == 0)
+    rng = np.random.default_rng(1000 + seed)
+    for k in range(3):
+        c, r = d.stress_spheres[int(rng.integers(0, 140))]
+        u = rng.normal(size=3)
+        u /= np.linalg.norm(u)
+        gap = float(rng.uniform(0.5, 3.0)) * 0.05
+        d.point_light(tuple(c + u * (r * 1.01 + gap)), (0.3, 0.3, 0.3))
+    for t in range(2):
+        u = rng.normal(size=3)
+        u[1] = abs(u[1])
+        u /= np.linalg.norm(u)
+        reach = 45.0 * 2 ** int(rng.integers(0, 4)) * float(rng.uniform(0.8, 1.3))
+        d.point_light(tuple(u * reach), (0.4, 0.4, 0.4))
+    return d
+
+
+@pytest.mark.parametrize("seed,scale", [(40, 1.0), (41, 1.0), (42, 0.1), (43, 0.1), (44, 10.0), (45, 3.0)])
+def test_light_buffers_at_their_constants(seed, scale):
+    """Lights near the light buffers' absolute constants (rho = 0.05 from a primitive; the
+    tiers' reach 45 * 2^t): frames and counters identical with the light buffers (default),
+    without them (lb_res=0: every shadow ray walks the hierarchy) and with the linear scan
+    (bvh=0: every shape tested for every ray, the reference's Scene::intersect)."""
+    desc = _lights_at_the_edges(seed, scale)
+    w, h, depth = 160, 120, 6
+    cam = stress_camera(w, h, scale, "std")
+    out = []
+    for tune in (None, "lb_res=0", "bvh=0"):
+        s = DeviceScene(desc, device=0, tuning=tune)
+        out.append(s.render(w, h, depth, cam=cam)[:2])
+        s.close()
+    for img, cnt in out[1:]:
+        assert same_bits(img, out[0][0]) and cnt == out[0][1]
