@@ -28,8 +28,12 @@
 
 namespace rtdev {
 
+// Keys per thread of a tile (a tile = 256 x RT_SORT_ITEMS keys).  Round 6, K = 20 on three
+// boxes, 12 against 16: +1.8 / +0.7 / -0.3%, K = 64 +2.1%; 8 / 10 / 14 / 20: -1.9 / -1.1 /
+// +0.4 / -3% (profiles/r6ab/r6ax_sort_items.log; rounds 2-3 had measured 8 / 24 / 32 against
+// 16 at smaller passes).  (A build flag, not a tuning key: the tile size shapes the kernels.)
 #ifndef RT_SORT_ITEMS
-#define RT_SORT_ITEMS 16
+#define RT_SORT_ITEMS 12
 #endif
 constexpr uint32_t SORT_THREADS = 256, SORT_ITEMS = RT_SORT_ITEMS, SORT_TILE = SORT_THREADS * SORT_ITEMS;
 constexpr uint32_t SORT_MAX_DIGIT_BITS = 11, SORT_MAX_DIGITS = 1u << SORT_MAX_DIGIT_BITS;
