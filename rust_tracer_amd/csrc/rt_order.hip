@@ -13,7 +13,7 @@
 // counters, so a whole frame is enqueued without a host round trip, and uses no global
 // atomics.  Passes of 8- to 11-bit digits, as few as the key needs (2 for keys of up to
 // 22 bits), each reduce-then-scan:
-//   count    per 4096-key tile, a digit histogram in LDS -> tile_counts[digit][tile]
+//   count    per tile (256 x RT_SORT_ITEMS keys), a digit histogram in LDS -> tile_counts[digit][tile]
 //   scan     per digit, exclusive scan over its tiles (one block per digit) + digit total
 //   scatter  per tile, stable block rank (rocprim::block_radix_rank, wave "match"
 //            algorithm: keys warp-striped, ranks ordered by (wave, item, lane) = index
